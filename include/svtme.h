@@ -1,0 +1,306 @@
+/*
+ * svtme.h — C ABI of the MI355X-native open-loop motion-estimation (ME) stage.
+ *
+ * Two surfaces, both plain C (pointers + sizes, no torch types):
+ *
+ *  1. Per-kernel rtcd variants (`*_hip`). Byte-identical signatures to the
+ *     reference's run-time-dispatch pointers so an encoder can register them
+ *     as a new variant after `svt_aom_setup_rtcd_internal`.
+ *     They take caller-owned HOST memory, run synchronously on the GPU and
+ *     return through the same out-params. They exist for drop-in registration
+ *     and per-kernel parity; one call is far below a GPU launch in size.
+ *
+ *  2. The picture-level job API (`svtme_*`). This is the performance boundary:
+ *     it replaces the per-SB loop of the ME thread
+ *     (reference Source/Lib/Codec/me_process.c:174-290) with one GPU job that
+ *     covers every 64x64 superblock (SB) x every reference of one picture.
+ *     Pictures are uploaded once; their padded full / quarter / sixteenth
+ *     pyramids stay resident in HBM, keyed by picture_number, until released.
+ *
+ * No entry point falls back to a CPU path. A HIP failure is reported through
+ * the returned status (job API) or svtme_last_error() (rtcd variants), and a
+ * message on stderr.
+ */
+#ifndef SVTME_H
+#define SVTME_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------
+ * Constants (reference values cited)
+ * ------------------------------------------------------------------------- */
+#define SVTME_PU_COUNT 85           /* SQUARE_PU_COUNT, me_sb_results.h:24 */
+#define SVTME_MAX_LISTS 2           /* MAX_NUM_OF_REF_PIC_LIST, definitions.h:2337 */
+#define SVTME_MAX_REFS 4            /* REF_LIST_MAX_DEPTH, EbSvtAv1Enc.h:36 */
+#define SVTME_MAX_PA_ME_CAND 23     /* MAX_PA_ME_CAND, me_sb_results.h:22 */
+#define SVTME_MAX_PA_ME_MV 7        /* MAX_PA_ME_MV, me_sb_results.h:21 */
+#define SVTME_MAX_SAD_VALUE (128u * 128u * 255u) /* motion_estimation.h:85 */
+#define SVTME_SUB_SAD_SEARCH 0      /* definitions.h:2071 */
+#define SVTME_FULL_SAD_SEARCH 1     /* definitions.h:2072 */
+#define SVTME_PAD_FULL 72           /* PA full-res padding (enc_handle.c:4057-4069) */
+#define SVTME_PAD_QUARTER 32        /* b64_size >> 1, reference_object.c:272 */
+#define SVTME_PAD_SIXTEENTH 16      /* b64_size >> 2, reference_object.c:287 */
+
+/* Status codes: the values of EbErrorType (API/EbSvtAv1.h:121-130). */
+typedef int32_t svtme_status;
+#define SVTME_OK 0
+#define SVTME_ERR_INSUFFICIENT_RESOURCES ((int32_t)0x80001000)
+#define SVTME_ERR_UNDEFINED ((int32_t)0x80001001)
+#define SVTME_ERR_BAD_PARAMETER ((int32_t)0x80001005)
+
+/* ---------------------------------------------------------------------------
+ * Picture-level ME controls: a POD snapshot of the MeContext control fields
+ * (me_context.h:280-364, 366-509) as set per picture by svt_aom_sig_deriv_me
+ * (enc_mode_config.c:671-808). The GPU takes them as parameters; it never
+ * re-derives them from the preset.
+ * ------------------------------------------------------------------------- */
+typedef struct svtme_area {
+    uint16_t width;
+    uint16_t height;
+} svtme_area;
+
+typedef struct svtme_area_minmax {
+    svtme_area sa_min;
+    svtme_area sa_max;
+} svtme_area_minmax;
+
+typedef struct svtme_controls {
+    /* search methods: SVTME_SUB_SAD_SEARCH / SVTME_FULL_SAD_SEARCH */
+    uint8_t hme_search_method;
+    uint8_t me_search_method;
+    /* HME enables (me_context.h:409-412) */
+    uint8_t enable_hme_flag;
+    uint8_t enable_hme_level0_flag;
+    uint8_t enable_hme_level1_flag;
+    uint8_t enable_hme_level2_flag;
+    /* number of HME-L0 search regions; only 2x2 is supported (motion_estimation.c:1875) */
+    uint8_t num_hme_sa_w;
+    uint8_t num_hme_sa_h;
+    /* search areas (MeHmeSearchAreaCtrls, me_context.h:342-347 / 421-429) */
+    svtme_area_minmax hme_l0_sa;
+    svtme_area hme_l1_sa;
+    svtme_area hme_l2_sa;
+    svtme_area_minmax me_sa;
+    /* MeHmeRefPruneCtrls (me_context.h:280-290) */
+    uint8_t enable_me_hme_ref_pruning;
+    uint8_t pad0;
+    uint16_t prune_ref_if_hme_sad_dev_bigger_than_th;
+    uint16_t prune_ref_if_me_sad_dev_bigger_than_th;
+    uint16_t zz_sad_pct;
+    uint32_t zz_sad_th;
+    uint32_t phme_sad_th;
+    uint16_t phme_sad_pct;
+    /* MeSrCtrls (me_context.h:292-305) */
+    uint8_t enable_me_sr_adjustment;
+    uint8_t distance_based_hme_resizing;
+    uint16_t reduce_me_sr_based_on_mv_length_th;
+    uint16_t stationary_hme_sad_abs_th;
+    uint16_t stationary_me_sr_divisor;
+    uint16_t reduce_me_sr_based_on_hme_sad_abs_th;
+    uint16_t me_sr_divisor_for_low_hme_sad;
+    /* MvBasedSearchAdj (me_context.h:356-364) */
+    uint8_t mv_sa_adj_enabled;
+    uint8_t mv_sa_adj_nearest_ref_only;
+    uint16_t mv_sa_adj_mv_size_th;
+    uint16_t mv_sa_adj_sa_multiplier;
+    /* Me8x8VarCtrls (me_context.h:310-319) */
+    uint8_t me_8x8_var_enabled;
+    uint8_t pad1;
+    uint32_t me_sr_div4_th;
+    uint32_t me_sr_div2_th;
+    uint32_t me_sr_mult2_th;
+    /* PreHmeCtrls (me_context.h:336-341) */
+    uint8_t prehme_enable;
+    uint8_t prehme_skip_search_line;
+    uint8_t prehme_l1_early_exit;
+    uint8_t pad2;
+    svtme_area_minmax prehme_sa_cfg[2];
+    /* misc (me_context.h:490-508) */
+    int32_t prune_me_candidates_th;
+    uint8_t use_best_unipred_cand_only;
+    uint8_t reduce_hme_l0_sr_th_min;
+    uint8_t reduce_hme_l0_sr_th_max;
+    uint8_t pad3;
+    uint32_t me_early_exit_th;
+    uint32_t me_safe_limit_zz_th;
+    uint32_t prev_me_stage_based_exit_th;
+} svtme_controls;
+
+/* ---------------------------------------------------------------------------
+ * One picture's ME job (the fields the reference reads from
+ * PictureParentControlSet / SequenceControlSet / MeContext per picture).
+ * ------------------------------------------------------------------------- */
+typedef struct svtme_job {
+    uint64_t picture_number;
+    uint32_t width;   /* luma width of the PA picture, multiple of 8 (aligned_width) */
+    uint32_t height;  /* luma height, multiple of 8 (aligned_height) */
+    uint64_t ref_picture_number[SVTME_MAX_LISTS][SVTME_MAX_REFS];
+    uint8_t num_lists;                 /* 1 = P slice, 2 = B slice (me_process.c:219-221) */
+    uint8_t num_refs[SVTME_MAX_LISTS]; /* ref_list{0,1}_count_try (me_process.c:223-225) */
+    uint8_t temporal_layer_index;
+    uint8_t is_ref;
+    uint8_t hierarchical_levels;
+    uint8_t similar_brightness_refs;
+    /* candidate construction (motion_estimation.c:2532-2835) */
+    uint8_t enable_me_8x8;
+    uint8_t enable_me_16x16;
+    uint8_t max_cand;   /* pa_me_data->max_cand (pcs.c:91-96) */
+    uint8_t max_refs;   /* pa_me_data->max_refs */
+    uint8_t max_l0;     /* pa_me_data->max_l0 */
+    uint8_t only_l_bwd; /* scs->mrp_ctrls.only_l_bwd */
+    uint8_t input_resolution; /* EbInputResolution: 0=240p .. 6=8K (definitions.h:2079-2085) */
+    uint8_t gm_enabled;       /* pcs->gm_ctrls.enabled */
+    uint8_t gm_use_distance_based_active_th;
+    uint8_t pad[3];
+    /* SB range [sb_begin, sb_begin + sb_count) in raster b64 order; sb_count 0 = all */
+    uint32_t sb_begin;
+    uint32_t sb_count;
+    svtme_controls ctrl;
+} svtme_job;
+
+/* ---------------------------------------------------------------------------
+ * Outputs.
+ * ------------------------------------------------------------------------- */
+/* Per SB x per searched (list, ref) slot; slots ordered list 0 refs then list 1
+ * refs, R = num_refs[0] + (num_lists == 2 ? num_refs[1] : 0) slots per SB. */
+typedef struct svtme_ref_record {
+    uint32_t best_sad[SVTME_PU_COUNT]; /* p_sb_best_sad[l][r][] Z-order PUs; 0xFFFFFFFF if !searched */
+    uint32_t best_mv[SVTME_PU_COUNT];  /* p_sb_best_mv[l][r][]: (uint32)(y<<16)|(uint16)x, full-pel */
+    uint64_t hme_sad;    /* final search_results[l][r].hme_sad (HME SAD, or me_prune_ref's 8x8 sum) */
+    int16_t hme_sc_x;    /* HME search centre (full-pel), search_results[l][r].hme_sc_{x,y} */
+    int16_t hme_sc_y;
+    uint32_t zz_sad;     /* zz_sad[l][r] (0xFFFFFFFF if not computed) */
+    uint8_t searched;    /* do_ref when the integer search ran */
+    uint8_t do_ref;      /* final do_ref */
+    uint8_t pad[6];
+} svtme_ref_record; /* 704 bytes */
+
+/* Per SB candidate list + distortions (MeSbResults, me_sb_results.h:44, and the
+ * per-SB pcs arrays written by compute_distortion, motion_estimation.c:2964). */
+typedef struct svtme_sb_result {
+    uint8_t total_me_candidate_index[SVTME_PU_COUNT];
+    uint8_t pad0[3];
+    /* MeCandidate bit-field byte: direction | ref_idx_l0<<2 | ref_idx_l1<<4 |
+     * ref0_list<<6 | ref1_list<<7 ; indexed [pu_index][cand] */
+    uint8_t me_candidate_array[SVTME_PU_COUNT][SVTME_MAX_PA_ME_CAND];
+    uint8_t pad1[1];
+    uint32_t me_mv_array[SVTME_PU_COUNT][SVTME_MAX_PA_ME_MV]; /* [pu_index][max_refs slot] */
+    uint32_t me_distortion[SVTME_PU_COUNT];
+    uint32_t me_8x8_cost_variance;
+    uint32_t rc_me_distortion;
+    uint32_t me_64x64_distortion;
+    uint32_t me_32x32_distortion;
+    uint32_t me_16x16_distortion;
+    uint32_t me_8x8_distortion;
+    uint8_t stationary_block_present;
+    uint8_t rc_me_allow_gm;
+    uint8_t pad2[6];
+} svtme_sb_result;
+
+/* ---------------------------------------------------------------------------
+ * Picture-level job API (the performance boundary)
+ * ------------------------------------------------------------------------- */
+typedef struct svtme_ctx svtme_ctx;
+
+/* Create a context on HIP device `device`. Sizes the plane cache lazily. */
+svtme_status svtme_ctx_create(int device, svtme_ctx **out);
+void svtme_ctx_destroy(svtme_ctx *ctx);
+
+/* Upload one 8-bit luma picture (host memory, `stride` bytes per row,
+ * width x height visible samples; width/height need not be multiples of 8:
+ * the right/bottom are replicated to the next multiple of 8 as
+ * svt_aom_pad_picture_to_multiple_of_min_blk_size_dimensions does). Builds the
+ * padded full (pad 72), quarter (pad 32) and sixteenth (pad 16) planes on the
+ * GPU (svt_aom_downsample_filtering_input_picture, pic_analysis_process.c:1945). */
+svtme_status svtme_picture_upload(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *y,
+                                  uint32_t stride, uint32_t width, uint32_t height);
+/* Same, for a 10-bit picture in uint16 samples (stride in samples): the
+ * searched plane is the 8-bit MSB plane p >> 2 (enc_handle.c:4964-4972). */
+svtme_status svtme_picture_upload_10bit(svtme_ctx *ctx, uint64_t picture_number, const uint16_t *y,
+                                        uint32_t stride, uint32_t width, uint32_t height);
+/* Same, from a DEVICE pointer already in HBM (no PCIe). */
+svtme_status svtme_picture_upload_device(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *d_y,
+                                         uint32_t stride, uint32_t width, uint32_t height);
+svtme_status svtme_picture_release(svtme_ctx *ctx, uint64_t picture_number);
+/* Copy a resident pyramid level back to host (level 0 = full, 1 = quarter,
+ * 2 = sixteenth), padding included: dst gets (h + 2 pad) rows of `stride` bytes. */
+svtme_status svtme_picture_download(svtme_ctx *ctx, uint64_t picture_number, int level, uint8_t *dst,
+                                    uint32_t *stride, uint32_t *width, uint32_t *height, uint32_t *pad);
+
+/* Run ME for one picture. `ref_records` receives sb_count x R records and
+ * `sb_results` (may be NULL) sb_count results, in host memory. Synchronous. */
+svtme_status svtme_submit_picture(svtme_ctx *ctx, const svtme_job *job, svtme_ref_record *ref_records,
+                                  svtme_sb_result *sb_results);
+
+/* Asynchronous variant for pipelining / benchmarking: records stay in device
+ * memory owned by ctx; svtme_sync waits, svtme_fetch copies them out. */
+svtme_status svtme_submit_picture_async(svtme_ctx *ctx, const svtme_job *job);
+svtme_status svtme_sync(svtme_ctx *ctx);
+svtme_status svtme_fetch(svtme_ctx *ctx, svtme_ref_record *ref_records, svtme_sb_result *sb_results);
+/* Device pointer of the last job's record buffer (for RCCL all-gather). */
+void *svtme_device_records(svtme_ctx *ctx, uint64_t *bytes);
+/* The HIP stream (hipStream_t) the context launches on, for event timing. */
+void *svtme_stream(svtme_ctx *ctx);
+
+/* Number of 64x64 SBs of a width x height picture, and R for a job. */
+uint32_t svtme_sb_total(uint32_t width, uint32_t height);
+uint32_t svtme_job_ref_slots(const svtme_job *job);
+
+/* Last error message of this thread (empty string if none). */
+const char *svtme_last_error(void);
+
+/* Fill `ctrl` as svt_aom_sig_deriv_me does for the non-RTC, non-screen-content
+ * path (enc_mode_config.c:671-808) for preset `enc_mode`, qp and resolution. */
+void svtme_derive_controls(int enc_mode, int qp, int input_resolution, int temporal_layer_index,
+                           int hierarchical_levels, int frame_rate_q16, svtme_controls *ctrl);
+
+/* ---------------------------------------------------------------------------
+ * Per-kernel rtcd variants. Signatures identical to the pointers declared in
+ * the reference's Source/Lib/Codec/aom_dsp_rtcd.h (line cited per entry).
+ * ------------------------------------------------------------------------- */
+/* aom_dsp_rtcd.h:779 svt_sad_loop_kernel */
+void svt_sad_loop_kernel_hip(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                             uint32_t block_height, uint32_t block_width, uint64_t *best_sad,
+                             int16_t *x_search_center, int16_t *y_search_center, uint32_t src_stride_raw,
+                             uint8_t skip_search_line, int16_t search_area_width, int16_t search_area_height);
+/* aom_dsp_rtcd.h:856 svt_nxm_sad_kernel */
+uint32_t svt_nxm_sad_kernel_hip(const uint8_t *src, uint32_t src_stride, const uint8_t *ref, uint32_t ref_stride,
+                                uint32_t height, uint32_t width);
+/* aom_dsp_rtcd.h:842 svt_ext_sad_calculation_8x8_16x16 */
+void svt_ext_sad_calculation_8x8_16x16_hip(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                                           uint32_t *p_best_sad_8x8, uint32_t *p_best_sad_16x16,
+                                           uint32_t *p_best_mv8x8, uint32_t *p_best_mv16x16, uint32_t mv,
+                                           uint32_t *p_sad16x16, uint32_t *p_sad8x8, bool sub_sad);
+/* aom_dsp_rtcd.h:848 svt_ext_sad_calculation_32x32_64x64 */
+void svt_ext_sad_calculation_32x32_64x64_hip(uint32_t *p_sad16x16, uint32_t *p_best_sad_32x32,
+                                             uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
+                                             uint32_t *p_best_mv64x64, uint32_t mv, uint32_t *p_sad32x32);
+/* aom_dsp_rtcd.h:853 svt_ext_all_sad_calculation_8x8_16x16 */
+void svt_ext_all_sad_calculation_8x8_16x16_hip(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                                               uint32_t mv, uint32_t *p_best_sad_8x8, uint32_t *p_best_sad_16x16,
+                                               uint32_t *p_best_mv8x8, uint32_t *p_best_mv16x16,
+                                               uint32_t p_eight_sad16x16[16][8], uint32_t p_eight_sad8x8[64][8],
+                                               bool sub_sad);
+/* aom_dsp_rtcd.h:854 svt_ext_eight_sad_calculation_32x32_64x64 */
+void svt_ext_eight_sad_calculation_32x32_64x64_hip(uint32_t p_sad16x16[16][8], uint32_t *p_best_sad_32x32,
+                                                   uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
+                                                   uint32_t *p_best_mv64x64, uint32_t mv, uint32_t p_sad32x32[4][8]);
+/* aom_dsp_rtcd.h:855 svt_initialize_buffer_32bits */
+void svt_initialize_buffer_32bits_hip(uint32_t *pointer, uint32_t count128, uint32_t count32, uint32_t value);
+/* aom_dsp_rtcd.h:841 downsample_2d */
+void svt_aom_downsample_2d_hip(uint8_t *input_samples, uint32_t input_stride, uint32_t input_area_width,
+                               uint32_t input_area_height, uint8_t *decim_samples, uint32_t decim_stride,
+                               uint32_t decim_step);
+/* aom_dsp_rtcd.h:863 sad_16b_kernel (mode-decision consumer; not on the ME path) */
+uint32_t svt_aom_sad_16b_kernel_hip(uint16_t *src, uint32_t src_stride, uint16_t *ref, uint32_t ref_stride,
+                                    uint32_t height, uint32_t width);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVTME_H */
