@@ -1,0 +1,60 @@
+// svtme_device.h — device-side layouts shared by the HIP kernels and the host
+// launcher (svtme_host.cpp). gfx950 (MI355X) only.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/svtme.h"
+
+// Device plane margins. The LOGICAL padding the search clamps use is the
+// reference's (72 / 32 / 16, reference_object.c:243-305); the device margins
+// are at least as wide and keep each interior row start 16-byte aligned and
+// 8 bytes of slack on the right for aligned dword loads. Margins hold the same
+// edge-replicated samples as the reference's padding.
+#define SVTME_DEV_FULL_LEFT 80
+#define SVTME_DEV_FULL_TOP 72
+#define SVTME_DEV_Q_LEFT 32
+#define SVTME_DEV_Q_TOP 32
+#define SVTME_DEV_S_LEFT 16
+#define SVTME_DEV_S_TOP 16
+
+struct DevPlane {
+    uint8_t *base;   // interior sample (0, 0); negative offsets reach the padding
+    int32_t stride;  // bytes per row (multiple of 64)
+    int32_t width;   // interior width
+    int32_t height;  // interior height
+    int32_t pad;     // logical padding (org_x == org_y of the reference plane)
+};
+
+struct DevPyramid {
+    DevPlane lv[3];  // 0 = full, 1 = quarter, 2 = sixteenth
+};
+
+// Parameters of one picture job as the kernel sees them.
+struct DevJob {
+    svtme_job job;                 // controls + picture description (host copy)
+    DevPyramid cur;
+    DevPyramid ref[2][4];
+    svtme_ref_record *out_records; // [sb_count][R]
+    svtme_sb_result *out_sb;       // [sb_count] or nullptr
+    uint32_t R;
+    uint32_t pic_w_b64;
+};
+
+static inline uint32_t svtme_round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }
+static inline uint32_t svtme_align8_u(uint32_t v) { return (v + 7u) & ~7u; }
+
+// plane geometry for an aligned W x H picture
+static inline void svtme_plane_geometry(int level, uint32_t W, uint32_t H, uint32_t *w, uint32_t *h, uint32_t *left,
+                                        uint32_t *top, uint32_t *stride, uint32_t *rows, uint32_t *pad) {
+    if (level == 0) {
+        *w = W, *h = H, *left = SVTME_DEV_FULL_LEFT, *top = SVTME_DEV_FULL_TOP, *pad = SVTME_PAD_FULL;
+        *stride = svtme_round_up(W + SVTME_DEV_FULL_LEFT + 88, 64);
+    } else if (level == 1) {
+        *w = W / 2, *h = H / 2, *left = SVTME_DEV_Q_LEFT, *top = SVTME_DEV_Q_TOP, *pad = SVTME_PAD_QUARTER;
+        *stride = svtme_round_up(W / 2 + SVTME_DEV_Q_LEFT + 40, 64);
+    } else {
+        *w = W / 4, *h = H / 4, *left = SVTME_DEV_S_LEFT, *top = SVTME_DEV_S_TOP, *pad = SVTME_PAD_SIXTEENTH;
+        *stride = svtme_round_up(W / 4 + SVTME_DEV_S_LEFT + 24, 64);
+    }
+    *rows = *h + 2 * *top;
+}

@@ -1,0 +1,125 @@
+"""GPU parity: the HIP picture job (libsvtme.so) vs the CPU oracle, bit-exact.
+
+The oracle is itself pinned to the reference (tests/test_oracle_vs_ref.py and
+tests/golden/). Cases mirror the reference's orchestration shapes: base and
+non-base layers, 1..4 refs per list, P and B pictures, partial SBs at the
+right/bottom edges, presets 4/6/8/12 (check_00_center, HME-L2, pre-HME with
+line skipping, 8x8-variance resize), flat/saturated/noise content for ties.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def content(kind, w, h, ts, S):
+    if kind == "pan":
+        syn = S.Synth(w, h)
+        return {t: syn.frame(t) for t in ts}
+    rng = np.random.default_rng(1234)
+    if kind == "noise":
+        return {t: rng.integers(0, 256, (h, w), dtype=np.uint8) for t in ts}
+    if kind == "flat":
+        return {t: np.full((h, w), 128, np.uint8) for t in ts}
+    if kind == "sat":
+        return {t: (rng.integers(0, 2, (h, w)) * 255).astype(np.uint8) for t in ts}
+    if kind == "stripes":
+        base = ((np.arange(w)[None, :] // 4 + np.arange(h)[:, None] // 8) % 2 * 200).astype(np.uint8)
+        return {t: np.roll(base, t, axis=1) for t in ts}
+    raise ValueError(kind)
+
+
+def run_case(S, gpu, kind, w, h, mode, tl, l0, l1, cur=8, gm=False, is_ref=True, e8=None, sb_begin=0, sb_count=0):
+    frames = content(kind, w, h, sorted(set([cur] + list(l0) + list(l1))), S)
+    res = S.input_resolution_of(w, h)
+    ctrl = S.derive_controls(mode, 35, res, tl)
+    job = S.make_job(w, h, ctrl, cur, l0, l1, temporal_layer_index=tl, is_ref=is_ref,
+                     enable_me_8x8=(res <= S.RES_720P) if e8 is None else e8,
+                     ref_count_used=(max(len(l0), 1), len(l1)), gm_enabled=gm, sb_begin=sb_begin, sb_count=sb_count)
+    for t, f in frames.items():
+        gpu.upload(1000 + t, f)
+    job.picture_number = 1000 + cur
+    for i, t in enumerate(l0):
+        job.ref_picture_number[0][i] = 1000 + t
+    for i, t in enumerate(l1):
+        job.ref_picture_number[1][i] = 1000 + t
+    recs, sbr = gpu.submit(job)
+    pyr = {t: S.build_host_pyramid(f, "oracle") for t, f in frames.items()}
+    refs = {}
+    for i, t in enumerate(l0):
+        refs[(0, i)] = pyr[t]
+    for i, t in enumerate(l1):
+        refs[(1, i)] = pyr[t]
+    ojob = S.make_job(w, h, ctrl, cur, l0, l1, temporal_layer_index=tl, is_ref=is_ref,
+                      enable_me_8x8=(res <= S.RES_720P) if e8 is None else e8,
+                      ref_count_used=(max(len(l0), 1), len(l1)), gm_enabled=gm, sb_begin=sb_begin,
+                      sb_count=sb_count)
+    orecs, osbr = S.run_checker(ojob, pyr[cur], refs, "oracle", nthreads=8)
+    for t in frames:
+        gpu.release(1000 + t)
+    return S.compare_records(orecs, recs, osbr, sbr)
+
+
+CASES = [
+    ("pan", 640, 360, 8, 1, (7, 6), (9, 10)),
+    ("pan", 640, 360, 8, 0, (7, 6, 5), (9, 10)),
+    ("pan", 640, 360, 12, 0, (7,), ()),
+    ("pan", 640, 360, 6, 1, (7,), (9,)),
+    ("pan", 640, 360, 4, 2, (7, 6), (9,)),
+    ("pan", 426, 240, 8, 2, (7, 6), (9,)),
+    ("pan", 1000, 562, 8, 1, (7, 6), (9, 10)),
+    ("pan", 72, 40, 8, 1, (7, 6), (9, 10)),
+    ("pan", 136, 8, 6, 1, (7,), (9,)),
+    ("pan", 640, 360, 8, 3, (7, 6, 4, 3), (9, 10, 12)),
+    ("noise", 320, 192, 8, 1, (7, 6), (9, 10)),
+    ("flat", 320, 192, 8, 1, (7, 6), (9, 10)),
+    ("flat", 320, 192, 4, 1, (7,), (9,)),
+    ("sat", 320, 192, 6, 1, (7, 6), (9,)),
+    ("stripes", 320, 192, 8, 1, (7, 6), (9, 10)),
+    ("stripes", 320, 192, 6, 0, (7, 6, 5), (9, 10)),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-{c[1]}x{c[2]}-p{c[3]}-tl{c[4]}-{len(c[5])}+{len(c[6])}")
+def test_picture_parity(svtme, gpu, case):
+    errs = run_case(svtme, gpu, *case)
+    assert not errs, errs[:5]
+
+
+def test_gm_parity(svtme, gpu):
+    assert not run_case(svtme, gpu, "pan", 640, 360, 4, 1, (7, 6), (9,), gm=True)
+    assert not run_case(svtme, gpu, "pan", 1280, 720, 8, 1, (7,), (9,), gm=True)
+
+
+def test_sb_range_parity(svtme, gpu):
+    # a shard of the picture (the multi-GPU band) must equal the same SBs of the full job
+    assert not run_case(svtme, gpu, "pan", 640, 360, 8, 1, (7, 6), (9, 10), sb_begin=17, sb_count=23)
+
+
+def test_pyramid_parity(svtme, gpu):
+    S = svtme
+    for (w, h) in ((640, 360), (1000, 562), (72, 40)):
+        f = S.Synth(w, h).frame(3)
+        gpu.upload(77, f)
+        p = S.build_host_pyramid(f, "oracle")
+        for lv, name in enumerate(("full", "quarter", "sixteenth")):
+            assert np.array_equal(gpu.download(77, lv), getattr(p, name)), (w, h, name)
+        gpu.release(77)
+
+
+def test_10bit_msb_parity(svtme, gpu):
+    S = svtme
+    w, h = 640, 360
+    syn = S.Synth(w, h)
+    f10 = {t: syn.frame10(t) for t in (7, 8, 9)}
+    for t, f in f10.items():
+        gpu.upload(2000 + t, f)
+    ctrl = S.derive_controls(6, 35, S.input_resolution_of(w, h), 1)
+    job = S.make_job(w, h, ctrl, 2008, (2007,), (2009,), temporal_layer_index=1, ref_count_used=(1, 1),
+                     enable_me_8x8=True)
+    recs, sbr = gpu.submit(job)
+    pyr = {t: S.build_host_pyramid(f, "oracle") for t, f in f10.items()}
+    orecs, osbr = S.run_checker(job, pyr[8], {(0, 0): pyr[7], (1, 0): pyr[9]}, "oracle", nthreads=8)
+    assert not S.compare_records(orecs, recs, osbr, sbr)
+    for t in f10:
+        gpu.release(2000 + t)
