@@ -242,6 +242,15 @@ svtme_status svtme_submit_picture(svtme_ctx *ctx, const svtme_job *job, svtme_re
 svtme_status svtme_submit_picture_async(svtme_ctx *ctx, const svtme_job *job);
 svtme_status svtme_sync(svtme_ctx *ctx);
 svtme_status svtme_fetch(svtme_ctx *ctx, svtme_ref_record *ref_records, svtme_sb_result *sb_results);
+/* Asynchronous variant writing into caller-provided DEVICE buffers (e.g. the
+ * slice of an all-gather tensor): sb_count x R records, and sb_count results
+ * when d_sb_results is not NULL. */
+svtme_status svtme_submit_picture_device(svtme_ctx *ctx, const svtme_job *job, svtme_ref_record *d_ref_records,
+                                         svtme_sb_result *d_sb_results);
+/* Time the per-SB ME kernel of every job with HIP events on the context's
+ * stream (enable = 1); svtme_kernel_ms returns the last job's kernel time. */
+svtme_status svtme_set_timing(svtme_ctx *ctx, int enable);
+float svtme_kernel_ms(svtme_ctx *ctx);
 /* Device pointer of the last job's record buffer (for RCCL all-gather). */
 void *svtme_device_records(svtme_ctx *ctx, uint64_t *bytes);
 /* The HIP stream (hipStream_t) the context launches on, for event timing. */

@@ -84,6 +84,8 @@ struct svtme_ctx {
     size_t sb_cap               = 0;
     uint32_t last_count = 0, last_R = 0;
     bool last_has_sb    = false;
+    bool timing         = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::mutex mu;
 };
 
@@ -126,6 +128,10 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         (void)hipFree(c->d_records);
     if (c->d_sb)
         (void)hipFree(c->d_sb);
+    if (c->ev0)
+        (void)hipEventDestroy(c->ev0);
+    if (c->ev1)
+        (void)hipEventDestroy(c->ev1);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -333,33 +339,74 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
     return SVTME_OK;
 }
 
-static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_sb) {
+static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_sb, svtme_ref_record *d_out,
+                                  svtme_sb_result *d_out_sb) {
     HIP_TRY(hipSetDevice(c->device));
     DevJob dj;
     uint32_t count;
     svtme_status st = validate_job(c, job, &dj, &count);
     if (st)
         return st;
-    if ((st = ensure_buf((void **)&c->d_records, &c->records_cap, (size_t)count * dj.R * sizeof(svtme_ref_record))))
-        return st;
-    dj.out_records = c->d_records;
-    if (with_sb) {
-        if ((st = ensure_buf((void **)&c->d_sb, &c->sb_cap, (size_t)count * sizeof(svtme_sb_result))))
+    if (d_out) {
+        dj.out_records = d_out;
+        dj.out_sb      = d_out_sb;
+    } else {
+        if ((st = ensure_buf((void **)&c->d_records, &c->records_cap,
+                             (size_t)count * dj.R * sizeof(svtme_ref_record))))
             return st;
-        dj.out_sb = c->d_sb;
+        dj.out_records = c->d_records;
+        if (with_sb) {
+            if ((st = ensure_buf((void **)&c->d_sb, &c->sb_cap, (size_t)count * sizeof(svtme_sb_result))))
+                return st;
+            dj.out_sb = c->d_sb;
+        }
     }
+    if (c->timing)
+        HIP_TRY(hipEventRecord(c->ev0, c->stream));
     HIP_TRY(svtme_launch_me(&dj, count, c->stream));
+    if (c->timing)
+        HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->last_count  = count;
     c->last_R      = dj.R;
-    c->last_has_sb = with_sb;
+    c->last_has_sb = with_sb && !d_out;
     return SVTME_OK;
+}
+
+extern "C" svtme_status svtme_submit_picture_device(svtme_ctx *c, const svtme_job *job, svtme_ref_record *d_recs,
+                                                    svtme_sb_result *d_sb) {
+    if (!c || !d_recs)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_picture_device: null ctx or output");
+    std::lock_guard<std::mutex> lk(c->mu);
+    return submit_locked(c, job, d_sb != nullptr, d_recs, d_sb);
+}
+
+extern "C" svtme_status svtme_set_timing(svtme_ctx *c, int enable) {
+    if (!c)
+        return fail(SVTME_ERR_BAD_PARAMETER, "null ctx");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    if (enable && !c->ev0) {
+        HIP_TRY(hipEventCreate(&c->ev0));
+        HIP_TRY(hipEventCreate(&c->ev1));
+    }
+    c->timing = enable != 0;
+    return SVTME_OK;
+}
+
+extern "C" float svtme_kernel_ms(svtme_ctx *c) {
+    if (!c || !c->timing)
+        return -1.0f;
+    float ms = -1.0f;
+    if (hipEventSynchronize(c->ev1) != hipSuccess || hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess)
+        return -1.0f;
+    return ms;
 }
 
 extern "C" svtme_status svtme_submit_picture_async(svtme_ctx *c, const svtme_job *job) {
     if (!c)
         return fail(SVTME_ERR_BAD_PARAMETER, "null ctx");
     std::lock_guard<std::mutex> lk(c->mu);
-    return submit_locked(c, job, true);
+    return submit_locked(c, job, true, nullptr, nullptr);
 }
 
 extern "C" svtme_status svtme_sync(svtme_ctx *c) {
@@ -394,7 +441,7 @@ extern "C" svtme_status svtme_submit_picture(svtme_ctx *c, const svtme_job *job,
         return fail(SVTME_ERR_BAD_PARAMETER, "null ctx");
     {
         std::lock_guard<std::mutex> lk(c->mu);
-        svtme_status st = submit_locked(c, job, sb != nullptr);
+        svtme_status st = submit_locked(c, job, sb != nullptr, nullptr, nullptr);
         if (st)
             return st;
     }

@@ -430,6 +430,12 @@ def load_product():
         lib.svtme_sync.restype = C.c_int32
         lib.svtme_fetch.argtypes = [vp, vp, vp]
         lib.svtme_fetch.restype = C.c_int32
+        lib.svtme_submit_picture_device.argtypes = [vp, C.POINTER(Job), vp, vp]
+        lib.svtme_submit_picture_device.restype = C.c_int32
+        lib.svtme_set_timing.argtypes = [vp, C.c_int]
+        lib.svtme_set_timing.restype = C.c_int32
+        lib.svtme_kernel_ms.argtypes = [vp]
+        lib.svtme_kernel_ms.restype = C.c_float
         lib.svtme_device_records.argtypes = [vp, C.POINTER(C.c_uint64)]
         lib.svtme_device_records.restype = vp
         lib.svtme_stream.argtypes = [vp]
@@ -507,6 +513,16 @@ class GpuME:
 
     def submit_async(self, job: Job):
         self._check(self.lib.svtme_submit_picture_async(self.ctx, C.byref(job)), "svtme_submit_picture_async")
+
+    def submit_device(self, job: Job, d_records: int, d_sb: int | None = None):
+        self._check(self.lib.svtme_submit_picture_device(self.ctx, C.byref(job), d_records, d_sb),
+                    "svtme_submit_picture_device")
+
+    def set_timing(self, enable: bool = True):
+        self._check(self.lib.svtme_set_timing(self.ctx, 1 if enable else 0), "svtme_set_timing")
+
+    def kernel_ms(self) -> float:
+        return float(self.lib.svtme_kernel_ms(self.ctx))
 
     def sync(self):
         self._check(self.lib.svtme_sync(self.ctx), "svtme_sync")
