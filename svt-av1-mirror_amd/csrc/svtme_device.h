@@ -38,6 +38,7 @@ struct DevJob {
     svtme_sb_result *out_sb;       // [sb_count] or nullptr
     uint32_t R;
     uint32_t pic_w_b64;
+    unsigned long long *stamps;    // diagnostic builds only: [sb_count][16] s_memtime
 };
 
 static inline uint32_t svtme_round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }

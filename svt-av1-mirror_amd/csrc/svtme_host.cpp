@@ -86,6 +86,12 @@ struct svtme_ctx {
     bool last_has_sb    = false;
     bool timing         = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+#ifdef SVTME_STAMPS
+    unsigned long long *d_stamps = nullptr;
+    size_t stamps_cap            = 0;
+    double stamp_sum[16]         = {0};
+    uint64_t stamp_n             = 0;
+#endif
     std::mutex mu;
 };
 
@@ -132,6 +138,18 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         (void)hipEventDestroy(c->ev0);
     if (c->ev1)
         (void)hipEventDestroy(c->ev1);
+#ifdef SVTME_STAMPS
+    if (c->stamp_n) {
+        fprintf(stderr, "[svtme stamps] %llu SBs, mean cycles per phase (from previous stamp):",
+                (unsigned long long)c->stamp_n);
+        for (int k = 1; k < 16; k++)
+            if (c->stamp_sum[k] > 0)
+                fprintf(stderr, " p%d=%.0f", k, c->stamp_sum[k] / c->stamp_n);
+        fprintf(stderr, "\n");
+    }
+    if (c->d_stamps)
+        (void)hipFree(c->d_stamps);
+#endif
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -361,9 +379,33 @@ static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_
             dj.out_sb = c->d_sb;
         }
     }
+#ifdef SVTME_STAMPS
+    if ((st = ensure_buf((void **)&c->d_stamps, &c->stamps_cap, (size_t)count * 16 * 8)))
+        return st;
+    HIP_TRY(hipMemsetAsync(c->d_stamps, 0, (size_t)count * 16 * 8, c->stream));
+    dj.stamps = c->d_stamps;
+#endif
     if (c->timing)
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
     HIP_TRY(svtme_launch_me(&dj, count, c->stream));
+#ifdef SVTME_STAMPS
+    {
+        std::vector<unsigned long long> h((size_t)count * 16);
+        HIP_TRY(hipMemcpyAsync(h.data(), c->d_stamps, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (uint32_t b = 0; b < count; b++) {
+            unsigned long long prev = h[b * 16];
+            for (int k = 1; k < 16; k++) {
+                const unsigned long long v = h[b * 16 + k];
+                if (v) {
+                    c->stamp_sum[k] += (double)(v - prev);
+                    prev = v;
+                }
+            }
+        }
+        c->stamp_n += count;
+    }
+#endif
     if (c->timing)
         HIP_TRY(hipEventRecord(c->ev1, c->stream));
     c->last_count  = count;

@@ -25,6 +25,18 @@
 #define ME_THREADS 256
 #define U32MAX 0xFFFFFFFFu
 
+// Diagnostic build only (-DSVTME_STAMPS): lane 0 stamps s_memtime at phase
+// boundaries into dj.stamps[sb][16]; the shipped kernel contains no stamp.
+#ifdef SVTME_STAMPS
+#define SVTME_STAMP(k)                                                                                              \
+    do {                                                                                                            \
+        if (threadIdx.x == 0 && dj.stamps)                                                                          \
+            dj.stamps[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();                               \
+    } while (0)
+#else
+#define SVTME_STAMP(k) do { } while (0)
+#endif
+
 // ----------------------------------------------------------------------------
 // Pyramid
 // ----------------------------------------------------------------------------
@@ -142,6 +154,7 @@ struct SbState {
     uint32_t best_sad[2][4][SVTME_PU_COUNT];
     uint32_t best_mv[2][4][SVTME_PU_COUNT];
     uint32_t me_distortion[SVTME_PU_COUNT];
+    uint8_t cand0[SVTME_PU_COUNT + 3]; // first candidate byte per PU (GM detection)
     int32_t flag; // uniform decisions broadcast from lane 0
     uint32_t b64_w, b64_h, ox_sb, oy_sb;
 };
@@ -610,6 +623,247 @@ __device__ void hme_l0_area(const SbState &st, const svtme_controls &c, int l, i
 }
 
 // ----------------------------------------------------------------------------
+// Tables for the candidate arrays (motion_estimation.c:2520-2531, definitions.h:2613-2632)
+// ----------------------------------------------------------------------------
+__constant__ uint8_t c_z_to_raster[85] = {
+    0,  1,  2,  3,  4,  5,  6,  9,  10, 7,  8,  11, 12, 13, 14, 17, 18, 15, 16, 19, 20, 21,
+    22, 29, 30, 23, 24, 31, 32, 37, 38, 45, 46, 39, 40, 47, 48, 25, 26, 33, 34, 27, 28, 35,
+    36, 41, 42, 49, 50, 43, 44, 51, 52, 53, 54, 61, 62, 55, 56, 63, 64, 69, 70, 77, 78, 71,
+    72, 79, 80, 57, 58, 65, 66, 59, 60, 67, 68, 73, 74, 81, 82, 75, 76, 83, 84};
+__constant__ uint8_t c_8x8_to_16x16[64] = {5,  5,  6,  6,  7,  7,  8,  8,  5,  5,  6,  6,  7,  7,  8,  8,
+                                           9,  9,  10, 10, 11, 11, 12, 12, 9,  9,  10, 10, 11, 11, 12, 12,
+                                           13, 13, 14, 14, 15, 15, 16, 16, 13, 13, 14, 14, 15, 15, 16, 16,
+                                           17, 17, 18, 18, 19, 19, 20, 20, 17, 17, 18, 18, 19, 19, 20, 20};
+__constant__ uint8_t c_16x16_to_32x32[16] = {1, 1, 2, 2, 1, 1, 2, 2, 3, 3, 4, 4, 3, 3, 4, 4};
+
+__device__ __forceinline__ uint8_t mk_cand(int dir, int r0, int r1, int l0, int l1) {
+    return (uint8_t)((dir & 3) | ((r0 & 3) << 2) | ((r1 & 3) << 4) | ((l0 & 1) << 6) | ((l1 & 1) << 7));
+}
+
+// Candidate arrays + distortions + GM detection for one SB, all threads
+// (motion_estimation.c:2532-3007). Thread n builds Z-order PU n.
+__device__ void finish_sb(SbState &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
+    const svtme_job &job = dj.job;
+    const int tid = threadIdx.x;
+    const int nl = job.num_lists, nr0 = job.num_refs[0], nr1 = nl == 2 ? job.num_refs[1] : 0;
+    svtme_sb_result *o = dj.out_sb + sb_local;
+    // zero the result (uint32 stores; sizeof is a multiple of 4)
+    uint32_t *ow = (uint32_t *)o;
+    for (int i = tid; i < (int)(sizeof(svtme_sb_result) / 4); i += ME_THREADS) ow[i] = 0;
+    __syncthreads();
+    const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
+    const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
+    if (mode != 2 && tid < npus)
+        o->total_me_candidate_index[tid] = 1; // memset(..., 1, number_of_pus)
+    __syncthreads();
+    if (tid < SVTME_PU_COUNT) {
+        const int n = tid;
+        const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
+        if (mode == 0) { // construct_me_candidate_array_single_ref
+            const int pu            = c_z_to_raster[n];
+            st.me_distortion[pu]    = st.best_sad[0][0][n];
+            st.cand0[pu]            = 0;
+            if (st.do_ref[0][0] && use) {
+                o->me_candidate_array[pu][0] = mk_cand(0, 0, 0, 0, 0);
+                o->me_mv_array[pu][0]        = st.best_mv[0][0][n];
+            }
+        } else if (mode == 1) { // construct_me_candidate_array_mrp_off
+            const int pu = c_z_to_raster[n];
+            uint32_t nlist = nl;
+            const uint8_t org0 = st.do_ref[0][0], org1 = nl == 1 ? 0 : st.do_ref[1][0];
+            if (nlist < 2 || !st.do_ref[1][0])
+                nlist = 1;
+            const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
+            uint8_t off = 0;
+            uint8_t blk[2] = {org0, org1};
+            const uint32_t s0 = st.best_sad[0][0][n], s1 = st.best_sad[1][0][n];
+            const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
+            st.me_distortion[pu] = best;
+            int min_list = -1;
+            if (job.ctrl.use_best_unipred_cand_only && blk[0] && blk[1])
+                min_list = s0 < s1 ? 0 : 1;
+            uint8_t c0 = 0;
+            for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
+                if (!blk[li])
+                    continue;
+                if (prune_th > 0) {
+                    const uint32_t dd = (st.best_sad[li][0][n] - best) * 100;
+                    if (dd > best * prune_th) {
+                        blk[li] = 0;
+                        continue;
+                    }
+                }
+                if (min_list != -1 && min_list != li) {
+                    if (use)
+                        o->me_mv_array[pu][li ? job.max_l0 : 0] = st.best_mv[li][0][n];
+                    continue;
+                }
+                if (use) {
+                    const uint8_t cb = mk_cand(li, 0, 0, li == 0 ? li : 24, li == 1 ? li : 24);
+                    o->me_candidate_array[pu][off] = cb;
+                    if (off == 0)
+                        c0 = cb;
+                    o->me_mv_array[pu][li ? job.max_l0 : 0] = st.best_mv[li][0][n];
+                }
+                off++;
+            }
+            if (blk[0] && blk[1] && use) {
+                const uint8_t cb = mk_cand(2, 0, 0, 0, 1);
+                o->me_candidate_array[pu][off] = cb;
+                if (off == 0)
+                    c0 = cb;
+                o->total_me_candidate_index[pu] = (uint8_t)(off + 1);
+            }
+            st.cand0[pu] = c0;
+        } else { // construct_me_candidate_array
+            const int pu = (n > 4) ? c_z_to_raster[n] : n;
+            uint8_t off = 0;
+            uint8_t blk[2][4] = {{0}};
+            const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
+            uint32_t best = U32MAX;
+            for (int li = 0; li < nl; li++)
+                for (int r = 0; r < (li ? nr1 : nr0); r++) {
+                    blk[li][r] = st.do_ref[li][r];
+                    if (!blk[li][r])
+                        continue;
+                    best = min_u32(best, st.best_sad[li][r][n]);
+                }
+            st.me_distortion[pu] = best;
+            uint8_t c0 = 0;
+            for (int li = 0; li < nl && (use || off == 0); ++li)
+                for (int r = 0; r < (li ? nr1 : nr0) && (use || off == 0); ++r) {
+                    if (!blk[li][r])
+                        continue;
+                    if (prune_th > 0) {
+                        const uint32_t dd = (st.best_sad[li][r][n] - best) * 100;
+                        if (dd > best * prune_th) {
+                            blk[li][r] = 0;
+                            continue;
+                        }
+                    }
+                    if (use) {
+                        const uint8_t cb = mk_cand(li, r, r, li == 0 ? li : 24, li == 1 ? li : 24);
+                        o->me_candidate_array[pu][off] = cb;
+                        if (off == 0)
+                            c0 = cb;
+                        o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.best_mv[li][r][n];
+                    }
+                    off++;
+                }
+            if (nl == 2 && use) {
+                for (int a2 = 0; a2 < nr0; a2++)
+                    for (int b2 = 0; b2 < nr1; b2++) {
+                        if (job.only_l_bwd && (a2 > 0 || b2 > 0))
+                            continue;
+                        if (blk[0][a2] && blk[1][b2]) {
+                            const uint8_t cb = mk_cand(2, a2, b2, 0, 1);
+                            if (off == 0)
+                                c0 = cb;
+                            o->me_candidate_array[pu][off++] = cb;
+                        }
+                    }
+                if (!job.only_l_bwd)
+                    for (int a2 = 1; a2 < nr0; a2++)
+                        if (blk[0][0] && blk[0][a2]) {
+                            const uint8_t cb = mk_cand(2, 0, a2, 0, 0);
+                            if (off == 0)
+                                c0 = cb;
+                            o->me_candidate_array[pu][off++] = cb;
+                        }
+                if (!job.only_l_bwd && nr1 == 3 && blk[1][0] && blk[1][2]) {
+                    const uint8_t cb = mk_cand(2, 0, 2, 1, 1);
+                    if (off == 0)
+                        c0 = cb;
+                    o->me_candidate_array[pu][off++] = cb;
+                }
+            }
+            if (use)
+                o->total_me_candidate_index[pu] = off;
+            st.cand0[pu] = use ? c0 : 0;
+        }
+    }
+    __syncthreads();
+    if (tid < SVTME_PU_COUNT)
+        o->me_distortion[tid] = st.me_distortion[tid];
+    if (tid == 0) {
+        // compute_distortion (motion_estimation.c:2964-3007)
+        uint32_t d64 = st.me_distortion[0], d32 = 0, d16 = 0, d8 = 0;
+        for (int i = 0; i < 4; i++) d32 += st.me_distortion[1 + i];
+        for (int i = 0; i < 16; i++) d16 += st.me_distortion[5 + i];
+        for (int i = 0; i < 64; i++) d8 += st.me_distortion[21 + i];
+        const uint64_t mean = d8 / 64;
+        uint64_t sum_sq = 0;
+        for (int i = 0; i < 64; i++) {
+            const int64_t diff = (int64_t)st.me_distortion[21 + i] - (int64_t)mean;
+            sum_sq += (uint64_t)(diff * diff);
+        }
+        o->me_8x8_cost_variance = (uint32_t)(sum_sq / 64);
+        o->rc_me_distortion     = (job.input_resolution <= 2) ? d8 : d16;
+        const uint32_t pix      = bw * bh;
+        o->me_64x64_distortion  = (d64 * 4096u) / pix;
+        o->me_32x32_distortion  = (d32 * 4096u) / pix;
+        o->me_16x16_distortion  = (d16 * 4096u) / pix;
+        o->me_8x8_distortion    = (d8 * 4096u) / pix;
+        // perform_gm_detection (motion_estimation.c:2838-2961)
+        if (job.gm_enabled) {
+            uint64_t stationary = 0, tot = 0;
+            uint32_t cnt[2][4][2][2];
+            for (int a2 = 0; a2 < 2; a2++)
+                for (int b2 = 0; b2 < 4; b2++)
+                    for (int cc = 0; cc < 2; cc++) cnt[a2][b2][cc][0] = cnt[a2][b2][cc][1] = 0;
+            const bool low = job.input_resolution <= 2;
+            const int n_blk = low ? 64 : 16;
+            for (int i = 0; i < n_blk; i++) {
+                uint8_t n = (uint8_t)(low ? 21 + i : 5 + i);
+                if (low && !job.enable_me_8x8) {
+                    if (n >= 21)
+                        n = c_8x8_to_16x16[n - 21];
+                    if (!job.enable_me_16x16 && n >= 5)
+                        n = c_16x16_to_32x32[n - 5];
+                }
+                if (!low && !job.enable_me_16x16 && n >= 5)
+                    n = c_16x16_to_32x32[n - 5];
+                const uint8_t cb = st.cand0[n];
+                const int dir = cb & 3, r0 = (cb >> 2) & 3, r1 = (cb >> 4) & 3, l0 = (cb >> 6) & 1, l1 = (cb >> 7) & 1;
+                const int li = (dir == 0 || dir == 2) ? l0 : l1;
+                const int ri = (dir == 0 || dir == 2) ? r0 : r1;
+                int active_th;
+                if (low) {
+                    const uint64_t a2 = job.picture_number, b2 = job.ref_picture_number[li][ri];
+                    const uint16_t dist = (uint16_t)absi((int16_t)((a2 > b2 ? a2 : b2) - (a2 < b2 ? a2 : b2)));
+                    active_th = job.gm_use_distance_based_active_th ? max(dist >> 1, 4) : 4;
+                } else {
+                    const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - job.ref_picture_number[li][ri]));
+                    active_th = job.gm_use_distance_based_active_th ? max(dist * 16, 32) : 32;
+                }
+                const uint32_t mv = st.best_mv[li][ri][n];
+                const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4;
+                if (mx < -active_th)
+                    cnt[li][ri][0][0]++;
+                else if (mx > active_th)
+                    cnt[li][ri][0][1]++;
+                if (my < -active_th)
+                    cnt[li][ri][1][0]++;
+                else if (my > active_th)
+                    cnt[li][ri][1][1]++;
+                const int stt = low ? 0 : 4;
+                if (absi(mx) <= stt && absi(my) <= stt)
+                    stationary++;
+                tot++;
+            }
+            if (stationary > ((tot * 5) / 100))
+                o->stationary_block_present = 1;
+            for (int a2 = 0; a2 < 2; a2++)
+                for (int b2 = 0; b2 < 4; b2++)
+                    for (int cc = 0; cc < 2; cc++)
+                        for (int s2 = 0; s2 < 2; s2++)
+                            if (cnt[a2][b2][cc][s2] > (tot / 2))
+                                o->rc_me_allow_gm = 1;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
 // The per-SB kernel
 // ----------------------------------------------------------------------------
 template <bool SUB_ME>
@@ -618,7 +872,11 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
     const int tid = threadIdx.x, lane = tid & 63;
-    const uint32_t sb_local = blockIdx.x;
+    // XCD-aware SB order: blocks b and b+8 share an XCD (round-robin dispatch), so give
+    // each XCD one contiguous band of SBs; neighbouring SBs share reference windows in
+    // that XCD's L2 (bijective for any grid size; placement only affects speed)
+    const uint32_t nwg = gridDim.x, bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const uint32_t sb_local = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     const uint32_t b64      = job.sb_begin + sb_local;
     const uint32_t ox = (b64 % dj.pic_w_b64) * 64, oy = (b64 / dj.pic_w_b64) * 64;
     const uint32_t bw = (job.width - ox) < 64 ? job.width - ox : 64;
@@ -626,6 +884,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
     const int nl = job.num_lists;
     const int nr0 = job.num_refs[0], nr1 = nl == 2 ? job.num_refs[1] : 0;
     const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
+    SVTME_STAMP(0);
 
     // ---- source blocks -> LDS (me_process.c:183-214)
     {
@@ -680,6 +939,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
     }
     for (int e = tid; e < 2 * 4 * SVTME_PU_COUNT; e += ME_THREADS) (&st.best_mv[0][0][0])[e] = 0;
     __syncthreads();
+    SVTME_STAMP(1);
 
     // ---- init_zz_sad (motion_estimation.c:2382-2437)
     if (c.me_early_exit_th || c.me_safe_limit_zz_th) {
@@ -723,6 +983,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
             }
         }
         __syncthreads();
+    SVTME_STAMP(2);
     }
 
     // ---- pre-HME (motion_estimation.c:1693-1796); list 1 runs after list 0
@@ -825,6 +1086,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
             }
         }
         __syncthreads();
+    SVTME_STAMP(3);
     }
 
     if (c.enable_hme_flag) {
@@ -926,6 +1188,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
                 }
             }
             __syncthreads();
+    SVTME_STAMP(4);
         }
         // ---- HME level 1 (motion_estimation.c:2041-2122)
         if (c.enable_hme_level1_flag) {
@@ -991,6 +1254,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
                 }
             }
             __syncthreads();
+    SVTME_STAMP(5);
         }
         // ---- HME level 2 (motion_estimation.c:2127-2177)
         if (c.enable_hme_level2_flag) {
@@ -1038,6 +1302,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
                 }
             }
             __syncthreads();
+    SVTME_STAMP(6);
         }
     }
 
@@ -1118,6 +1383,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
             for (int r = 0; r < 4; r++) st.searched[l][r] = st.do_ref[l][r];
     }
     __syncthreads();
+    SVTME_STAMP(7);
 
     // ---- integer_search_b64 (motion_estimation.c:1249-1516)
     // two rounds when enable_me_sr_adjustment == 2 (other refs read ref (0,0)'s result)
@@ -1263,6 +1529,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
                 }
         }
         __syncthreads();
+    SVTME_STAMP(8);
         if (st.nfp) {
             run_fullpel<SUB_ME>(st, job, dj);
             // decode the centre results, then the 8x8-variance resize (motion_estimation.c:1414-1438)
@@ -1300,6 +1567,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
                 }
             }
             __syncthreads();
+    SVTME_STAMP(9);
         }
         // final area clamp + main full-pel search of every searched reference
         if (tid == 0) {
@@ -1345,6 +1613,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
             decode_keys(st, l, r, st.is_xc[l][r], st.is_yc[l][r], st.fp[f].xo, st.fp[f].yo, st.fp[f].w);
         }
         __syncthreads();
+    SVTME_STAMP(10);
     }
 
     // ---- me_prune_ref (motion_estimation.c:1522-1565)
@@ -1372,6 +1641,7 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
         }
     }
     __syncthreads();
+    SVTME_STAMP(11);
 
     // ---- records
     {
@@ -1397,233 +1667,12 @@ __global__ void __launch_bounds__(ME_THREADS) k_me_sb(const DevJob dj) {
             }
         }
     }
+    if (dj.out_sb) {
+        __syncthreads();
+        finish_sb(st, dj, sb_local, bw, bh);
+    }
+    SVTME_STAMP(12);
     (void)lane;
-}
-
-// ----------------------------------------------------------------------------
-// Candidate arrays + distortions: one thread per SB (motion_estimation.c:2532-3007)
-// ----------------------------------------------------------------------------
-__constant__ uint8_t c_z_to_raster[85] = {
-    0,  1,  2,  3,  4,  5,  6,  9,  10, 7,  8,  11, 12, 13, 14, 17, 18, 15, 16, 19, 20, 21,
-    22, 29, 30, 23, 24, 31, 32, 37, 38, 45, 46, 39, 40, 47, 48, 25, 26, 33, 34, 27, 28, 35,
-    36, 41, 42, 49, 50, 43, 44, 51, 52, 53, 54, 61, 62, 55, 56, 63, 64, 69, 70, 77, 78, 71,
-    72, 79, 80, 57, 58, 65, 66, 59, 60, 67, 68, 73, 74, 81, 82, 75, 76, 83, 84};
-__constant__ uint8_t c_8x8_to_16x16[64] = {5,  5,  6,  6,  7,  7,  8,  8,  5,  5,  6,  6,  7,  7,  8,  8,
-                                           9,  9,  10, 10, 11, 11, 12, 12, 9,  9,  10, 10, 11, 11, 12, 12,
-                                           13, 13, 14, 14, 15, 15, 16, 16, 13, 13, 14, 14, 15, 15, 16, 16,
-                                           17, 17, 18, 18, 19, 19, 20, 20, 17, 17, 18, 18, 19, 19, 20, 20};
-__constant__ uint8_t c_16x16_to_32x32[16] = {1, 1, 2, 2, 1, 1, 2, 2, 3, 3, 4, 4, 3, 3, 4, 4};
-
-__device__ __forceinline__ uint8_t mk_cand(int dir, int r0, int r1, int l0, int l1) {
-    return (uint8_t)((dir & 3) | ((r0 & 3) << 2) | ((r1 & 3) << 4) | ((l0 & 1) << 6) | ((l1 & 1) << 7));
-}
-
-__global__ void __launch_bounds__(64) k_me_post(const DevJob dj, uint32_t sb_count) {
-    const uint32_t sb = blockIdx.x * blockDim.x + threadIdx.x;
-    if (sb >= sb_count)
-        return;
-    const svtme_job &job          = dj.job;
-    const svtme_ref_record *recs  = dj.out_records + (size_t)sb * dj.R;
-    svtme_sb_result *o            = dj.out_sb + sb;
-    const int nl = job.num_lists, nr0 = job.num_refs[0], nr1 = nl == 2 ? job.num_refs[1] : 0;
-    const svtme_ref_record *rec[2][4] = {{nullptr}};
-    for (int l = 0, k = 0; l < nl; l++)
-        for (int r = 0; r < (l ? nr1 : nr0); r++) rec[l][r] = &recs[k++];
-    uint8_t *ob = (uint8_t *)o;
-    for (size_t i = 0; i < sizeof(svtme_sb_result); i++) ob[i] = 0;
-    uint32_t me_dist[85];
-    const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
-    auto BS = [&](int l, int r, int n) -> uint32_t { return rec[l][r]->best_sad[n]; };
-    auto BM = [&](int l, int r, int n) -> uint32_t { return rec[l][r]->best_mv[n]; };
-    auto DR = [&](int l, int r) -> uint8_t { return rec[l][r] ? rec[l][r]->do_ref : 0; };
-    if (nr0 == 1 && nr1 == 0) { // construct_me_candidate_array_single_ref
-        const uint8_t blk = DR(0, 0);
-        for (int n = 0; n < npus; n++) o->total_me_candidate_index[n] = 1;
-        for (int n = 0; n < 85; n++) {
-            const int pu  = c_z_to_raster[n];
-            const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
-            me_dist[pu]   = BS(0, 0, n);
-            if (!blk)
-                continue;
-            if (use) {
-                o->me_candidate_array[pu][0] = mk_cand(0, 0, 0, 0, 0);
-                o->me_mv_array[pu][0]        = BM(0, 0, n);
-            }
-        }
-    } else if (nr0 == 1 && nr1 == 1) { // construct_me_candidate_array_mrp_off
-        uint32_t nlist = nl;
-        const uint8_t org0 = DR(0, 0), org1 = nl == 1 ? 0 : DR(1, 0);
-        if (nlist < 2 || !DR(1, 0))
-            nlist = 1;
-        const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
-        for (int n = 0; n < npus; n++) o->total_me_candidate_index[n] = 1;
-        for (int n = 0; n < 85; n++) {
-            const int pu  = c_z_to_raster[n];
-            uint8_t off   = 0;
-            const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
-            uint8_t blk[2] = {org0, org1};
-            const uint32_t best = (org0 && org1) ? min_u32(BS(0, 0, n), BS(1, 0, n)) : org0 ? BS(0, 0, n) : BS(1, 0, n);
-            me_dist[pu]         = best;
-            int min_list        = -1;
-            if (job.ctrl.use_best_unipred_cand_only && blk[0] && blk[1])
-                min_list = BS(0, 0, n) < BS(1, 0, n) ? 0 : 1;
-            for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
-                if (!blk[li])
-                    continue;
-                if (prune_th > 0) {
-                    const uint32_t dd = (BS(li, 0, n) - best) * 100;
-                    if (dd > best * prune_th) {
-                        blk[li] = 0;
-                        continue;
-                    }
-                }
-                if (min_list != -1 && min_list != li) {
-                    if (use)
-                        o->me_mv_array[pu][li ? job.max_l0 : 0] = BM(li, 0, n);
-                    continue;
-                }
-                if (use) {
-                    o->me_candidate_array[pu][off] = mk_cand(li, 0, 0, li == 0 ? li : 24, li == 1 ? li : 24);
-                    o->me_mv_array[pu][li ? job.max_l0 : 0] = BM(li, 0, n);
-                }
-                off++;
-            }
-            if (blk[0] && blk[1] && use) {
-                o->me_candidate_array[pu][off]  = mk_cand(2, 0, 0, 0, 1);
-                o->total_me_candidate_index[pu] = (uint8_t)(off + 1);
-            }
-        }
-    } else { // construct_me_candidate_array
-        for (int n = 0; n < 85; n++) {
-            const int pu  = (n > 4) ? c_z_to_raster[n] : n;
-            uint8_t off   = 0;
-            const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
-            uint8_t blk[2][4] = {{0}};
-            const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
-            uint32_t best           = U32MAX;
-            for (int li = 0; li < nl; li++)
-                for (int r = 0; r < (li ? nr1 : nr0); r++) {
-                    blk[li][r] = DR(li, r);
-                    if (!blk[li][r])
-                        continue;
-                    best = min_u32(best, BS(li, r, n));
-                }
-            me_dist[pu] = best;
-            for (int li = 0; li < nl && (use || off == 0); ++li)
-                for (int r = 0; r < (li ? nr1 : nr0) && (use || off == 0); ++r) {
-                    if (!blk[li][r])
-                        continue;
-                    if (prune_th > 0) {
-                        const uint32_t dd = (BS(li, r, n) - best) * 100;
-                        if (dd > best * prune_th) {
-                            blk[li][r] = 0;
-                            continue;
-                        }
-                    }
-                    if (use) {
-                        o->me_candidate_array[pu][off] = mk_cand(li, r, r, li == 0 ? li : 24, li == 1 ? li : 24);
-                        o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = BM(li, r, n);
-                    }
-                    off++;
-                }
-            if (nl == 2 && use) {
-                for (int a = 0; a < nr0; a++)
-                    for (int b = 0; b < nr1; b++) {
-                        if (job.only_l_bwd && (a > 0 || b > 0))
-                            continue;
-                        if (blk[0][a] && blk[1][b])
-                            o->me_candidate_array[pu][off++] = mk_cand(2, a, b, 0, 1);
-                    }
-                if (!job.only_l_bwd)
-                    for (int a = 1; a < nr0; a++)
-                        if (blk[0][0] && blk[0][a])
-                            o->me_candidate_array[pu][off++] = mk_cand(2, 0, a, 0, 0);
-                if (!job.only_l_bwd && nr1 == 3 && blk[1][0] && blk[1][2])
-                    o->me_candidate_array[pu][off++] = mk_cand(2, 0, 2, 1, 1);
-            }
-            if (use)
-                o->total_me_candidate_index[pu] = off;
-        }
-    }
-    for (int i = 0; i < 85; i++) o->me_distortion[i] = me_dist[i];
-    // compute_distortion (motion_estimation.c:2964-3007)
-    const uint32_t b64 = job.sb_begin + sb;
-    const uint32_t ox = (b64 % dj.pic_w_b64) * 64, oy = (b64 / dj.pic_w_b64) * 64;
-    const uint32_t bw = (job.width - ox) < 64 ? job.width - ox : 64;
-    const uint32_t bh = (job.height - oy) < 64 ? job.height - oy : 64;
-    uint32_t d64 = me_dist[0], d32 = 0, d16 = 0, d8 = 0;
-    for (int i = 0; i < 4; i++) d32 += me_dist[1 + i];
-    for (int i = 0; i < 16; i++) d16 += me_dist[5 + i];
-    for (int i = 0; i < 64; i++) d8 += me_dist[21 + i];
-    const uint64_t mean = d8 / 64;
-    uint64_t sum_sq     = 0;
-    for (int i = 0; i < 64; i++) {
-        const int64_t diff = (int64_t)me_dist[21 + i] - (int64_t)mean;
-        sum_sq += (uint64_t)(diff * diff);
-    }
-    o->me_8x8_cost_variance = (uint32_t)(sum_sq / 64);
-    o->rc_me_distortion     = (job.input_resolution <= 2) ? d8 : d16;
-    const uint32_t pix      = bw * bh;
-    o->me_64x64_distortion  = (d64 * 4096u) / pix;
-    o->me_32x32_distortion  = (d32 * 4096u) / pix;
-    o->me_16x16_distortion  = (d16 * 4096u) / pix;
-    o->me_8x8_distortion    = (d8 * 4096u) / pix;
-    // perform_gm_detection (motion_estimation.c:2838-2961)
-    if (job.gm_enabled) {
-        uint64_t stationary = 0, tot = 0;
-        uint32_t cnt[2][4][2][2];
-        for (int a = 0; a < 2; a++)
-            for (int b = 0; b < 4; b++)
-                for (int cc = 0; cc < 2; cc++) cnt[a][b][cc][0] = cnt[a][b][cc][1] = 0;
-        const bool low = job.input_resolution <= 2;
-        const int n_blk = low ? 64 : 16;
-        for (int i = 0; i < n_blk; i++) {
-            uint8_t n = (uint8_t)(low ? 21 + i : 5 + i);
-            if (low && !job.enable_me_8x8) {
-                if (n >= 21)
-                    n = c_8x8_to_16x16[n - 21];
-                if (!job.enable_me_16x16 && n >= 5)
-                    n = c_16x16_to_32x32[n - 5];
-            }
-            if (!low && !job.enable_me_16x16 && n >= 5)
-                n = c_16x16_to_32x32[n - 5];
-            const uint8_t cb = o->me_candidate_array[n][0];
-            const int dir = cb & 3, r0 = (cb >> 2) & 3, r1 = (cb >> 4) & 3, l0 = (cb >> 6) & 1, l1 = (cb >> 7) & 1;
-            const int li = (dir == 0 || dir == 2) ? l0 : l1;
-            const int ri = (dir == 0 || dir == 2) ? r0 : r1;
-            int active_th;
-            if (low) {
-                const uint64_t a = job.picture_number, b = job.ref_picture_number[li][ri];
-                const uint16_t dist = (uint16_t)absi((int16_t)((a > b ? a : b) - (a < b ? a : b)));
-                active_th = job.gm_use_distance_based_active_th ? max(dist >> 1, 4) : 4;
-            } else {
-                const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - job.ref_picture_number[li][ri]));
-                active_th = job.gm_use_distance_based_active_th ? max(dist * 16, 32) : 32;
-            }
-            const uint32_t mv = rec[li][ri] ? rec[li][ri]->best_mv[n] : 0;
-            const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4;
-            if (mx < -active_th)
-                cnt[li][ri][0][0]++;
-            else if (mx > active_th)
-                cnt[li][ri][0][1]++;
-            if (my < -active_th)
-                cnt[li][ri][1][0]++;
-            else if (my > active_th)
-                cnt[li][ri][1][1]++;
-            const int stt = low ? 0 : 4;
-            if (absi(mx) <= stt && absi(my) <= stt)
-                stationary++;
-            tot++;
-        }
-        if (stationary > ((tot * 5) / 100))
-            o->stationary_block_present = 1;
-        for (int a = 0; a < 2; a++)
-            for (int b = 0; b < 4; b++)
-                for (int cc = 0; cc < 2; cc++)
-                    for (int s = 0; s < 2; s++)
-                        if (cnt[a][b][cc][s] > (tot / 2))
-                            o->rc_me_allow_gm = 1;
-    }
 }
 
 // ----------------------------------------------------------------------------
@@ -1653,9 +1702,5 @@ extern "C" hipError_t svtme_launch_me(const DevJob *dj, uint32_t sb_count, hipSt
         hipLaunchKernelGGL(k_me_sb<false>, dim3(sb_count), dim3(ME_THREADS), 0, s, *dj);
     else
         hipLaunchKernelGGL(k_me_sb<true>, dim3(sb_count), dim3(ME_THREADS), 0, s, *dj);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !dj->out_sb)
-        return e;
-    hipLaunchKernelGGL(k_me_post, dim3((sb_count + 63) / 64), dim3(64), 0, s, *dj, sb_count);
     return hipGetLastError();
 }

@@ -400,7 +400,8 @@ def make_job(width: int, height: int, ctrl: Controls, picture_number: int, refs_
 # Product library (HIP): loaded lazily; raises if absent
 # ----------------------------------------------------------------------------
 def product_lib_path() -> str:
-    return os.path.join(PKG_DIR, "libsvtme.so")
+    # SVTME_LIB selects a diagnostic build (e.g. libsvtme_stamps.so); default is the product
+    return os.path.join(PKG_DIR, os.environ.get("SVTME_LIB", "libsvtme.so"))
 
 
 def load_product():
