@@ -29,6 +29,7 @@ extern "C" hipError_t svtme_launch_build_full(const void *src, uint32_t src_stri
 extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int left, int top, int rows,
                                               hipStream_t s);
 extern "C" hipError_t svtme_launch_me(const DevJob *dj, uint32_t sb_count, hipStream_t s);
+extern "C" hipError_t svtme_launch_me2(const DevJob *dj, uint32_t sb_count, hipStream_t s);
 
 // ----------------------------------------------------------------------------
 // errors
@@ -387,7 +388,11 @@ static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_
 #endif
     if (c->timing)
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    HIP_TRY(svtme_launch_me(&dj, count, c->stream));
+    static const bool use_v1 = [] {
+        const char *e = getenv("SVTME_KERNEL");
+        return e && strcmp(e, "v1") == 0;
+    }();
+    HIP_TRY(use_v1 ? svtme_launch_me(&dj, count, c->stream) : svtme_launch_me2(&dj, count, c->stream));
 #ifdef SVTME_STAMPS
     {
         std::vector<unsigned long long> h((size_t)count * 16);
