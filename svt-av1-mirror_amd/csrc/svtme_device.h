@@ -29,6 +29,28 @@ struct DevPyramid {
     DevPlane lv[3];  // 0 = full, 1 = quarter, 2 = sixteenth
 };
 
+// Stage-A result of one search (svtme_stages.hip). Index layout per SB:
+// [0, 8) zz SAD by slot (sad = raw sub-sampled n x m sum), [8, 24) pre-HME
+// slot * 2 + region, [24, 56) HME level 0 slot * 4 + quadrant (sx * 2 + sy).
+struct ARes {
+    uint32_t sad;
+    int16_t x, y; // final (scaled, absolute) search-centre MV
+};
+#define SVTME_A_ZZ 0
+#define SVTME_A_PH 8
+#define SVTME_A_L0 24
+#define SVTME_A_N 56
+
+// Stage-B output per SB: the SearchResults of every slot after HME and the
+// HME-based pruning (me_context.h:348-355), consumed by stage C.
+struct BState {
+    uint64_t hme_sad[8];
+    uint32_t zz[8];
+    uint32_t reduce_div[8];
+    int16_t sc_x[8], sc_y[8];
+    uint8_t do_ref[8];
+};
+
 // Parameters of one picture job as the kernel sees them.
 struct DevJob {
     svtme_job job;                 // controls + picture description (host copy)
@@ -39,6 +61,10 @@ struct DevJob {
     uint32_t R;
     uint32_t pic_w_b64;
     unsigned long long *stamps;    // diagnostic builds only: [sb_count][16] s_memtime
+    ARes *ares;                    // [sb_count][SVTME_A_N] stage-A results
+    BState *bst;                   // [sb_count] stage-B state
+    uint32_t ta_count;             // stage-A searches per SB
+    uint8_t ta_list[SVTME_A_N];    // their ARes indices
 };
 
 static inline uint32_t svtme_round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }

@@ -30,6 +30,8 @@ extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int l
                                               hipStream_t s);
 extern "C" hipError_t svtme_launch_me(const DevJob *dj, uint32_t sb_count, hipStream_t s);
 extern "C" hipError_t svtme_launch_me2(const DevJob *dj, uint32_t sb_count, hipStream_t s);
+extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s);
+extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 
 // ----------------------------------------------------------------------------
 // errors
@@ -87,6 +89,10 @@ struct svtme_ctx {
     bool last_has_sb    = false;
     bool timing         = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    ARes *d_ares    = nullptr; // stage-A results [count][SVTME_A_N]
+    size_t ares_cap = 0;
+    BState *d_bst   = nullptr; // stage-B state [count]
+    size_t bst_cap  = 0;
 #ifdef SVTME_STAMPS
     unsigned long long *d_stamps = nullptr;
     size_t stamps_cap            = 0;
@@ -151,6 +157,10 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
     if (c->d_stamps)
         (void)hipFree(c->d_stamps);
 #endif
+    if (c->d_ares)
+        (void)hipFree(c->d_ares);
+    if (c->d_bst)
+        (void)hipFree(c->d_bst);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -323,6 +333,10 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
     if (job->ctrl.num_hme_sa_w != 2 || job->ctrl.num_hme_sa_h != 2)
         return fail(SVTME_ERR_BAD_PARAMETER, "only 2x2 HME-L0 search regions are supported "
                                              "(motion_estimation.c:1875)");
+    if (job->ctrl.enable_me_sr_adjustment && job->ctrl.distance_based_hme_resizing &&
+        job->ctrl.reduce_hme_l0_sr_th_min && job->ctrl.reduce_hme_l0_sr_th_max)
+        return fail(SVTME_ERR_BAD_PARAMETER, "reduce_hme_l0_sr_th_min/max (real-time tune, enc_mode_config.c:690-703) "
+                                             "are not supported");
     if (job->width > 16384 || job->height > 16384)
         return fail(SVTME_ERR_BAD_PARAMETER, "picture too large for int16 search arithmetic");
     const uint32_t total = svtme_sb_total(job->width, job->height);
@@ -353,6 +367,7 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
     dj->R         = svtme_job_ref_slots(job);
     dj->pic_w_b64 = (job->width + 63) / 64;
     *count        = n;
+    dj->job.sb_count = n;
     if (dj->R == 0)
         return fail(SVTME_ERR_BAD_PARAMETER, "job has no references");
     return SVTME_OK;
@@ -388,11 +403,23 @@ static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_
 #endif
     if (c->timing)
         HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    static const bool use_v1 = [] {
+    if ((st = ensure_buf((void **)&c->d_ares, &c->ares_cap, (size_t)count * SVTME_A_N * sizeof(ARes))))
+        return st;
+    if ((st = ensure_buf((void **)&c->d_bst, &c->bst_cap, (size_t)count * sizeof(BState))))
+        return st;
+    dj.ares = c->d_ares;
+    dj.bst  = c->d_bst;
+    svtme_stage_a_list(&dj.job, dj.ta_list, &dj.ta_count);
+    static const int kernel_version = [] {
         const char *e = getenv("SVTME_KERNEL");
-        return e && strcmp(e, "v1") == 0;
+        return e ? atoi(e + (e[0] == 'v')) : 3;
     }();
-    HIP_TRY(use_v1 ? svtme_launch_me(&dj, count, c->stream) : svtme_launch_me2(&dj, count, c->stream));
+    if (kernel_version == 1)
+        HIP_TRY(svtme_launch_me(&dj, count, c->stream));
+    else if (kernel_version == 2)
+        HIP_TRY(svtme_launch_me2(&dj, count, c->stream));
+    else
+        HIP_TRY(svtme_launch_stages(&dj, count, c->stream));
 #ifdef SVTME_STAMPS
     {
         std::vector<unsigned long long> h((size_t)count * 16);

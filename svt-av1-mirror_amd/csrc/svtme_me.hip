@@ -163,6 +163,7 @@ struct St {
     DevPlane pl[8][3];      // reference planes by slot (copied from the kernel argument)
     uint64_t refpic[8];
     uint16_t dist[8];
+    uint32_t gm_cnt[2][4][2][2];
     const uint8_t *req[16]; // n x m SAD requests (zz, check_00_center)
     int32_t req_stride[16];
     int8_t req_slot[8];
@@ -456,6 +457,41 @@ __device__ __forceinline__ void quad_rows_lds(const uint32_t *win, int pitch_dw,
     }
 }
 
+// v_qsad_pk_u16_u8: 4 SADs of one source dword against the 4 byte shifts of a
+// reference dword pair, accumulated in 4 u16 lanes
+__device__ __forceinline__ unsigned long long qsad(uint32_t lo, uint32_t hi, uint32_t s, unsigned long long a) {
+    return __builtin_amdgcn_qsad_pk_u16_u8(((unsigned long long)hi << 32) | lo, s, a);
+}
+__device__ __forceinline__ void qsad_unpack(unsigned long long a, uint32_t acc[4]) {
+    acc[0] += (uint32_t)a & 0xFFFFu;
+    acc[1] += (uint32_t)a >> 16;
+    acc[2] += (uint32_t)(a >> 32) & 0xFFFFu;
+    acc[3] += (uint32_t)(a >> 48);
+}
+
+// quad_rows_lds for whole-dword block widths on v_qsad_pk_u16_u8; the u16
+// lanes are widened every 64 / nd rows (nd * 1020 * rows <= 65280)
+__device__ __forceinline__ void quad_rows_qsad(const uint32_t *win, int pitch_dw, int row0, int ystep,
+                                               const uint8_t *src, int src_stride, int nd, int k0, int k1,
+                                               uint32_t acc[4]) {
+    const int chunk = 64 / nd;
+    for (int kc = k0; kc < k1; kc += chunk) {
+        const int ke         = min(k1, kc + chunk);
+        unsigned long long a = 0;
+        for (int k = kc; k < ke; k++) {
+            const uint32_t *rd = win + (row0 + k * ystep) * pitch_dw;
+            const uint32_t *sd = (const uint32_t *)(src + k * src_stride);
+            uint32_t d0        = rd[0];
+            for (int j = 0; j < nd; j++) {
+                const uint32_t d1 = rd[j + 1];
+                a                 = qsad(d0, d1, sd[j], a);
+                d0                = d1;
+            }
+        }
+        qsad_unpack(a, acc);
+    }
+}
+
 // same from global memory at an arbitrary byte address (oversized windows)
 __device__ __forceinline__ void quad_rows_global(const uint8_t *ref, int ref_stride, const uint8_t *src, int src_stride,
                                                  int bw, int k0, int k1, uint32_t acc[4]) {
@@ -525,7 +561,7 @@ __device__ void search_tasks(St &st) {
                     else if (bw & 3)
                         quad_rows_lds<true>(win + q, pitch, odd ? yy : y, ystep, src, sstride, bw, k0, k1, acc);
                     else
-                        quad_rows_lds<false>(win + q, pitch, odd ? yy : y, ystep, src, sstride, bw, k0, k1, acc);
+                        quad_rows_qsad(win + q, pitch, odd ? yy : y, ystep, src, sstride, bw >> 2, k0, k1, acc);
                 }
                 for (int o = 1; o < G; o <<= 1)
 #pragma unroll
@@ -671,20 +707,15 @@ __device__ void fullpel_run(St &st) {
                 uint32_t acc[4] = {0, 0, 0, 0};
                 if (!direct) {
                     const uint32_t *win = wbase + y * pitch + q;
+                    unsigned long long a = 0;
 #pragma unroll
                     for (int rr = 0; rr < ROWS; rr++) {
                         const uint32_t *rd = win + rr * RSTEP * pitch;
                         const uint32_t d0 = rd[0], d1 = rd[1], d2 = rd[2];
-                        const uint32_t s0 = src[rr][0], s1 = src[rr][1];
-                        acc[0] = __builtin_amdgcn_sad_u8(d0, s0, acc[0]);
-                        acc[0] = __builtin_amdgcn_sad_u8(d1, s1, acc[0]);
-                        acc[1] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d1, d0, 1), s0, acc[1]);
-                        acc[1] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d2, d1, 1), s1, acc[1]);
-                        acc[2] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d1, d0, 2), s0, acc[2]);
-                        acc[2] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d2, d1, 2), s1, acc[2]);
-                        acc[3] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d1, d0, 3), s0, acc[3]);
-                        acc[3] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d2, d1, 3), s1, acc[3]);
+                        a = qsad(d0, d1, src[rr][0], a);
+                        a = qsad(d1, d2, src[rr][1], a);
                     }
+                    qsad_unpack(a, acc);
                 } else {
                     const uint8_t *rp = F.g + (ptrdiff_t)(y + by * 8) * gstride + x0 + bx * 8;
                     const int sh      = (int)((uintptr_t)rp & 3);
@@ -827,21 +858,21 @@ __device__ void finish_sb(St &st, const DevJob &dj, uint32_t sb_local, uint32_t 
                 nlist = 1;
             const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
             uint8_t off = 0;
-            uint8_t blk[2] = {org0, org1};
+            uint32_t blk = (org0 ? 1u : 0u) | (org1 ? 2u : 0u); // bit li
             const uint32_t s0 = st.best_sad[(0) * 4 + (0)][n], s1 = st.best_sad[(1) * 4 + (0)][n];
             const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
             st.me_distortion[pu] = best;
             int min_list = -1;
-            if (job.ctrl.use_best_unipred_cand_only && blk[0] && blk[1])
+            if (job.ctrl.use_best_unipred_cand_only && (blk & 3u) == 3u)
                 min_list = s0 < s1 ? 0 : 1;
             uint8_t c0 = 0;
             for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
-                if (!blk[li])
+                if (!((blk >> li) & 1u))
                     continue;
                 if (prune_th > 0) {
                     const uint32_t dd = (st.best_sad[(li) * 4 + (0)][n] - best) * 100;
                     if (dd > best * prune_th) {
-                        blk[li] = 0;
+                        blk &= ~(1u << li);
                         continue;
                     }
                 }
@@ -859,7 +890,7 @@ __device__ void finish_sb(St &st, const DevJob &dj, uint32_t sb_local, uint32_t 
                 }
                 off++;
             }
-            if (blk[0] && blk[1] && use) {
+            if ((blk & 3u) == 3u && use) {
                 const uint8_t cb = mk_cand(2, 0, 0, 0, 1);
                 o->me_candidate_array[pu][off] = cb;
                 if (off == 0)
@@ -870,13 +901,13 @@ __device__ void finish_sb(St &st, const DevJob &dj, uint32_t sb_local, uint32_t 
         } else { // construct_me_candidate_array
             const int pu = (n > 4) ? c_z_to_raster[n] : n;
             uint8_t off = 0;
-            uint8_t blk[2][4] = {{0}};
+            uint32_t blk = 0; // bit li * 4 + r
             const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
             uint32_t best = U32MAX;
             for (int li = 0; li < nl; li++)
                 for (int r = 0; r < (li ? nr1 : nr0); r++) {
-                    blk[li][r] = st.do_ref[(li) * 4 + (r)];
-                    if (!blk[li][r])
+                    blk |= st.do_ref[(li) * 4 + (r)] ? 1u << (li * 4 + r) : 0u;
+                    if (!((blk >> (li * 4 + r)) & 1u))
                         continue;
                     best = min_u32(best, st.best_sad[(li) * 4 + (r)][n]);
                 }
@@ -884,12 +915,12 @@ __device__ void finish_sb(St &st, const DevJob &dj, uint32_t sb_local, uint32_t 
             uint8_t c0 = 0;
             for (int li = 0; li < nl && (use || off == 0); ++li)
                 for (int r = 0; r < (li ? nr1 : nr0) && (use || off == 0); ++r) {
-                    if (!blk[li][r])
+                    if (!((blk >> (li * 4 + r)) & 1u))
                         continue;
                     if (prune_th > 0) {
                         const uint32_t dd = (st.best_sad[(li) * 4 + (r)][n] - best) * 100;
                         if (dd > best * prune_th) {
-                            blk[li][r] = 0;
+                            blk &= ~(1u << (li * 4 + r));
                             continue;
                         }
                     }
@@ -907,7 +938,7 @@ __device__ void finish_sb(St &st, const DevJob &dj, uint32_t sb_local, uint32_t 
                     for (int b2 = 0; b2 < nr1; b2++) {
                         if (job.only_l_bwd && (a2 > 0 || b2 > 0))
                             continue;
-                        if (blk[0][a2] && blk[1][b2]) {
+                        if (((blk >> (0 * 4 + a2)) & 1u) && ((blk >> (1 * 4 + b2)) & 1u)) {
                             const uint8_t cb = mk_cand(2, a2, b2, 0, 1);
                             if (off == 0)
                                 c0 = cb;
@@ -916,13 +947,13 @@ __device__ void finish_sb(St &st, const DevJob &dj, uint32_t sb_local, uint32_t 
                     }
                 if (!job.only_l_bwd)
                     for (int a2 = 1; a2 < nr0; a2++)
-                        if (blk[0][0] && blk[0][a2]) {
+                        if (((blk >> (0 * 4 + 0)) & 1u) && ((blk >> (0 * 4 + a2)) & 1u)) {
                             const uint8_t cb = mk_cand(2, 0, a2, 0, 0);
                             if (off == 0)
                                 c0 = cb;
                             o->me_candidate_array[pu][off++] = cb;
                         }
-                if (!job.only_l_bwd && nr1 == 3 && blk[1][0] && blk[1][2]) {
+                if (!job.only_l_bwd && nr1 == 3 && ((blk >> (1 * 4 + 0)) & 1u) && ((blk >> (1 * 4 + 2)) & 1u)) {
                     const uint8_t cb = mk_cand(2, 0, 2, 1, 1);
                     if (off == 0)
                         c0 = cb;
@@ -959,7 +990,7 @@ __device__ void finish_sb(St &st, const DevJob &dj, uint32_t sb_local, uint32_t 
         // perform_gm_detection (motion_estimation.c:2838-2961)
         if (job.gm_enabled) {
             uint64_t stationary = 0, tot = 0;
-            uint32_t cnt[2][4][2][2];
+            uint32_t(*cnt)[4][2][2] = st.gm_cnt;
             for (int a2 = 0; a2 < 2; a2++)
                 for (int b2 = 0; b2 < 4; b2++)
                     for (int cc = 0; cc < 2; cc++) cnt[a2][b2][cc][0] = cnt[a2][b2][cc][1] = 0;

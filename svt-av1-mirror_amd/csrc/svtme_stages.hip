@@ -1,0 +1,1401 @@
+// svtme_stages.hip — open-loop motion estimation as three stage kernels (gfx950).
+//
+// svt_aom_motion_estimation_b64 (reference motion_estimation.c:3076-3153) runs
+// per 64x64 superblock (SB) as a chain of dependent searches. On MI355X the
+// chain is executed stage-major over the whole picture so every stage is a
+// wide, high-occupancy launch and no workgroup idles on a dependency:
+//
+//   k_stage_a  one wavefront per independent search of every SB: zz SAD
+//              (init_zz_sad), both pre-HME regions of every reference of both
+//              lists, and the four HME level-0 quadrants. None of these
+//              searches depends on another's result; whether the reference
+//              would have skipped one is decided afterwards from the same
+//              data (stage B), so skipped searches are simply not read.
+//   k_stage_b  one workgroup per SB: the zz / pre-HME / level-0 decisions in
+//              reference order, HME level 1 (and 2), search-centre selection
+//              and HME pruning (set_final_seach_centre_sb,
+//              hme_prune_ref_and_adjust_sr).
+//   k_stage_c  one workgroup per SB: integer_search_b64 (check_00_center,
+//              8x8-variance probe, full-pel search with the 85-PU argmin),
+//              me_prune_ref, the per-reference records and the candidate
+//              arrays / distortions / GM detection.
+//
+// SAD primitive: v_qsad_pk_u16_u8 gives the SADs of 4 consecutive positions
+// for one source dword. Positions are grouped in quads aligned to the
+// reference plane's dword grid, so every load is a plain aligned dword load
+// and no byte realignment is ever needed; positions of a quad outside the
+// search area are masked out of the argmin. Argmins use 64-bit keys
+// (sad << 32 | y << 16 | x, or sad << 32 | raster order) so the reference's
+// strict-< first-minimum scan order (compute_sad_c.c:90,
+// motion_estimation.c:137-425) falls out of an integer min.
+#include <type_traits>
+
+#include "svtme_me_common.h"
+
+namespace svtme {
+
+// ----------------------------------------------------------------------------
+// Wavefront SAD searches (sad_loop, compute_sad_c.c:58-101)
+// ----------------------------------------------------------------------------
+// rows [k0, k1) of an ND-dword block row for the 4 positions of an aligned quad
+template <int ND>
+__device__ __forceinline__ void rows_qsad(const uint32_t *rp, int bstride_dw, const uint8_t *src, int src_stride,
+                                          int k0, int k1, uint32_t acc[4]) {
+    constexpr int CH = 64 / ND; // u16 lanes: ND * 1020 * CH <= 65280
+    for (int kc = k0; kc < k1; kc += CH) {
+        const int ke         = min(k1, kc + CH);
+        unsigned long long a = 0;
+#pragma unroll 2
+        for (int k = kc; k < ke; k++) {
+            const uint32_t *rd = rp + k * bstride_dw;
+            const uint32_t *sd = (const uint32_t *)(src + k * src_stride);
+            uint32_t d[ND + 1];
+#pragma unroll
+            for (int j = 0; j <= ND; j++) d[j] = rd[j];
+#pragma unroll
+            for (int j = 0; j < ND; j++) a = qsad(d[j], d[j + 1], sd[j], a);
+        }
+        qsad_unpack(a, acc);
+    }
+}
+
+// any block width (partial last dword masked): v_sad_u8 on the 4 byte shifts
+__device__ __forceinline__ void rows_sad_any(const uint32_t *rp, int bstride_dw, const uint8_t *src, int src_stride,
+                                             int bw, int k0, int k1, uint32_t acc[4]) {
+    const int nd             = (bw + 3) >> 2;
+    const uint32_t last_mask = (bw & 3) ? ((1u << (8 * (bw & 3))) - 1u) : 0xFFFFFFFFu;
+    for (int k = k0; k < k1; k++) {
+        const uint32_t *rd = rp + k * bstride_dw;
+        const uint8_t *sb  = src + k * src_stride;
+        uint32_t d0        = rd[0];
+        for (int j = 0; j < nd; j++) {
+            const uint32_t d1 = rd[j + 1];
+            const uint32_t m  = (j == nd - 1) ? last_mask : 0xFFFFFFFFu;
+            const uint32_t s  = *(const uint32_t *)(sb + 4 * j) & m;
+            acc[0] = __builtin_amdgcn_sad_u8(d0 & m, s, acc[0]);
+            acc[1] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d1, d0, 1) & m, s, acc[1]);
+            acc[2] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d1, d0, 2) & m, s, acc[2]);
+            acc[3] = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d1, d0, 3) & m, s, acc[3]);
+            d0 = d1;
+        }
+    }
+}
+
+// One sad_loop over plane p, executed by the calling wavefront (all arguments
+// wave-uniform): window top-left (plane coords) (wx, wy), search area
+// sa_w x sa_h, block bw x bh_eff rows (sub: block rows 2 plane rows apart),
+// source block at src (stride src_stride between block rows). Returns the
+// wave-uniform best key (sad << 32 | y << 16 | x), ~0 if nothing searched.
+__device__ unsigned long long wave_sad_task(const uint8_t *pbase, int pstride, int wx, int wy, int sa_w, int sa_h,
+                                            int bw, int bh_eff, bool sub, bool skip_flag, const uint8_t *src,
+                                            int src_stride) {
+    const int lane  = threadIdx.x & 63;
+    const bool skip = skip_flag && bw == 16 && bh_eff <= 16; // compute_sad_c.c:74
+    const int nrows = (sa_w > 0 && sa_h > 0) ? (skip ? sa_h / 2 : sa_h) : 0;
+    if (nrows <= 0 || bh_eff <= 0)
+        return ~0ull;
+    const uint8_t *w0  = pbase + (ptrdiff_t)wy * pstride + wx;
+    const int sh       = (int)((uintptr_t)w0 & 3);
+    const uint32_t *a0 = (const uint32_t *)(w0 - sh);
+    const int nq       = (sh + sa_w + 3) >> 2; // dword-aligned position quads
+    const int sdw      = pstride >> 2;
+    const int bstr     = sub ? 2 * sdw : sdw;
+    const int quads    = nrows * nq;
+    int lg             = 0; // 2^lg lanes share a quad, splitting its block rows
+    while ((2 << lg) <= bh_eff && quads * (2 << lg) <= 64) lg++;
+    const int G = 1 << lg, per = (bh_eff + G - 1) >> lg, nitems = quads << lg;
+    const uint32_t mnq = magic_u32((uint32_t)nq);
+    const int mode     = (bw & 3) ? 0 : (bw == 16 ? 4 : (bw == 32 ? 8 : (bw == 64 ? 16 : (bw == 8 ? 2 : 0))));
+    unsigned long long best = ~0ull;
+    for (int base = 0; base < nitems; base += 64) {
+        const int i  = base + lane;
+        const int g  = i & (G - 1), qi = i >> lg;
+        const int yy = mdiv(qi, mnq), q = qi - yy * nq;
+        const int y  = skip ? 2 * yy + 1 : yy;
+        uint32_t acc[4] = {0, 0, 0, 0};
+        if (i < nitems) {
+            const int k0 = min(bh_eff, g * per), k1 = min(bh_eff, k0 + per);
+            const uint32_t *rp = a0 + (ptrdiff_t)y * sdw + q;
+            switch (mode) {
+            case 2: rows_qsad<2>(rp, bstr, src, src_stride, k0, k1, acc); break;
+            case 4: rows_qsad<4>(rp, bstr, src, src_stride, k0, k1, acc); break;
+            case 8: rows_qsad<8>(rp, bstr, src, src_stride, k0, k1, acc); break;
+            case 16: rows_qsad<16>(rp, bstr, src, src_stride, k0, k1, acc); break;
+            default: rows_sad_any(rp, bstr, src, src_stride, bw, k0, k1, acc); break;
+            }
+        }
+        for (int o = 1; o < G; o <<= 1)
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc[k] += __shfl_xor(acc[k], o, 64);
+        if (i < nitems && g == 0) {
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const int x = 4 * q - sh + s;
+                if (x >= 0 && x < sa_w) {
+                    const unsigned long long kk =
+                        ((unsigned long long)acc[s] << 32) | ((uint32_t)y << 16) | (uint32_t)x;
+                    best = kk < best ? kk : best;
+                }
+            }
+        }
+    }
+    return wave_min_u64(best);
+}
+
+// sad_loop output: best_sad starts at 0xffffff; the centre stays (0,0) unless
+// a position beats it (compute_sad_c.c:71, :90)
+__device__ __forceinline__ void key_result(unsigned long long k, uint32_t *best, int *x, int *y) {
+    const uint32_t sad = (uint32_t)(k >> 32);
+    if (k != ~0ull && sad < 0xffffffu) {
+        *best = sad;
+        *x    = (int)(int16_t)(k & 0xFFFF);
+        *y    = (int)(int16_t)((k >> 16) & 0xFFFF);
+    } else {
+        *best = 0xffffff;
+        *x = *y = 0;
+    }
+}
+
+// n x m SAD (compute_sad_c.c:20-37) of a width x rows block, by one wavefront;
+// ref may be unaligned, cur is dword aligned
+__device__ uint32_t wave_nxm(const uint8_t *ref, int rstride, const uint8_t *cur, int cstride, int rows, int width) {
+    const int lane     = threadIdx.x & 63;
+    const int wd4      = (width + 3) >> 2;
+    const uint32_t mwd = magic_u32((uint32_t)wd4);
+    const int sh       = (int)((uintptr_t)ref & 3);
+    uint32_t acc       = 0;
+    for (int e = lane; e < rows * wd4; e += 64) {
+        const int r = mdiv(e, mwd), j = e - r * wd4;
+        const uint32_t *da = (const uint32_t *)(ref + (ptrdiff_t)r * rstride - sh) + j;
+        uint32_t run       = __builtin_amdgcn_alignbyte(da[1], da[0], sh);
+        uint32_t s         = *((const uint32_t *)(cur + (ptrdiff_t)r * cstride) + j);
+        const int valid    = width - 4 * j;
+        if (valid < 4) {
+            const uint32_t m = (1u << (8 * valid)) - 1u;
+            run &= m;
+            s &= m;
+        }
+        acc = __builtin_amdgcn_sad_u8(run, s, acc);
+    }
+    return wave_sum_u32(acc);
+}
+
+// SB geometry of a picture-local SB index
+struct SbGeo {
+    uint32_t ox, oy, bw, bh;
+};
+__device__ __forceinline__ SbGeo sb_geo(const DevJob &dj, uint32_t sb_local) {
+    const uint32_t b64 = dj.job.sb_begin + sb_local;
+    SbGeo g;
+    g.ox = (b64 % dj.pic_w_b64) * 64;
+    g.oy = (b64 / dj.pic_w_b64) * 64;
+    g.bw = (dj.job.width - g.ox) < 64 ? dj.job.width - g.ox : 64;
+    g.bh = (dj.job.height - g.oy) < 64 ? dj.job.height - g.oy : 64;
+    return g;
+}
+
+// XCD-aware block order: blocks b and b + 8 share an XCD (round-robin
+// dispatch), so each XCD gets one contiguous band of work whose reference
+// windows overlap in its L2 (bijective for any grid size)
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
+    const uint32_t xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
+
+// per-slot reference planes into LDS with constant-index argument reads
+template <int NLV>
+__device__ __forceinline__ void copy_planes(const DevJob &dj, DevPlane (*pl)[NLV], uint16_t *dist) {
+#pragma unroll
+    for (int s = 0; s < 8; s++) {
+#pragma unroll
+        for (int v = 0; v < NLV; v++) pl[s][v] = dj.ref[s >> 2][s & 3].lv[v];
+        dist[s] = ref_dist_const(dj.job, s >> 2, s & 3);
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Stage A: every independent search of every SB, one wavefront each
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_stage_a(const DevJob dj) {
+    __shared__ DevPlane pl[8][3];
+    __shared__ uint16_t dist[8];
+    __shared__ __attribute__((aligned(16))) uint8_t srcb[4][256];
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid == 0)
+        copy_planes<3>(dj, pl, dist);
+    __syncthreads();
+    const uint32_t total = job.sb_count * dj.ta_count;
+    const uint32_t gw    = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (gw >= total)
+        return;
+    const uint32_t sb_local = UNI(gw / dj.ta_count);
+    const int t             = UNI(dj.ta_list[gw - sb_local * dj.ta_count]);
+    const SbGeo G           = sb_geo(dj, sb_local);
+    ARes *out               = dj.ares + (size_t)sb_local * SVTME_A_N + t;
+    const bool hsub         = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
+    if (t < SVTME_A_PH) { // zz SAD (init_zz_sad, motion_estimation.c:2382-2437)
+        const int s       = t;
+        const DevPlane &P = pl[s][0];
+        const DevPlane &C = dj.cur.lv[0];
+        const uint32_t v  = wave_nxm(P.base + (ptrdiff_t)G.oy * P.stride + G.ox, 2 * P.stride,
+                                     C.base + (ptrdiff_t)G.oy * C.stride + G.ox, 2 * C.stride, (int)(G.bh >> 1),
+                                     (int)G.bw);
+        if (lane == 0)
+            *out = ARes{v, 0, 0};
+        return;
+    }
+    // sixteenth-resolution source block (16 x 16) into this wave's LDS slot
+    {
+        const DevPlane &S = dj.cur.lv[2];
+        if (lane < 16)
+            ((uint4 *)srcb[wid])[lane] =
+                *(const uint4 *)(S.base + (ptrdiff_t)((G.oy >> 2) + lane) * S.stride + (G.ox >> 2));
+    }
+    __builtin_amdgcn_s_waitcnt(0); // wave-local LDS hand-off (no other wave reads srcb[wid])
+    __builtin_amdgcn_wave_barrier();
+    const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
+    const int bws = (int)(G.bw >> 2), bhs = hsub ? (int)(G.bh >> 2) >> 1 : (int)(G.bh >> 2);
+    int16_t xo, yo, sw, shh;
+    int skip = 0, mul = 4;
+    int s;
+    if (t < SVTME_A_L0) { // pre-HME region (prehme_core, motion_estimation.c:1568-1636)
+        s            = (t - SVTME_A_PH) >> 1;
+        const int sr = (t - SVTME_A_PH) & 1;
+        const uint32_t f = scaled_dist(dist[s]);
+        const uint16_t sa_w = (uint16_t)min((uint32_t)c.prehme_sa_cfg[sr].sa_min.width * f,
+                                            (uint32_t)c.prehme_sa_cfg[sr].sa_max.width);
+        const uint16_t sa_h = (uint16_t)min((uint32_t)c.prehme_sa_cfg[sr].sa_min.height * f,
+                                            (uint32_t)c.prehme_sa_cfg[sr].sa_max.height);
+        prehme_area(pl[s][2], sox, soy, (int16_t)sa_w, (int16_t)sa_h, &xo, &yo, &sw, &shh);
+        skip = c.prehme_skip_search_line;
+    } else { // HME level-0 quadrant (hme_level_0, motion_estimation.c:835-889)
+        s           = (t - SVTME_A_L0) >> 2;
+        const int q = (t - SVTME_A_L0) & 3;
+        int16_t sa_w, sa_h;
+        hme_l0_area(c, s >> 2, s & 3, dist[s], 0, 0, &sa_w, &sa_h);
+        hme_l0_rect(c, pl[s][2], sox, soy, sa_w, sa_h, q >> 1, q & 1, &xo, &yo, &sw, &shh);
+    }
+    const DevPlane &P = pl[s][2];
+    const unsigned long long k =
+        wave_sad_task(P.base, P.stride, sox + xo, soy + yo, sw, shh, bws, bhs, hsub, skip, srcb[wid], hsub ? 32 : 16);
+    if (lane == 0) {
+        uint32_t best;
+        int x, y;
+        key_result(k, &best, &x, &y);
+        *out = ARes{hsub ? best * 2 : best, i16((x + xo) * mul), i16((y + yo) * mul)};
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Stage B: decisions of stage A in reference order, HME level 1 / 2, search
+// centre and HME pruning; one workgroup per SB
+// ----------------------------------------------------------------------------
+struct PreHme {
+    uint64_t sad;
+    int16_t col, row;
+    uint8_t valid, performed;
+    uint8_t pad[2];
+};
+
+struct BTask {
+    int16_t wx, wy, sa_w, sa_h;
+    int16_t xo, yo;
+    uint8_t slot, q;
+    uint8_t pad[2];
+};
+
+struct StB {
+    ARes a[SVTME_A_N];
+    DevPlane pl[8][3];
+    uint16_t dist[8];
+    uint32_t zz[8];
+    uint8_t do_ref[8];
+    PreHme ph[8][2];
+    int16_t lx[3][8][4], ly[3][8][4]; // [level][slot][q = sx * 2 + sy]
+    uint64_t lsad[3][8][4];
+    BTask bt[32];
+    unsigned long long bkey[32];
+    int32_t nbt;
+    __attribute__((aligned(16))) uint8_t src[64 * 64];
+};
+
+__global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
+    __shared__ StB st;
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool w0           = wid == 0;
+    const uint32_t sb_local = xcd_remap(blockIdx.x, gridDim.x);
+    const SbGeo G           = sb_geo(dj, sb_local);
+    const uint32_t ox = G.ox, oy = G.oy, bw = G.bw, bh = G.bh;
+    const int nl     = job.num_lists;
+    const bool hsub  = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
+    const uint32_t vmask = valid_mask(job);
+
+    if (tid < SVTME_A_N)
+        st.a[tid] = dj.ares[(size_t)sb_local * SVTME_A_N + tid];
+    if (tid == 0)
+        copy_planes<3>(dj, st.pl, st.dist);
+    if (tid < 8) { // init_me_hme_data (motion_estimation.c:3010-3070)
+        st.do_ref[tid] = 1;
+        st.zz[tid]     = U32MAX;
+        for (int k = 0; k < 2; k++) {
+            st.ph[tid][k].valid     = 0;
+            st.ph[tid][k].performed = 0;
+            st.ph[tid][k].sad       = 0;
+            st.ph[tid][k].col = st.ph[tid][k].row = 0;
+        }
+    }
+    if (tid < 96) {
+        (&st.lx[0][0][0])[tid]   = 0;
+        (&st.ly[0][0][0])[tid]   = 0;
+        (&st.lsad[0][0][0])[tid] = 0;
+    }
+    if (c.enable_hme_flag && c.enable_hme_level1_flag && tid < 64) { // quarter source block 32 x 32
+        const DevPlane &Q = dj.cur.lv[1];
+        const int r = tid >> 1, j = tid & 1;
+        ((uint4 *)st.src)[tid] = *(const uint4 *)(Q.base + (ptrdiff_t)((oy >> 1) + r) * Q.stride + (ox >> 1) + 16 * j);
+    }
+    __syncthreads();
+
+    if (w0) {
+        // ---- init_zz_sad decisions (motion_estimation.c:2382-2437)
+        if (c.me_early_exit_th || c.me_safe_limit_zz_th) {
+            const int s = lane;
+            uint32_t zz = U32MAX;
+            const bool have = slot_valid(vmask, s) && tl_or_l0(job, s >> 2);
+            if (have) {
+                zz       = st.a[SVTME_A_ZZ + s].sad << 1;
+                zz       = (zz * 64 * 64) / (bw * bh);
+                st.zz[s] = zz;
+            }
+            const uint32_t best = wave_min_u32(zz);
+            if (have && (s & 3) > 0 && job.temporal_layer_index > 0 && best < c.zz_sad_th &&
+                (uint32_t)((zz - best) * 100u) > (uint32_t)(c.zz_sad_pct * best))
+                st.do_ref[s] = 0;
+            if (c.me_safe_limit_zz_th) {
+                const bool safe = job.hierarchical_levels > 0 && nl == 2 &&
+                    job.temporal_layer_index >= job.hierarchical_levels && job.similar_brightness_refs &&
+                    st.zz[0] < c.me_safe_limit_zz_th && st.zz[4] < c.me_safe_limit_zz_th;
+                if (safe && slot_valid(vmask, lane) && (lane & 3) > 0)
+                    st.do_ref[lane] = 0;
+            }
+        }
+        // ---- pre-HME decisions (motion_estimation.c:1693-1796), list 0 then list 1
+        if (c.prehme_enable) {
+            for (int l = 0; l < nl; l++) {
+                const int r = lane >> 1, sr = lane & 1, s = l * 4 + r;
+                if (lane < 8 && slot_valid(vmask, s) && tl_or_l0(job, l)) {
+                    PreHme &d = st.ph[s][sr];
+                    bool done = false;
+                    if (c.me_early_exit_th && st.zz[s] < c.me_early_exit_th) { // check_prehme_early_exit
+                        d.col = d.row = 0;
+                        d.sad   = 0;
+                        d.valid = 1;
+                        done    = true;
+                    }
+                    if (!done && c.prehme_l1_early_exit && l == 1) {
+                        const PreHme &z = st.ph[r][sr];
+                        if (z.valid && ((z.sad < (32 * 32)) || ((absi(z.col) < 16) && (absi(z.row) < 16)))) {
+                            d.col   = (int16_t)-z.col;
+                            d.row   = (int16_t)-z.row;
+                            d.sad   = z.sad;
+                            d.valid = 1;
+                            done    = true;
+                        }
+                    }
+                    if (!done && !st.do_ref[s]) {
+                        d.col = d.row = 0;
+                        d.sad = U32MAX;
+                        done  = true;
+                    }
+                    if (!done) { // searched in stage A
+                        const ARes &a = st.a[SVTME_A_PH + s * 2 + sr];
+                        d.sad         = a.sad;
+                        d.col         = a.x;
+                        d.row         = a.y;
+                        d.valid       = 1;
+                        d.performed   = 1;
+                    }
+                }
+            }
+            uint32_t m  = U32MAX;
+            const int s = lane;
+            if (slot_valid(vmask, s)) {
+                if (tl_or_l0(job, s >> 2)) {
+                    m = (uint32_t)min_u64(st.ph[s][0].sad, st.ph[s][1].sad);
+                } else { // list 1 at the base layer mirrors list 0
+                    for (int k = 0; k < 2; k++) {
+                        st.ph[s][k].col = (int16_t)-st.ph[s & 3][k].col;
+                        st.ph[s][k].row = (int16_t)-st.ph[s & 3][k].row;
+                        st.ph[s][k].sad = st.ph[s & 3][k].sad;
+                    }
+                }
+            }
+            const uint32_t best = wave_min_u32(m);
+            if (job.temporal_layer_index > 0 && best < c.phme_sad_th && slot_valid(vmask, s) && (s & 3) > 0 &&
+                st.do_ref[s] && (uint32_t)((m - best) * 100u) > (uint32_t)(c.phme_sad_pct * best))
+                st.do_ref[s] = 0;
+        }
+        // ---- HME level 0 decisions (motion_estimation.c:1906-2036)
+        if (c.enable_hme_flag && c.enable_hme_level0_flag) {
+            const int s = lane >> 2, q = lane & 3;
+            bool searched = false;
+            if (lane < 32 && slot_valid(vmask, s)) {
+                int16_t &X = st.lx[0][s][q], &Y = st.ly[0][s][q];
+                uint64_t &SD = st.lsad[0][s][q];
+                bool done = false;
+                if (c.me_early_exit_th && st.zz[s] < (c.me_early_exit_th >> 2)) {
+                    X = Y = 0;
+                    SD   = 0;
+                    done = true;
+                }
+                if (!done && c.prev_me_stage_based_exit_th) {
+                    const int k = st.ph[s][0].sad <= st.ph[s][1].sad ? 0 : 1;
+                    if (st.ph[s][k].performed && st.ph[s][k].sad < (c.prev_me_stage_based_exit_th >> 4)) {
+                        X    = st.ph[s][k].col;
+                        Y    = st.ph[s][k].row;
+                        SD   = st.ph[s][k].sad;
+                        done = true;
+                    }
+                }
+                if (!done && !st.do_ref[s]) {
+                    X = Y = 0;
+                    SD   = U32MAX;
+                    done = true;
+                }
+                if (!done && tl_or_l0(job, s >> 2)) {
+                    const ARes &a = st.a[SVTME_A_L0 + s * 4 + q];
+                    X             = a.x;
+                    Y             = a.y;
+                    SD            = a.sad;
+                    searched      = true;
+                }
+            }
+            // pre-HME replaces the worst quadrant of each searched slot (:2005-2032)
+            const unsigned long long sm = __ballot(searched);
+            if (c.prehme_enable && lane < 8 && ((sm >> (4 * lane)) & 0xF)) {
+                const int s2 = lane;
+                uint64_t *S  = st.lsad[0][s2];
+                int wq       = 0; // get_worst_quadrant: strict > in (0,0),(1,0),(0,1),(1,1) order
+                uint64_t mx  = 0;
+                if (S[0] > mx) { mx = S[0]; wq = 0; }
+                if (S[2] > mx) { mx = S[2]; wq = 2; }
+                if (S[1] > mx) { mx = S[1]; wq = 1; }
+                if (S[3] > mx) { wq = 3; }
+                const int k = st.ph[s2][0].sad <= st.ph[s2][1].sad ? 0 : 1;
+                if (st.ph[s2][k].sad < S[wq]) {
+                    S[wq]            = st.ph[s2][k].sad;
+                    st.lx[0][s2][wq] = st.ph[s2][k].col;
+                    st.ly[0][s2][wq] = st.ph[s2][k].row;
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- HME level 1 / 2 (motion_estimation.c:2041-2177)
+    for (int level = 1; level <= 2; level++) {
+        if (!c.enable_hme_flag || (level == 1 && !c.enable_hme_level1_flag) ||
+            (level == 2 && !c.enable_hme_level2_flag))
+            continue;
+        if (level == 2) { // full-resolution source block
+            __syncthreads();
+            const DevPlane &F = dj.cur.lv[0];
+            const int r = tid >> 2, j = tid & 3;
+            ((uint4 *)st.src)[tid] = *(const uint4 *)(F.base + (ptrdiff_t)(oy + r) * F.stride + ox + 16 * j);
+        }
+        if (w0) {
+            const int s = lane >> 2, q = lane & 3;
+            bool mk = false;
+            BTask bt;
+            if (lane < 32 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2)) {
+                int16_t &X = st.lx[level][s][q], &Y = st.ly[level][s][q];
+                uint64_t &SD = st.lsad[level][s][q];
+                bool done = false;
+                if (level == 1) {
+                    if (c.me_early_exit_th && st.zz[s] < (c.me_early_exit_th >> 2)) {
+                        X = Y = 0;
+                        SD   = 0;
+                        done = true;
+                    }
+                    if (!done && !st.do_ref[s]) {
+                        X = Y = 0;
+                        SD   = U32MAX;
+                        done = true;
+                    }
+                    if (!done && c.prev_me_stage_based_exit_th &&
+                        st.lsad[0][s][q] < (c.prev_me_stage_based_exit_th >> 5)) {
+                        X    = st.lx[0][s][q];
+                        Y    = st.ly[0][s][q];
+                        SD   = st.lsad[0][s][q];
+                        done = true;
+                    }
+                } else if (c.prev_me_stage_based_exit_th && st.lsad[1][s][q] < (c.prev_me_stage_based_exit_th >> 2)) {
+                    X    = st.lx[1][s][q];
+                    Y    = st.ly[1][s][q];
+                    SD   = st.lsad[1][s][q];
+                    done = true;
+                }
+                if (!done) {
+                    const DevPlane &P   = st.pl[s][level == 1 ? 1 : 0];
+                    const int16_t cx    = level == 1 ? i16(st.lx[0][s][q] >> 1) : st.lx[1][s][q];
+                    const int16_t cy    = level == 1 ? i16(st.ly[0][s][q] >> 1) : st.ly[1][s][q];
+                    const int16_t qx    = level == 1 ? i16(((int16_t)ox) >> 1) : (int16_t)ox;
+                    const int16_t qy    = level == 1 ? i16(((int16_t)oy) >> 1) : (int16_t)oy;
+                    const svtme_area sa = level == 1 ? c.hme_l1_sa : c.hme_l2_sa;
+                    int16_t xo, yo, sw, sh2;
+                    hme_refine_rect(level, P, qx, qy, (int16_t)sa.width, (int16_t)sa.height, cx, cy, &xo, &yo, &sw,
+                                    &sh2);
+                    bt = BTask{i16(qx + xo), i16(qy + yo), sw, sh2, xo, yo, (uint8_t)s, (uint8_t)q, {0, 0}};
+                    mk = true;
+                }
+            }
+            int tot;
+            const int k = wave_compact(mk, &tot);
+            if (mk)
+                st.bt[k] = bt;
+            if (lane == 0)
+                st.nbt = tot;
+        }
+        __syncthreads();
+        {
+            const int bwl = level == 1 ? (int)(bw >> 1) : (int)bw;
+            const int bhl = level == 1 ? (int)(bh >> 1) : (int)bh;
+            const int sst = (level == 1 ? 32 : 64) * (hsub ? 2 : 1);
+            for (int t = wid; t < st.nbt; t += 4) {
+                const BTask &T    = st.bt[t];
+                const int s       = UNI(T.slot);
+                const DevPlane &P = st.pl[s][level == 1 ? 1 : 0];
+                const unsigned long long k = wave_sad_task(P.base, P.stride, UNI(T.wx), UNI(T.wy), UNI(T.sa_w),
+                                                           UNI(T.sa_h), bwl, hsub ? bhl >> 1 : bhl, hsub, false,
+                                                           st.src, sst);
+                if (lane == 0)
+                    st.bkey[t] = k;
+            }
+        }
+        __syncthreads();
+        if (w0 && lane < st.nbt) {
+            const BTask &T = st.bt[lane];
+            const int s = T.slot, q = T.q;
+            uint32_t best;
+            int x, y;
+            key_result(st.bkey[lane], &best, &x, &y);
+            const int mul          = level == 1 ? 2 : 1;
+            st.lsad[level][s][q]   = hsub ? (uint64_t)best * 2 : best;
+            st.lx[level][s][q]     = i16((x + T.xo) * mul);
+            st.ly[level][s][q]     = i16((y + T.yo) * mul);
+        }
+        __syncthreads();
+    }
+
+    // ---- set_final_seach_centre_sb (motion_estimation.c:2182-2380) + hme_prune_ref_and_adjust_sr (:2477-2518)
+    if (w0) {
+        const int s      = lane;
+        const bool valid = slot_valid(vmask, s);
+        int lvl          = -1;
+        if (c.enable_hme_level0_flag && !c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
+            lvl = 0;
+        if (c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
+            lvl = 1;
+        if (c.enable_hme_level2_flag)
+            lvl = 2;
+        const bool hme_slot = valid && tl_or_l0(job, s >> 2) && c.enable_hme_flag;
+        int16_t hx = 0, hy = 0;
+        uint64_t hs    = 0;
+        const bool own = hme_slot && lvl >= 0;
+        if (own) {
+            const int16_t *X = st.lx[lvl][s], *Y = st.ly[lvl][s];
+            const uint64_t *S = st.lsad[lvl][s];
+            hx = X[0], hy = Y[0], hs = S[0];
+            // scan order (w, h): (1,0), (0,1), (1,1) = q 2, 1, 3
+            if (S[2] < hs) { hx = X[2]; hy = Y[2]; hs = S[2]; }
+            if (S[1] < hs) { hx = X[1]; hy = Y[1]; hs = S[1]; }
+            if (S[3] < hs) { hx = X[3]; hy = Y[3]; hs = S[3]; }
+        }
+        // the reference carries function-scope values across slots
+        int16_t cx = 0, cy = 0, scx = 0, scy = 0;
+        uint64_t cs = 0;
+        int16_t my_scx = 0, my_scy = 0;
+        uint64_t my_hs = 0;
+        for (int k = 0; k < 8; k++) {
+            if (!((vmask >> k) & 1u))
+                continue;
+            const bool ok = __shfl((int)own, k, 64) != 0;
+            const bool hk = __shfl((int)hme_slot, k, 64) != 0;
+            const bool tk = tl_or_l0(job, k >> 2);
+            const int16_t kx = (int16_t)__shfl((int)hx, k, 64), ky = (int16_t)__shfl((int)hy, k, 64);
+            const uint64_t ks = __shfl(hs, k, 64);
+            if (ok) {
+                cx = kx, cy = ky, cs = ks;
+            }
+            if (tk) {
+                if (hk) {
+                    scx = cx;
+                    scy = cy;
+                }
+            } else {
+                scx = 0;
+                scy = 0;
+            }
+            if (lane == k) {
+                my_scx = scx, my_scy = scy, my_hs = cs;
+            }
+        }
+        uint64_t hsad = U32MAX; // SearchResults init (hme_sad = MAX_U32)
+        if (valid)
+            hsad = my_hs;
+        uint32_t rdiv = 1;
+        uint8_t dref  = s < 8 ? st.do_ref[s] : 0;
+        if (c.enable_hme_flag) { // prune_ref = enable_hme_flag && me_type != ME_MCTF
+            const uint16_t th = c.prune_ref_if_hme_sad_dev_bigger_than_th;
+            if (c.enable_me_hme_ref_pruning && th != (uint16_t)~0) {
+                const uint64_t best = wave_min_u64(s < 8 ? hsad : ~0ull);
+                if (s < 8 && (s & 3) >= 1 && (hsad - best) * 100 > (th * best))
+                    dref = 0;
+            }
+            if (c.enable_me_sr_adjustment && s < 8) {
+                if (absi(my_scx) <= c.reduce_me_sr_based_on_mv_length_th &&
+                    absi(my_scy) <= c.reduce_me_sr_based_on_mv_length_th && hsad < c.stationary_hme_sad_abs_th)
+                    rdiv = c.stationary_me_sr_divisor;
+                else if (hsad < c.reduce_me_sr_based_on_hme_sad_abs_th)
+                    rdiv = c.me_sr_divisor_for_low_hme_sad;
+            }
+        }
+        if (s < 8) {
+            BState *b        = dj.bst + sb_local;
+            b->hme_sad[s]    = hsad;
+            b->zz[s]         = st.zz[s];
+            b->reduce_div[s] = rdiv;
+            b->sc_x[s]       = valid ? my_scx : 0;
+            b->sc_y[s]       = valid ? my_scy : 0;
+            b->do_ref[s]     = dref;
+        }
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Stage C: integer full-pel search with the 85-PU argmin, ME pruning, records,
+// candidates; one workgroup per SB
+// ----------------------------------------------------------------------------
+struct FpRef {        // one full-pel search window of a reference slot
+    const uint32_t *a; // dword-aligned address of window row 0 (search row 0)
+    int32_t sdw;       // plane stride in dwords
+    int32_t nitems;    // rows x aligned quads
+    uint32_t mnq;
+    int16_t xo, yo, w, h;
+    int32_t order_base; // 0: 8x8-variance centre probe, 1: main search
+    uint8_t slot, nq, sh, pad;
+};
+
+struct StC {
+    __attribute__((aligned(16))) uint8_t src[64 * 64];
+    DevPlane pl[8][1];
+    uint16_t dist[8];
+    uint64_t refpic[8];
+    uint64_t hme_sad[8];
+    uint32_t zz[8];
+    uint32_t reduce_div[8];
+    int16_t sc_x[8], sc_y[8];
+    uint8_t do_ref[8], searched[8], in_round[8];
+    int16_t is_w[8], is_h[8], is_wb[8], is_hb[8], is_xc[8], is_yc[8];
+    uint64_t is_best_hme[8];
+    const uint8_t *req[16]; // check_00_center n x m requests
+    int32_t req_stride[16];
+    int8_t req_slot[8];
+    uint32_t nxm[16];
+    int32_t nreq, nfp, k32;
+    FpRef fp[8];
+    unsigned long long keys[8][SVTME_PU_COUNT];
+    uint32_t best_sad[8][SVTME_PU_COUNT];
+    uint32_t best_mv[8][SVTME_PU_COUNT];
+    uint32_t me_distortion[SVTME_PU_COUNT];
+    uint8_t cand0[SVTME_PU_COUNT + 3];
+    uint32_t gm_cnt[2][4][2][2];
+};
+
+// Window of one reference: rows h, positions w, dword-aligned quads
+__device__ void make_fp(FpRef &F, const DevPlane &P, uint32_t ox, uint32_t oy, int slot, int16_t xo, int16_t yo,
+                        int16_t w, int16_t h, int order_base) {
+    const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yo) * P.stride + ((int)ox + xo);
+    F.sh             = (uint8_t)((uintptr_t)g & 3);
+    F.a              = (const uint32_t *)(g - F.sh);
+    F.sdw            = P.stride >> 2;
+    F.slot           = (uint8_t)slot;
+    F.xo = xo, F.yo = yo, F.w = w, F.h = h;
+    F.order_base = order_base;
+    F.nq         = (uint8_t)((F.sh + w + 3) >> 2);
+    F.mnq        = magic_u32(F.nq);
+    F.nitems     = (int)h * F.nq;
+}
+
+// Full-pel search of the planned windows (motion_estimation.c:98-425, 781-817):
+// lane = 8x8 block in Z-order; one item = one aligned position quad of a
+// search row; 16x16 / 32x32 / 64x64 SADs are DPP lane sums. Keys are
+// (sad << 12 | order) in 32 bits when every order < 4096 (64x64 SAD < 2^20),
+// else (sad << 32 | order).
+template <bool SUB, bool K32>
+__device__ void fullpel_run(StC &st) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int z16 = lane >> 2, k4 = lane & 3;
+    const int by = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
+    const int bx = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1;
+    typedef typename std::conditional<K32, uint32_t, unsigned long long>::type key_t;
+    for (int e = tid; e < st.nfp * SVTME_PU_COUNT; e += 256) {
+        const int f = e / SVTME_PU_COUNT;
+        st.keys[st.fp[f].slot][e - f * SVTME_PU_COUNT] = ~0ull;
+    }
+    uint32_t src[ROWS][2];
+#pragma unroll
+    for (int r = 0; r < ROWS; r++) {
+        const uint32_t *s = (const uint32_t *)(st.src + (by * 8 + r * RSTEP) * 64 + bx * 8);
+        src[r][0] = s[0];
+        src[r][1] = s[1];
+    }
+    __syncthreads();
+    const int nfp = st.nfp;
+    for (int f = 0; f < nfp; f++) {
+        const FpRef &F   = st.fp[f];
+        const int nitems = UNI(F.nitems);
+        if (wid >= nitems)
+            continue; // wave-uniform
+        const int nq = UNI(F.nq), w = UNI(F.w), obase = UNI(F.order_base), sdw = UNI(F.sdw), sh = UNI(F.sh);
+        const uint32_t mnq = (uint32_t)UNI(F.mnq);
+        const uint32_t *ab = F.a + (ptrdiff_t)(by * 8) * sdw + bx * 2;
+        key_t b8 = (key_t)~0ull, b16 = (key_t)~0ull, b32 = (key_t)~0ull, b64 = (key_t)~0ull;
+        for (int i = wid; i < nitems; i += 4) {
+            const int y = mdiv(i, mnq), q = i - y * nq;
+            const uint32_t *rp = ab + (ptrdiff_t)y * sdw + q;
+            uint32_t d[ROWS][3];
+#pragma unroll
+            for (int rr = 0; rr < ROWS; rr++) {
+                const uint32_t *rd = rp + (ptrdiff_t)(rr * RSTEP) * sdw;
+                d[rr][0] = rd[0];
+                d[rr][1] = rd[1];
+                d[rr][2] = rd[2];
+            }
+            unsigned long long a = 0;
+#pragma unroll
+            for (int rr = 0; rr < ROWS; rr++) {
+                a = qsad(d[rr][0], d[rr][1], src[rr][0], a);
+                a = qsad(d[rr][1], d[rr][2], src[rr][1], a);
+            }
+            uint32_t acc[4] = {0, 0, 0, 0};
+            qsad_unpack(a, acc);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int x = 4 * q - sh + k;
+                if (x < 0 || x >= w)
+                    continue; // wave-uniform
+                const uint32_t s8  = SUB ? acc[k] << 1 : acc[k];
+                const uint32_t s16 = dpp_add<0x4E>(dpp_add<0xB1>(s8));                  // xor 1, xor 2
+                const uint32_t s32 = dpp_add<0x128>(dpp_add<0x124>(s16));               // row_ror 4, 8
+                const uint32_t s64 = dpp_add<0x143, 0xC>(dpp_add<0x142, 0xA>(s32));     // valid in row 3
+                const uint32_t o   = (uint32_t)(obase + y * w + x);
+                if (K32) {
+                    b8  = min_u32((uint32_t)b8, (s8 << 12) | o);
+                    b16 = min_u32((uint32_t)b16, (s16 << 12) | o);
+                    b32 = min_u32((uint32_t)b32, (s32 << 12) | o);
+                    b64 = min_u32((uint32_t)b64, (s64 << 12) | o);
+                } else {
+                    const unsigned long long k8  = ((unsigned long long)s8 << 32) | o;
+                    const unsigned long long k16 = ((unsigned long long)s16 << 32) | o;
+                    const unsigned long long k32 = ((unsigned long long)s32 << 32) | o;
+                    const unsigned long long k64 = ((unsigned long long)s64 << 32) | o;
+                    b8  = k8 < b8 ? k8 : b8;
+                    b16 = k16 < b16 ? k16 : b16;
+                    b32 = k32 < b32 ? k32 : b32;
+                    b64 = k64 < b64 ? k64 : b64;
+                }
+            }
+        }
+        unsigned long long *pk = st.keys[UNI(F.slot)];
+        auto wide = [](key_t kk) -> unsigned long long {
+            if (K32) {
+                const uint32_t v = (uint32_t)kk;
+                return v == 0xFFFFFFFFu ? ~0ull : (((unsigned long long)(v >> 12) << 32) | (v & 0xFFFu));
+            }
+            return (unsigned long long)kk;
+        };
+        atomicMin(&pk[21 + lane], wide(b8));
+        if ((lane & 3) == 0)
+            atomicMin(&pk[5 + (lane >> 2)], wide(b16));
+        if ((lane & 15) == 0)
+            atomicMin(&pk[1 + (lane >> 4)], wide(b32));
+        if (lane == 63)
+            atomicMin(&pk[0], wide(b64));
+    }
+    __syncthreads();
+    // decode: strict-< update of the running best (motion_estimation.c:1366, :137-205)
+    for (int e = tid; e < st.nfp * SVTME_PU_COUNT; e += 256) {
+        const int f = e / SVTME_PU_COUNT, pu = e - f * SVTME_PU_COUNT;
+        const FpRef &F             = st.fp[f];
+        const unsigned long long k = st.keys[F.slot][pu];
+        const uint32_t sad         = (uint32_t)(k >> 32);
+        if (k != ~0ull && sad < st.best_sad[F.slot][pu]) {
+            const int p      = (int)(uint32_t)k - F.order_base;
+            const int16_t my = (int16_t)(F.yo + p / F.w);
+            const int16_t mx = (int16_t)(F.xo + p % F.w);
+            st.best_sad[F.slot][pu] = sad;
+            st.best_mv[F.slot][pu]  = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
+        }
+    }
+    __syncthreads();
+}
+
+template <bool SUB>
+__device__ void fullpel(StC &st) {
+    if (st.k32)
+        fullpel_run<SUB, true>(st);
+    else
+        fullpel_run<SUB, false>(st);
+}
+
+// Candidate arrays + distortions + GM detection for one SB, all threads
+// (motion_estimation.c:2532-3007). Thread n builds Z-order PU n.
+__device__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
+    const svtme_job &job = dj.job;
+    const int tid = threadIdx.x;
+    const int nl = job.num_lists, nr0 = job.num_refs[0], nr1 = nl == 2 ? job.num_refs[1] : 0;
+    svtme_sb_result *o = dj.out_sb + sb_local;
+    uint32_t *ow = (uint32_t *)o; // zero the result (sizeof is a multiple of 4)
+    for (int i = tid; i < (int)(sizeof(svtme_sb_result) / 4); i += 256) ow[i] = 0;
+    __syncthreads();
+    const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
+    const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
+    if (mode != 2 && tid < npus)
+        o->total_me_candidate_index[tid] = 1; // memset(..., 1, number_of_pus)
+    __syncthreads();
+    if (tid < SVTME_PU_COUNT) {
+        const int n   = tid;
+        const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
+        if (mode == 0) { // construct_me_candidate_array_single_ref
+            const int pu         = c_z_to_raster[n];
+            st.me_distortion[pu] = st.best_sad[0][n];
+            st.cand0[pu]         = 0;
+            if (st.do_ref[0] && use) {
+                o->me_candidate_array[pu][0] = mk_cand(0, 0, 0, 0, 0);
+                o->me_mv_array[pu][0]        = st.best_mv[0][n];
+            }
+        } else if (mode == 1) { // construct_me_candidate_array_mrp_off
+            const int pu        = c_z_to_raster[n];
+            uint32_t nlist      = nl;
+            const uint8_t org0  = st.do_ref[0], org1 = nl == 1 ? 0 : st.do_ref[4];
+            if (nlist < 2 || !st.do_ref[4])
+                nlist = 1;
+            const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
+            uint8_t off  = 0;
+            uint32_t blk = (org0 ? 1u : 0u) | (org1 ? 2u : 0u); // bit li
+            const uint32_t s0 = st.best_sad[0][n], s1 = st.best_sad[4][n];
+            const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
+            st.me_distortion[pu] = best;
+            int min_list         = -1;
+            if (job.ctrl.use_best_unipred_cand_only && (blk & 3u) == 3u)
+                min_list = s0 < s1 ? 0 : 1;
+            uint8_t c0 = 0;
+            for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
+                if (!((blk >> li) & 1u))
+                    continue;
+                if (prune_th > 0) {
+                    const uint32_t dd = (st.best_sad[li * 4][n] - best) * 100;
+                    if (dd > best * prune_th) {
+                        blk &= ~(1u << li);
+                        continue;
+                    }
+                }
+                if (min_list != -1 && min_list != li) {
+                    if (use)
+                        o->me_mv_array[pu][li ? job.max_l0 : 0] = st.best_mv[li * 4][n];
+                    continue;
+                }
+                if (use) {
+                    const uint8_t cb               = mk_cand(li, 0, 0, li == 0 ? li : 24, li == 1 ? li : 24);
+                    o->me_candidate_array[pu][off] = cb;
+                    if (off == 0)
+                        c0 = cb;
+                    o->me_mv_array[pu][li ? job.max_l0 : 0] = st.best_mv[li * 4][n];
+                }
+                off++;
+            }
+            if ((blk & 3u) == 3u && use) {
+                const uint8_t cb               = mk_cand(2, 0, 0, 0, 1);
+                o->me_candidate_array[pu][off] = cb;
+                if (off == 0)
+                    c0 = cb;
+                o->total_me_candidate_index[pu] = (uint8_t)(off + 1);
+            }
+            st.cand0[pu] = c0;
+        } else { // construct_me_candidate_array
+            const int pu = (n > 4) ? c_z_to_raster[n] : n;
+            uint8_t off  = 0;
+            uint32_t blk = 0; // bit li * 4 + r
+            const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
+            uint32_t best = U32MAX;
+            for (int li = 0; li < nl; li++)
+                for (int r = 0; r < (li ? nr1 : nr0); r++) {
+                    if (!st.do_ref[li * 4 + r])
+                        continue;
+                    blk |= 1u << (li * 4 + r);
+                    best = min_u32(best, st.best_sad[li * 4 + r][n]);
+                }
+            st.me_distortion[pu] = best;
+            uint8_t c0 = 0;
+            for (int li = 0; li < nl && (use || off == 0); ++li)
+                for (int r = 0; r < (li ? nr1 : nr0) && (use || off == 0); ++r) {
+                    if (!((blk >> (li * 4 + r)) & 1u))
+                        continue;
+                    if (prune_th > 0) {
+                        const uint32_t dd = (st.best_sad[li * 4 + r][n] - best) * 100;
+                        if (dd > best * prune_th) {
+                            blk &= ~(1u << (li * 4 + r));
+                            continue;
+                        }
+                    }
+                    if (use) {
+                        const uint8_t cb               = mk_cand(li, r, r, li == 0 ? li : 24, li == 1 ? li : 24);
+                        o->me_candidate_array[pu][off] = cb;
+                        if (off == 0)
+                            c0 = cb;
+                        o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.best_mv[li * 4 + r][n];
+                    }
+                    off++;
+                }
+            if (nl == 2 && use) {
+                for (int a2 = 0; a2 < nr0; a2++)
+                    for (int b2 = 0; b2 < nr1; b2++) {
+                        if (job.only_l_bwd && (a2 > 0 || b2 > 0))
+                            continue;
+                        if (((blk >> a2) & 1u) && ((blk >> (4 + b2)) & 1u)) {
+                            const uint8_t cb = mk_cand(2, a2, b2, 0, 1);
+                            if (off == 0)
+                                c0 = cb;
+                            o->me_candidate_array[pu][off++] = cb;
+                        }
+                    }
+                if (!job.only_l_bwd)
+                    for (int a2 = 1; a2 < nr0; a2++)
+                        if ((blk & 1u) && ((blk >> a2) & 1u)) {
+                            const uint8_t cb = mk_cand(2, 0, a2, 0, 0);
+                            if (off == 0)
+                                c0 = cb;
+                            o->me_candidate_array[pu][off++] = cb;
+                        }
+                if (!job.only_l_bwd && nr1 == 3 && ((blk >> 4) & 1u) && ((blk >> 6) & 1u)) {
+                    const uint8_t cb = mk_cand(2, 0, 2, 1, 1);
+                    if (off == 0)
+                        c0 = cb;
+                    o->me_candidate_array[pu][off++] = cb;
+                }
+            }
+            if (use)
+                o->total_me_candidate_index[pu] = off;
+            st.cand0[pu] = use ? c0 : 0;
+        }
+    }
+    __syncthreads();
+    if (tid < SVTME_PU_COUNT)
+        o->me_distortion[tid] = st.me_distortion[tid];
+    // compute_distortion (motion_estimation.c:2964-3007): wave 0, lane-parallel sums
+    if (tid < 64) {
+        const int lane = tid;
+        const uint32_t d8v  = st.me_distortion[21 + lane];
+        const uint32_t d16v = lane < 16 ? st.me_distortion[5 + lane] : 0;
+        const uint32_t d32v = lane < 4 ? st.me_distortion[1 + lane] : 0;
+        const uint32_t d8 = wave_sum_u32(d8v), d16 = wave_sum_u32(d16v), d32 = wave_sum_u32(d32v);
+        const uint32_t d64 = st.me_distortion[0];
+        const uint64_t mean = d8 / 64;
+        const int64_t diff  = (int64_t)d8v - (int64_t)mean;
+        uint64_t sq         = (uint64_t)(diff * diff);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off, 64);
+        if (lane == 0) {
+            o->me_8x8_cost_variance = (uint32_t)(sq / 64);
+            o->rc_me_distortion     = (job.input_resolution <= 2) ? d8 : d16;
+            const uint32_t pix      = bw * bh;
+            o->me_64x64_distortion  = (d64 * 4096u) / pix;
+            o->me_32x32_distortion  = (d32 * 4096u) / pix;
+            o->me_16x16_distortion  = (d16 * 4096u) / pix;
+            o->me_8x8_distortion    = (d8 * 4096u) / pix;
+        }
+    }
+    // perform_gm_detection (motion_estimation.c:2838-2961)
+    if (job.gm_enabled && tid == 0) {
+        uint64_t stationary = 0, tot = 0;
+        uint32_t(*cnt)[4][2][2] = st.gm_cnt;
+        for (int a2 = 0; a2 < 2; a2++)
+            for (int b2 = 0; b2 < 4; b2++)
+                for (int cc = 0; cc < 2; cc++) cnt[a2][b2][cc][0] = cnt[a2][b2][cc][1] = 0;
+        const bool low  = job.input_resolution <= 2;
+        const int n_blk = low ? 64 : 16;
+        for (int i = 0; i < n_blk; i++) {
+            uint8_t n = (uint8_t)(low ? 21 + i : 5 + i);
+            if (low && !job.enable_me_8x8) {
+                if (n >= 21)
+                    n = c_8x8_to_16x16[n - 21];
+                if (!job.enable_me_16x16 && n >= 5)
+                    n = c_16x16_to_32x32[n - 5];
+            }
+            if (!low && !job.enable_me_16x16 && n >= 5)
+                n = c_16x16_to_32x32[n - 5];
+            const uint8_t cb = st.cand0[n];
+            const int dir = cb & 3, r0 = (cb >> 2) & 3, r1 = (cb >> 4) & 3, l0 = (cb >> 6) & 1, l1 = (cb >> 7) & 1;
+            const int li = (dir == 0 || dir == 2) ? l0 : l1;
+            const int ri = (dir == 0 || dir == 2) ? r0 : r1;
+            int active_th;
+            if (low) {
+                const uint64_t a2 = job.picture_number, b2 = st.refpic[li * 4 + ri];
+                const uint16_t dist = (uint16_t)absi((int16_t)((a2 > b2 ? a2 : b2) - (a2 < b2 ? a2 : b2)));
+                active_th = job.gm_use_distance_based_active_th ? max(dist >> 1, 4) : 4;
+            } else {
+                const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - st.refpic[li * 4 + ri]));
+                active_th = job.gm_use_distance_based_active_th ? max(dist * 16, 32) : 32;
+            }
+            const uint32_t mv = st.best_mv[li * 4 + ri][n];
+            const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4;
+            if (mx < -active_th)
+                cnt[li][ri][0][0]++;
+            else if (mx > active_th)
+                cnt[li][ri][0][1]++;
+            if (my < -active_th)
+                cnt[li][ri][1][0]++;
+            else if (my > active_th)
+                cnt[li][ri][1][1]++;
+            const int stt = low ? 0 : 4;
+            if (absi(mx) <= stt && absi(my) <= stt)
+                stationary++;
+            tot++;
+        }
+        if (stationary > ((tot * 5) / 100))
+            o->stationary_block_present = 1;
+        for (int a2 = 0; a2 < 2; a2++)
+            for (int b2 = 0; b2 < 4; b2++)
+                for (int cc = 0; cc < 2; cc++)
+                    for (int s2 = 0; s2 < 2; s2++)
+                        if (cnt[a2][b2][cc][s2] > (tot / 2))
+                            o->rc_me_allow_gm = 1;
+    }
+}
+
+template <bool SUB_ME>
+__global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
+    __shared__ StC st;
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool w0           = wid == 0;
+    const uint32_t sb_local = xcd_remap(blockIdx.x, gridDim.x);
+    const SbGeo G           = sb_geo(dj, sb_local);
+    const uint32_t ox = G.ox, oy = G.oy, bw = G.bw, bh = G.bh;
+    const uint32_t vmask = valid_mask(job);
+
+    { // full-resolution source block (me_process.c:183-214)
+        const DevPlane &F = dj.cur.lv[0];
+        const int r = tid >> 2, j = tid & 3;
+        ((uint4 *)st.src)[tid] = *(const uint4 *)(F.base + (ptrdiff_t)(oy + r) * F.stride + ox + 16 * j);
+    }
+    if (tid == 0) {
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            st.pl[s][0]  = dj.ref[s >> 2][s & 3].lv[0];
+            st.dist[s]   = ref_dist_const(job, s >> 2, s & 3);
+            st.refpic[s] = job.ref_picture_number[s >> 2][s & 3];
+        }
+    }
+    if (tid < 8) {
+        const BState *b    = dj.bst + sb_local;
+        st.hme_sad[tid]    = b->hme_sad[tid];
+        st.zz[tid]         = b->zz[tid];
+        st.reduce_div[tid] = b->reduce_div[tid];
+        st.sc_x[tid]       = b->sc_x[tid];
+        st.sc_y[tid]       = b->sc_y[tid];
+        st.do_ref[tid]     = b->do_ref[tid];
+        st.searched[tid]   = b->do_ref[tid];
+    }
+    for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) (&st.best_mv[0][0])[e] = 0;
+    __syncthreads();
+
+    // ---- integer_search_b64 (motion_estimation.c:1249-1516); lane s of wave 0 owns slot s.
+    // Two rounds when enable_me_sr_adjustment == 2: the other slots read slot 0's 64x64 SAD.
+    const int rounds = c.enable_me_sr_adjustment == 2 ? 2 : 1;
+    for (int round = 0; round < rounds; round++) {
+        if (w0) { // search area up to the 8x8-variance decision
+            const int s = lane, l = s >> 2, r = s & 3;
+            const bool act = slot_valid(vmask, s) && (rounds == 1 || ((s == 0) == (round == 0))) && st.do_ref[s];
+            bool need = false;
+            if (act) {
+                int16_t xc = st.sc_x[s], yc = st.sc_y[s];
+                int16_t w = (int16_t)c.me_sa.sa_min.width, h = (int16_t)c.me_sa.sa_min.height;
+                const uint16_t dist = scaled_dist(st.dist[s]);
+                w = i16(min((int)(w * dist), (int)c.me_sa.sa_max.width));
+                h = i16(min((int)(h * dist), (int)c.me_sa.sa_max.height));
+                if (c.mv_sa_adj_enabled && (!c.mv_sa_adj_nearest_ref_only || r == 0)) {
+                    if (absi(xc) > c.mv_sa_adj_mv_size_th)
+                        w = i16(w * c.mv_sa_adj_sa_multiplier);
+                    if (absi(yc) > c.mv_sa_adj_mv_size_th)
+                        h = i16(h * c.mv_sa_adj_sa_multiplier);
+                }
+                w = i16((max(1u, ((uint32_t)(int32_t)w / st.reduce_div[s])) + 7) & ~0x07u);
+                h = i16(max(3u, ((uint32_t)(int32_t)h / st.reduce_div[s])));
+                st.is_wb[s]       = w;
+                st.is_hb[s]       = h;
+                st.is_best_hme[s] = ~0ull;
+                if (c.me_early_exit_th) {
+                    if (st.zz[s] < (c.me_early_exit_th / 6)) {
+                        w = 1;
+                        h = 1;
+                    }
+                } else if ((xc != 0 || yc != 0) && job.is_ref) {
+                    need = true; // check_00_center (motion_estimation.c:1139-1206): clamp the centre
+                    const DevPlane &P = st.pl[s][0];
+                    const int16_t pad = 63, org_x = (int16_t)ox, org_y = (int16_t)oy;
+                    const int16_t pw = i16(P.width), ph = i16(P.height);
+                    xc = ((org_x + xc) < -pad) ? i16(-pad - org_x) : xc;
+                    xc = ((org_x + xc) > pw - 1) ? i16(xc - ((org_x + xc) - (pw - 1))) : xc;
+                    yc = ((org_y + yc) < -pad) ? i16(-pad - org_y) : yc;
+                    yc = ((org_y + yc) > ph - 1) ? i16(yc - ((org_y + yc) - (ph - 1))) : yc;
+                }
+                st.is_w[s]  = w;
+                st.is_h[s]  = h;
+                st.is_xc[s] = xc;
+                st.is_yc[s] = yc;
+            }
+            if (s < 8)
+                st.in_round[s] = act;
+            int tot;
+            const int k = wave_compact(need, &tot);
+            if (need) { // requests [2k] = (0,0), [2k+1] = clamped centre
+                const DevPlane &P = st.pl[s][0];
+                st.req[2 * k]     = P.base + (ptrdiff_t)oy * P.stride + ox;
+                st.req[2 * k + 1] = P.base + (ptrdiff_t)((int)oy + st.is_yc[s]) * P.stride + ((int)ox + st.is_xc[s]);
+                st.req_stride[2 * k] = st.req_stride[2 * k + 1] = 2 * P.stride;
+                st.req_slot[k] = (int8_t)s;
+            }
+            if (lane == 0)
+                st.nreq = tot;
+        }
+        __syncthreads();
+        if (st.nreq) {
+            for (int q = wid; q < 2 * st.nreq; q += 4) {
+                const uint32_t v = wave_nxm(st.req[q], st.req_stride[q], st.src, 128, (int)(bh >> 1), (int)bw);
+                if (lane == 0)
+                    st.nxm[q] = v;
+            }
+            __syncthreads();
+            if (w0 && lane < st.nreq) {
+                const int s             = st.req_slot[lane];
+                const uint32_t zero_sad = st.nxm[2 * lane] << 1, hme_mv_sad = st.nxm[2 * lane + 1] << 1;
+                const uint64_t zc = (uint64_t)zero_sad << 8, hc = (uint64_t)hme_mv_sad << 8;
+                if (min_u64(zc, hc) == zc) {
+                    st.is_xc[s] = 0;
+                    st.is_yc[s] = 0;
+                }
+                st.is_best_hme[s] = hme_mv_sad;
+            }
+        }
+        if (w0) { // sr adjustment level 2, 8x8-variance centre probe setup
+            const int s = lane, l = s >> 2, r = s & 3;
+            const bool act = s < 8 && st.in_round[s];
+            bool probe = false;
+            if (act) {
+                int16_t w = st.is_w[s], h = st.is_h[s];
+                if (!c.me_early_exit_th) {
+                    const int16_t xc0 = st.sc_x[s], yc0 = st.sc_y[s];
+                    uint8_t accurate  = 1;
+                    if ((xc0 != 0 || yc0 != 0) && job.is_ref && st.is_xc[s] == 0 && st.is_yc[s] == 0)
+                        accurate = 0;
+                    if (c.enable_me_sr_adjustment == 2) {
+                        if ((accurate && (st.is_best_hme[s] < (24 * 24))) ||
+                            (job.is_ref && st.hme_sad[s] < (24 * 24)))
+                            h = i16(h / 2);
+                        if ((l || r) && st.best_sad[0][0] < 5000 && h == st.is_hb[s] && w == st.is_wb[s]) {
+                            h = i16(h >> 1);
+                            w = i16(w >> 1);
+                        }
+                    }
+                }
+                st.is_w[s] = w;
+                st.is_h[s] = h;
+                probe      = c.me_8x8_var_enabled && (w * h > 24);
+            }
+            int tot;
+            const int k = wave_compact(probe, &tot);
+            if (probe)
+                make_fp(st.fp[k], st.pl[s][0], ox, oy, s, st.is_xc[s], st.is_yc[s], 1, 1, 0);
+            if (lane == 0) {
+                st.nfp = tot;
+                st.k32 = 1; // a single position
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) {
+            const int s = e / SVTME_PU_COUNT;
+            if (st.in_round[s])
+                (&st.best_sad[0][0])[e] = SVTME_MAX_SAD_VALUE;
+        }
+        if (st.nfp) {
+            fullpel<SUB_ME>(st); // centre probe (motion_estimation.c:1414-1417)
+            // 8x8-variance resize (motion_estimation.c:1418-1438)
+            if (w0 && lane < 8 && st.in_round[lane] && c.me_8x8_var_enabled && (st.is_w[lane] * st.is_h[lane] > 24)) {
+                const int s = lane;
+                int16_t w = st.is_w[s], h = st.is_h[s];
+                const uint32_t mean = st.best_sad[s][0] / 64;
+                uint32_t sum_sq     = 0;
+                for (int i = 0; i < 64; i++) {
+                    const int32_t diff = (int32_t)st.best_sad[s][21 + i] - (int32_t)mean;
+                    sum_sq += (uint32_t)(diff * diff);
+                }
+                const uint32_t var = sum_sq / 64;
+                if (var > c.me_sr_mult2_th) {
+                    w = i16((max(1, w * 3 / 2) + 7) & ~0x7);
+                    h = i16(max(1, h * 3 / 2));
+                }
+                if (var < c.me_sr_div4_th) {
+                    w = i16((max(1, w >> 2) + 7) & ~0x7);
+                    h = i16(max(1, h >> 2));
+                    h = i16(max(3, (int)h));
+                } else if (var < c.me_sr_div2_th) {
+                    w = i16((min((int)w, w >> 1) + 7) & ~0x7);
+                    h = i16(min((int)h, h >> 1));
+                    h = i16(max(3, (int)h));
+                }
+                st.is_w[s] = w;
+                st.is_h[s] = h;
+            }
+        }
+        if (w0) { // final area clamp + main full-pel search (motion_estimation.c:1440-1516)
+            const int s = lane;
+            const bool act = s < 8 && st.in_round[s];
+            int16_t w = 0, h = 0, xo = 0, yo = 0;
+            if (act) {
+                w = st.is_w[s], h = st.is_h[s];
+                const int16_t xc = st.is_xc[s], yc = st.is_yc[s];
+                const int16_t pad = 63, org_x = (int16_t)ox, org_y = (int16_t)oy;
+                const int16_t pic_w = (int16_t)job.width, pic_h = (int16_t)job.height;
+                xo = i16(xc - (w >> 1));
+                yo = i16(yc - (h >> 1));
+                xo = ((org_x + xo) < -pad) ? i16(-pad - org_x) : xo;
+                w  = ((org_x + xo) < -pad) ? i16(w - (-pad - (org_x + xo))) : w;
+                xo = ((org_x + xo) > pic_w - 1) ? i16(xo - ((org_x + xo) - (pic_w - 1))) : xo;
+                w  = ((org_x + xo + w) > pic_w) ? i16(max(1, w - ((org_x + xo + w) - pic_w))) : w;
+                w  = (w < 8) ? w : i16(w & ~0x07);
+                yo = ((org_y + yo) < -pad) ? i16(-pad - org_y) : yo;
+                h  = ((org_y + yo) < -pad) ? i16(h - (-pad - (org_y + yo))) : h;
+                yo = ((org_y + yo) > pic_h - 1) ? i16(yo - ((org_y + yo) - (pic_h - 1))) : yo;
+                h  = (org_y + yo + h > pic_h) ? i16(max(1, h - ((org_y + yo + h) - pic_h))) : h;
+            }
+            int tot;
+            const int k = wave_compact(act, &tot);
+            if (act)
+                make_fp(st.fp[k], st.pl[s][0], ox, oy, s, xo, yo, w, h, 1);
+            const bool k32 = __all(!act || (1 + (int)w * (int)h <= 4096));
+            if (lane == 0) {
+                st.nfp = tot;
+                st.k32 = k32;
+            }
+        }
+        __syncthreads();
+        if (st.nfp)
+            fullpel<SUB_ME>(st);
+    }
+
+    // ---- me_prune_ref (motion_estimation.c:1522-1565)
+    if (c.enable_hme_flag && c.enable_me_hme_ref_pruning && w0) {
+        const int s = lane;
+        uint64_t v  = ~0ull;
+        if (s < 8) {
+            v = st.hme_sad[s];
+            if (slot_valid(vmask, s)) {
+                if (!st.do_ref[s])
+                    v = (uint64_t)SVTME_MAX_SAD_VALUE * 64;
+                else {
+                    uint64_t sum = 0;
+                    for (int i = 0; i < 64; i++) sum += st.best_sad[s][21 + i];
+                    v = sum;
+                }
+                st.hme_sad[s] = v;
+            }
+        }
+        const uint16_t th = c.prune_ref_if_me_sad_dev_bigger_than_th;
+        if (th != (uint16_t)~0) {
+            const uint64_t best = wave_min_u64(v);
+            if (s < 8 && (s & 3) >= 1 && (v - best) * 100 > (th * best))
+                st.do_ref[s] = 0;
+        }
+    }
+    __syncthreads();
+
+    // ---- records (sb_count x R, slots in list-0-then-list-1 order)
+    {
+        svtme_ref_record *out = dj.out_records + (size_t)sb_local * dj.R;
+        const int R = (int)dj.R;
+        for (int k = 0; k < R; k++) { // 704 bytes = 176 dwords per record
+            const int s = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
+            const int w = tid;
+            if (w >= 176)
+                continue;
+            uint32_t v;
+            if (w < 85)
+                v = st.searched[s] ? st.best_sad[s][w] : U32MAX;
+            else if (w < 170)
+                v = st.best_mv[s][w - 85];
+            else if (w == 170)
+                v = (uint32_t)st.hme_sad[s];
+            else if (w == 171)
+                v = (uint32_t)(st.hme_sad[s] >> 32);
+            else if (w == 172)
+                v = (uint32_t)(uint16_t)st.sc_x[s] | ((uint32_t)(uint16_t)st.sc_y[s] << 16);
+            else if (w == 173)
+                v = st.zz[s];
+            else if (w == 174)
+                v = (uint32_t)st.searched[s] | ((uint32_t)st.do_ref[s] << 8);
+            else
+                v = 0;
+            ((uint32_t *)(out + k))[w] = v;
+        }
+    }
+    if (dj.out_sb) {
+        __syncthreads();
+        finish_sb(st, dj, sb_local, bw, bh);
+    }
+}
+
+} // namespace svtme
+
+// Stage-A search list of a job: every independent search the reference may
+// perform for a valid slot (see k_stage_a). Host-side, pure.
+extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count) {
+    const svtme_controls &c = job->ctrl;
+    uint32_t n = 0;
+    for (int s = 0; s < 8; s++) {
+        const int l = s >> 2, r = s & 3;
+        if (l >= job->num_lists || r >= job->num_refs[l])
+            continue;
+        if (!(job->temporal_layer_index > 0 || l == 0))
+            continue;
+        if (c.me_early_exit_th || c.me_safe_limit_zz_th)
+            list[n++] = (uint8_t)(SVTME_A_ZZ + s);
+        if (c.prehme_enable) {
+            list[n++] = (uint8_t)(SVTME_A_PH + s * 2);
+            list[n++] = (uint8_t)(SVTME_A_PH + s * 2 + 1);
+        }
+        if (c.enable_hme_flag && c.enable_hme_level0_flag)
+            for (int q = 0; q < 4; q++) list[n++] = (uint8_t)(SVTME_A_L0 + s * 4 + q);
+    }
+    *count = n;
+}
+
+extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s) {
+    if (dj->ta_count) {
+        const uint32_t waves = sb_count * dj->ta_count;
+        hipLaunchKernelGGL(svtme::k_stage_a, dim3((waves + 3) / 4), dim3(256), 0, s, *dj);
+    }
+    hipLaunchKernelGGL(svtme::k_stage_b, dim3(sb_count), dim3(256), 0, s, *dj);
+    if (dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH)
+        hipLaunchKernelGGL(svtme::k_stage_c<false>, dim3(sb_count), dim3(256), 0, s, *dj);
+    else
+        hipLaunchKernelGGL(svtme::k_stage_c<true>, dim3(sb_count), dim3(256), 0, s, *dj);
+    return hipGetLastError();
+}
