@@ -14,19 +14,27 @@ from collections import defaultdict
 
 def main(out):
     per = defaultdict(list)
+    per_kernel = defaultdict(lambda: defaultdict(list))
     for path in glob.glob(os.path.join(out, "pmc_*", "**", "*counter_collection.csv"), recursive=True):
         with open(path) as fh:
             rows = list(csv.DictReader(fh))
         by_dispatch = defaultdict(dict)
+        names = {}
         for r in rows:
-            if "k_me_sb" not in r["Kernel_Name"]:
+            if not any(k in r["Kernel_Name"] for k in ("k_me_sb", "k_stage")):
                 continue
             by_dispatch[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
-        for d in by_dispatch.values():
+            names[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0]
+        for disp, d in by_dispatch.items():
             for k, v in d.items():
-                per[k].append(v)
-    avg = {k: sum(v) / len(v) for k, v in per.items() if v}
-    res = {"counters_avg_per_launch": avg}
+                per_kernel[names[disp]][k].append(v)
+    kern = {n: {k: sum(v) / len(v) for k, v in d.items() if v} for n, d in per_kernel.items()}
+    # one "launch" of the ME path = one dispatch of every stage kernel
+    avg = defaultdict(float)
+    for d in kern.values():
+        for k, v in d.items():
+            avg[k] += v
+    res = {"counters_avg_per_launch": dict(avg), "per_kernel": kern}
     if "FETCH_SIZE" in avg:
         res["fetch_bytes_corrected"] = avg["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in avg:

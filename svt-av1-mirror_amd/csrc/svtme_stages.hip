@@ -34,12 +34,25 @@
 
 namespace svtme {
 
+#ifdef SVTME_STAMPS
+#define STAMP(k)                                                                                                    \
+    do {                                                                                                            \
+        if (threadIdx.x == 0 && dj.stamps)                                                                          \
+            dj.stamps[(size_t)sb_local * 16 + (k)] = __builtin_amdgcn_s_memtime();                                 \
+    } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
+#define STAGE_A_BUF_DW 1152 // per-wave window buffers (dwords)
+#define STAGE_B_BUF_DW 1280
+
 // ----------------------------------------------------------------------------
 // Wavefront SAD searches (sad_loop, compute_sad_c.c:58-101)
 // ----------------------------------------------------------------------------
 // rows [k0, k1) of an ND-dword block row for the 4 positions of an aligned quad
-template <int ND>
-__device__ __forceinline__ void rows_qsad(const uint32_t *rp, int bstride_dw, const uint8_t *src, int src_stride,
+template <int ND, typename P>
+__device__ __forceinline__ void rows_qsad(P rp, int bstride_dw, const uint8_t *src, int src_stride,
                                           int k0, int k1, uint32_t acc[4]) {
     constexpr int CH = 64 / ND; // u16 lanes: ND * 1020 * CH <= 65280
     for (int kc = k0; kc < k1; kc += CH) {
@@ -47,7 +60,7 @@ __device__ __forceinline__ void rows_qsad(const uint32_t *rp, int bstride_dw, co
         unsigned long long a = 0;
 #pragma unroll 2
         for (int k = kc; k < ke; k++) {
-            const uint32_t *rd = rp + k * bstride_dw;
+            const P rd         = rp + k * bstride_dw;
             const uint32_t *sd = (const uint32_t *)(src + k * src_stride);
             uint32_t d[ND + 1];
 #pragma unroll
@@ -60,13 +73,14 @@ __device__ __forceinline__ void rows_qsad(const uint32_t *rp, int bstride_dw, co
 }
 
 // any block width (partial last dword masked): v_sad_u8 on the 4 byte shifts
-__device__ __forceinline__ void rows_sad_any(const uint32_t *rp, int bstride_dw, const uint8_t *src, int src_stride,
+template <typename P>
+__device__ __forceinline__ void rows_sad_any(P rp, int bstride_dw, const uint8_t *src, int src_stride,
                                              int bw, int k0, int k1, uint32_t acc[4]) {
     const int nd             = (bw + 3) >> 2;
     const uint32_t last_mask = (bw & 3) ? ((1u << (8 * (bw & 3))) - 1u) : 0xFFFFFFFFu;
     for (int k = k0; k < k1; k++) {
-        const uint32_t *rd = rp + k * bstride_dw;
-        const uint8_t *sb  = src + k * src_stride;
+        const P rd        = rp + k * bstride_dw;
+        const uint8_t *sb = src + k * src_stride;
         uint32_t d0        = rd[0];
         for (int j = 0; j < nd; j++) {
             const uint32_t d1 = rd[j + 1];
@@ -81,57 +95,159 @@ __device__ __forceinline__ void rows_sad_any(const uint32_t *rp, int bstride_dw,
     }
 }
 
-// One sad_loop over plane p, executed by the calling wavefront (all arguments
-// wave-uniform): window top-left (plane coords) (wx, wy), search area
-// sa_w x sa_h, block bw x bh_eff rows (sub: block rows 2 plane rows apart),
-// source block at src (stride src_stride between block rows). Returns the
-// wave-uniform best key (sad << 32 | y << 16 | x), ~0 if nothing searched.
-__device__ unsigned long long wave_sad_task(const uint8_t *pbase, int pstride, int wx, int wy, int sa_w, int sa_h,
-                                            int bw, int bh_eff, bool sub, bool skip_flag, const uint8_t *src,
-                                            int src_stride) {
-    const int lane  = threadIdx.x & 63;
+// exact-division magics for small divisors (uniform table lookups)
+struct MagicTab {
+    uint32_t v[256];
+};
+constexpr MagicTab make_magic_tab() {
+    MagicTab t{};
+    for (uint32_t d = 1; d < 256; d++) t.v[d] = 0xFFFFFFFFu / d + 1u;
+    return t;
+}
+__constant__ MagicTab c_magic = make_magic_tab();
+__device__ __forceinline__ uint32_t magic_of(int d) { return d < 256 ? c_magic.v[d] : magic_u32((uint32_t)d); }
+
+// block widths the SAD loops are specialised for (bit = dwords per row)
+#define RW_2 (1 << 2)
+#define RW_4 (1 << 4)
+#define RW_8 (1 << 8)
+#define RW_16 (1 << 16)
+
+template <int ALLOW, typename P>
+__device__ __forceinline__ void rows_dispatch(int mode, P rp, int kstride, const uint8_t *src, int src_stride, int bw,
+                                              int k0, int k1, uint32_t acc[4]) {
+    if ((ALLOW & RW_4) && mode == 4)
+        rows_qsad<4>(rp, kstride, src, src_stride, k0, k1, acc);
+    else if ((ALLOW & RW_8) && mode == 8)
+        rows_qsad<8>(rp, kstride, src, src_stride, k0, k1, acc);
+    else if ((ALLOW & RW_16) && mode == 16)
+        rows_qsad<16>(rp, kstride, src, src_stride, k0, k1, acc);
+    else if ((ALLOW & RW_2) && mode == 2)
+        rows_qsad<2>(rp, kstride, src, src_stride, k0, k1, acc);
+    else
+        rows_sad_any(rp, kstride, src, src_stride, bw, k0, k1, acc);
+}
+
+// Wave-uniform geometry of one sad_loop (compute_sad_c.c:58-101): window
+// top-left (plane coords) (wx, wy), search area sa_w x sa_h, block bw x bh_eff
+// rows (sub: block rows 2 plane rows apart). Positions are grouped in quads
+// aligned to the plane's dword grid; the staged window holds odd plane rows
+// only for skip + sub, else every row.
+struct SadGeo {
+    const uint32_t *a0; // dword-aligned address of search row 0's first quad
+    const uint32_t *g;  // first staged row
+    int gs;             // dwords between staged rows in the plane
+    int sdw, sh, nq, bw, bh, per, lg, nitems, mode, sa_w, skip, odd, ystep, wrows, wdw, pitch, staged, sub;
+    uint32_t mnq;
+};
+
+__device__ __forceinline__ SadGeo sad_geo(const uint8_t *pbase, int pstride, int wx, int wy, int sa_w, int sa_h,
+                                          int bw, int bh_eff, bool sub, bool skip_flag, int buf_dw) {
+    SadGeo g;
     const bool skip = skip_flag && bw == 16 && bh_eff <= 16; // compute_sad_c.c:74
-    const int nrows = (sa_w > 0 && sa_h > 0) ? (skip ? sa_h / 2 : sa_h) : 0;
-    if (nrows <= 0 || bh_eff <= 0)
-        return ~0ull;
-    const uint8_t *w0  = pbase + (ptrdiff_t)wy * pstride + wx;
-    const int sh       = (int)((uintptr_t)w0 & 3);
-    const uint32_t *a0 = (const uint32_t *)(w0 - sh);
-    const int nq       = (sh + sa_w + 3) >> 2; // dword-aligned position quads
-    const int sdw      = pstride >> 2;
-    const int bstr     = sub ? 2 * sdw : sdw;
-    const int quads    = nrows * nq;
-    int lg             = 0; // 2^lg lanes share a quad, splitting its block rows
+    const int nrows = (sa_w > 0 && sa_h > 0 && bh_eff > 0) ? (skip ? sa_h / 2 : sa_h) : 0;
+    const uint8_t *w0 = pbase + (ptrdiff_t)wy * pstride + wx;
+    g.sh     = (int)((uintptr_t)w0 & 3);
+    g.a0     = (const uint32_t *)(w0 - g.sh);
+    g.nq     = (g.sh + sa_w + 3) >> 2;
+    g.bw     = bw;
+    g.bh     = bh_eff;
+    g.sdw    = pstride >> 2;
+    g.sa_w   = sa_w;
+    g.skip   = skip;
+    g.sub    = sub;
+    const int nd    = (bw + 3) >> 2;
+    const int quads = nrows > 0 ? nrows * g.nq : 0;
+    int lg = 0; // 2^lg lanes share a quad, splitting its block rows
     while ((2 << lg) <= bh_eff && quads * (2 << lg) <= 64) lg++;
-    const int G = 1 << lg, per = (bh_eff + G - 1) >> lg, nitems = quads << lg;
-    const uint32_t mnq = magic_u32((uint32_t)nq);
-    const int mode     = (bw & 3) ? 0 : (bw == 16 ? 4 : (bw == 32 ? 8 : (bw == 64 ? 16 : (bw == 8 ? 2 : 0))));
-    unsigned long long best = ~0ull;
-    for (int base = 0; base < nitems; base += 64) {
-        const int i  = base + lane;
-        const int g  = i & (G - 1), qi = i >> lg;
-        const int yy = mdiv(qi, mnq), q = qi - yy * nq;
-        const int y  = skip ? 2 * yy + 1 : yy;
-        uint32_t acc[4] = {0, 0, 0, 0};
-        if (i < nitems) {
-            const int k0 = min(bh_eff, g * per), k1 = min(bh_eff, k0 + per);
-            const uint32_t *rp = a0 + (ptrdiff_t)y * sdw + q;
-            switch (mode) {
-            case 2: rows_qsad<2>(rp, bstr, src, src_stride, k0, k1, acc); break;
-            case 4: rows_qsad<4>(rp, bstr, src, src_stride, k0, k1, acc); break;
-            case 8: rows_qsad<8>(rp, bstr, src, src_stride, k0, k1, acc); break;
-            case 16: rows_qsad<16>(rp, bstr, src, src_stride, k0, k1, acc); break;
-            default: rows_sad_any(rp, bstr, src, src_stride, bw, k0, k1, acc); break;
+    g.lg     = lg;
+    g.per    = (bh_eff + (1 << lg) - 1) >> lg;
+    g.nitems = quads << lg;
+    g.mnq    = magic_of(g.nq > 0 ? g.nq : 1);
+    g.mode   = (bw & 3) ? 0 : (bw == 16 ? 4 : (bw == 32 ? 8 : (bw == 64 ? 16 : (bw == 8 ? 2 : 0))));
+    g.odd    = skip && sub;
+    g.ystep  = g.odd ? 1 : (sub ? 2 : 1);
+    const int last_y = skip ? 2 * nrows - 1 : nrows - 1;
+    g.wrows  = nrows <= 0 ? 0 : (g.odd ? (nrows - 1) + bh_eff : last_y + (bh_eff - 1) * g.ystep + 1);
+    g.wdw    = g.nq + nd;
+    g.pitch  = g.wdw | 1;
+    g.staged = g.wrows * g.pitch <= buf_dw;
+    g.g      = g.a0 + (g.odd ? g.sdw : 0);
+    g.gs     = g.odd ? 2 * g.sdw : g.sdw;
+    return g;
+}
+
+// Wave copy of a window (wrows x wdw dwords from dword-aligned plane rows gs
+// dwords apart) into LDS rows `pitch` dwords apart; loads are issued 8 deep
+// so a window costs about one memory round trip. No fence: the caller
+// publishes the LDS writes (wave_lds_fence) once everything is staged.
+__device__ __forceinline__ void wave_stage(uint32_t *buf, int pitch, const uint32_t *g, int gs, int wrows, int wdw) {
+    const int lane    = threadIdx.x & 63;
+    const int n       = wrows * wdw;
+    const uint32_t mw = magic_of(wdw);
+    for (int base = 0; base < n; base += 512) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int e = base + u * 64 + lane;
+            if (e < n) {
+                const int r = mdiv(e, mw);
+                v[u]        = g[(ptrdiff_t)r * gs + (e - r * wdw)];
             }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int e = base + u * 64 + lane;
+            if (e < n) {
+                const int r                    = mdiv(e, mw);
+                buf[r * pitch + (e - r * wdw)] = v[u];
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void sad_stage(const SadGeo &g, uint32_t *buf) {
+    if (g.staged && g.nitems)
+        wave_stage(buf, g.pitch, g.g, g.gs, g.wrows, g.wdw);
+}
+
+// The search itself; returns the wave-uniform best key (sad << 32 | y << 16 | x),
+// ~0 if nothing was searched.
+template <int ALLOW>
+__device__ __forceinline__ unsigned long long sad_compute(const SadGeo &g, const uint32_t *buf, const uint8_t *src,
+                                                          int src_stride) {
+    const int lane = threadIdx.x & 63;
+    const int G    = 1 << g.lg;
+    unsigned long long best = ~0ull;
+    for (int base = 0; base < g.nitems; base += 64) {
+        const int i  = base + lane;
+        const int gi = i & (G - 1), qi = i >> g.lg;
+        const int yy = mdiv(qi, g.mnq), q = qi - yy * g.nq;
+        const int y  = g.skip ? 2 * yy + 1 : yy;
+        uint32_t acc[4] = {0, 0, 0, 0};
+        if (i < g.nitems) {
+            const int k0 = min(g.bh, gi * g.per), k1 = min(g.bh, k0 + g.per);
+            if (g.staged)
+                rows_dispatch<ALLOW>(g.mode, buf + (g.odd ? yy : y) * g.pitch + q, g.ystep * g.pitch, src,
+                                     src_stride, g.bw, k0, k1, acc);
+            else
+                rows_dispatch<ALLOW>(g.mode, g.a0 + (ptrdiff_t)y * g.sdw + q, g.sub ? 2 * g.sdw : g.sdw, src,
+                                     src_stride, g.bw, k0, k1, acc);
         }
         for (int o = 1; o < G; o <<= 1)
 #pragma unroll
             for (int k = 0; k < 4; k++) acc[k] += __shfl_xor(acc[k], o, 64);
-        if (i < nitems && g == 0) {
+        if (i < g.nitems && gi == 0) {
 #pragma unroll
             for (int s = 0; s < 4; s++) {
-                const int x = 4 * q - sh + s;
-                if (x >= 0 && x < sa_w) {
+                const int x = 4 * q - g.sh + s;
+                if (x >= 0 && x < g.sa_w) {
                     const unsigned long long kk =
                         ((unsigned long long)acc[s] << 32) | ((uint32_t)y << 16) | (uint32_t)x;
                     best = kk < best ? kk : best;
@@ -216,16 +332,12 @@ __device__ __forceinline__ void copy_planes(const DevJob &dj, DevPlane (*pl)[NLV
 // ----------------------------------------------------------------------------
 // Stage A: every independent search of every SB, one wavefront each
 // ----------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_stage_a(const DevJob dj) {
-    __shared__ DevPlane pl[8][3];
-    __shared__ uint16_t dist[8];
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_stage_a(const DevJob dj) {
     __shared__ __attribute__((aligned(16))) uint8_t srcb[4][256];
+    __shared__ uint32_t wbuf[4][STAGE_A_BUF_DW];
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (tid == 0)
-        copy_planes<3>(dj, pl, dist);
-    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t total = job.sb_count * dj.ta_count;
     const uint32_t gw    = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
     if (gw >= total)
@@ -237,7 +349,7 @@ __global__ void __launch_bounds__(256) k_stage_a(const DevJob dj) {
     const bool hsub         = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
     if (t < SVTME_A_PH) { // zz SAD (init_zz_sad, motion_estimation.c:2382-2437)
         const int s       = t;
-        const DevPlane &P = pl[s][0];
+        const DevPlane &P = dj.ref[s >> 2][s & 3].lv[0];
         const DevPlane &C = dj.cur.lv[0];
         const uint32_t v  = wave_nxm(P.base + (ptrdiff_t)G.oy * P.stride + G.ox, 2 * P.stride,
                                      C.base + (ptrdiff_t)G.oy * C.stride + G.ox, 2 * C.stride, (int)(G.bh >> 1),
@@ -246,45 +358,45 @@ __global__ void __launch_bounds__(256) k_stage_a(const DevJob dj) {
             *out = ARes{v, 0, 0};
         return;
     }
-    // sixteenth-resolution source block (16 x 16) into this wave's LDS slot
-    {
-        const DevPlane &S = dj.cur.lv[2];
-        if (lane < 16)
-            ((uint4 *)srcb[wid])[lane] =
-                *(const uint4 *)(S.base + (ptrdiff_t)((G.oy >> 2) + lane) * S.stride + (G.ox >> 2));
-    }
-    __builtin_amdgcn_s_waitcnt(0); // wave-local LDS hand-off (no other wave reads srcb[wid])
-    __builtin_amdgcn_wave_barrier();
+    // sixteenth-resolution source block (16 x 16): issued now, stored with the window
+    const DevPlane &S = dj.cur.lv[2];
+    uint4 sv          = make_uint4(0, 0, 0, 0);
+    if (lane < 16)
+        sv = *(const uint4 *)(S.base + (ptrdiff_t)((G.oy >> 2) + lane) * S.stride + (G.ox >> 2));
     const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
     const int bws = (int)(G.bw >> 2), bhs = hsub ? (int)(G.bh >> 2) >> 1 : (int)(G.bh >> 2);
+    const bool is_ph = t < SVTME_A_L0;
+    const int s      = is_ph ? (t - SVTME_A_PH) >> 1 : (t - SVTME_A_L0) >> 2;
+    const int l = s >> 2, r = s & 3;
+    const DevPlane &P   = dj.ref[l][r].lv[2];
+    const uint16_t dist = ref_dist_const(job, l, r);
     int16_t xo, yo, sw, shh;
-    int skip = 0, mul = 4;
-    int s;
-    if (t < SVTME_A_L0) { // pre-HME region (prehme_core, motion_estimation.c:1568-1636)
-        s            = (t - SVTME_A_PH) >> 1;
-        const int sr = (t - SVTME_A_PH) & 1;
-        const uint32_t f = scaled_dist(dist[s]);
+    if (is_ph) { // pre-HME region (prehme_core, motion_estimation.c:1568-1636)
+        const int sr        = (t - SVTME_A_PH) & 1;
+        const uint32_t f    = scaled_dist(dist);
         const uint16_t sa_w = (uint16_t)min((uint32_t)c.prehme_sa_cfg[sr].sa_min.width * f,
                                             (uint32_t)c.prehme_sa_cfg[sr].sa_max.width);
         const uint16_t sa_h = (uint16_t)min((uint32_t)c.prehme_sa_cfg[sr].sa_min.height * f,
                                             (uint32_t)c.prehme_sa_cfg[sr].sa_max.height);
-        prehme_area(pl[s][2], sox, soy, (int16_t)sa_w, (int16_t)sa_h, &xo, &yo, &sw, &shh);
-        skip = c.prehme_skip_search_line;
+        prehme_area(P, sox, soy, (int16_t)sa_w, (int16_t)sa_h, &xo, &yo, &sw, &shh);
     } else { // HME level-0 quadrant (hme_level_0, motion_estimation.c:835-889)
-        s           = (t - SVTME_A_L0) >> 2;
         const int q = (t - SVTME_A_L0) & 3;
         int16_t sa_w, sa_h;
-        hme_l0_area(c, s >> 2, s & 3, dist[s], 0, 0, &sa_w, &sa_h);
-        hme_l0_rect(c, pl[s][2], sox, soy, sa_w, sa_h, q >> 1, q & 1, &xo, &yo, &sw, &shh);
+        hme_l0_area(c, l, r, dist, 0, 0, &sa_w, &sa_h);
+        hme_l0_rect(c, P, sox, soy, sa_w, sa_h, q >> 1, q & 1, &xo, &yo, &sw, &shh);
     }
-    const DevPlane &P = pl[s][2];
-    const unsigned long long k =
-        wave_sad_task(P.base, P.stride, sox + xo, soy + yo, sw, shh, bws, bhs, hsub, skip, srcb[wid], hsub ? 32 : 16);
+    const SadGeo g = sad_geo(P.base, P.stride, sox + xo, soy + yo, sw, shh, bws, bhs, hsub,
+                             is_ph && c.prehme_skip_search_line, STAGE_A_BUF_DW);
+    sad_stage(g, wbuf[wid]);
+    if (lane < 16)
+        ((uint4 *)srcb[wid])[lane] = sv;
+    wave_lds_fence();
+    const unsigned long long k = sad_compute<RW_4>(g, wbuf[wid], srcb[wid], hsub ? 32 : 16);
     if (lane == 0) {
         uint32_t best;
         int x, y;
         key_result(k, &best, &x, &y);
-        *out = ARes{hsub ? best * 2 : best, i16((x + xo) * mul), i16((y + yo) * mul)};
+        *out = ARes{hsub ? best * 2 : best, i16((x + xo) * 4), i16((y + yo) * 4)};
     }
 }
 
@@ -319,6 +431,7 @@ struct StB {
     unsigned long long bkey[32];
     int32_t nbt;
     __attribute__((aligned(16))) uint8_t src[64 * 64];
+    uint32_t wbuf[4][STAGE_B_BUF_DW];
 };
 
 __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
@@ -333,6 +446,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
     const int nl     = job.num_lists;
     const bool hsub  = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
     const uint32_t vmask = valid_mask(job);
+    STAMP(0);
 
     if (tid < SVTME_A_N)
         st.a[tid] = dj.ares[(size_t)sb_local * SVTME_A_N + tid];
@@ -359,6 +473,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
         ((uint4 *)st.src)[tid] = *(const uint4 *)(Q.base + (ptrdiff_t)((oy >> 1) + r) * Q.stride + (ox >> 1) + 16 * j);
     }
     __syncthreads();
+    STAMP(1);
 
     if (w0) {
         // ---- init_zz_sad decisions (motion_estimation.c:2382-2437)
@@ -495,6 +610,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
         }
     }
     __syncthreads();
+    STAMP(3);
 
     // ---- HME level 1 / 2 (motion_estimation.c:2041-2177)
     for (int level = 1; level <= 2; level++) {
@@ -561,17 +677,35 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
                 st.nbt = tot;
         }
         __syncthreads();
+        STAMP(4);
         {
             const int bwl = level == 1 ? (int)(bw >> 1) : (int)bw;
             const int bhl = level == 1 ? (int)(bh >> 1) : (int)bh;
             const int sst = (level == 1 ? 32 : 64) * (hsub ? 2 : 1);
-            for (int t = wid; t < st.nbt; t += 4) {
+            // every task of this wave staged together (one memory round trip), then searched
+            const int nbt = st.nbt;
+            auto geo = [&](int t, int room) {
                 const BTask &T    = st.bt[t];
                 const int s       = UNI(T.slot);
                 const DevPlane &P = st.pl[s][level == 1 ? 1 : 0];
-                const unsigned long long k = wave_sad_task(P.base, P.stride, UNI(T.wx), UNI(T.wy), UNI(T.sa_w),
-                                                           UNI(T.sa_h), bwl, hsub ? bhl >> 1 : bhl, hsub, false,
-                                                           st.src, sst);
+                return sad_geo(P.base, P.stride, UNI(T.wx), UNI(T.wy), UNI(T.sa_w), UNI(T.sa_h), bwl,
+                               hsub ? bhl >> 1 : bhl, hsub, false, room);
+            };
+            int off = 0;
+            for (int t = wid; t < nbt; t += 4) {
+                const SadGeo g = geo(t, STAGE_B_BUF_DW - off);
+                if (g.staged && g.nitems) {
+                    sad_stage(g, st.wbuf[wid] + off);
+                    off += g.wrows * g.pitch;
+                }
+            }
+            wave_lds_fence();
+            off = 0;
+            for (int t = wid; t < nbt; t += 4) {
+                const SadGeo g = geo(t, STAGE_B_BUF_DW - off);
+                const unsigned long long k = sad_compute<RW_8 | RW_16 | RW_4 | RW_2>(g, st.wbuf[wid] + off, st.src, sst);
+                if (g.staged && g.nitems)
+                    off += g.wrows * g.pitch;
                 if (lane == 0)
                     st.bkey[t] = k;
             }
@@ -589,6 +723,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
             st.ly[level][s][q]     = i16((y + T.yo) * mul);
         }
         __syncthreads();
+        STAMP(5);
     }
 
     // ---- set_final_seach_centre_sb (motion_estimation.c:2182-2380) + hme_prune_ref_and_adjust_sr (:2477-2518)
@@ -684,6 +819,7 @@ struct FpRef {        // one full-pel search window of a reference slot
     const uint32_t *a; // dword-aligned address of window row 0 (search row 0)
     int32_t sdw;       // plane stride in dwords
     int32_t nitems;    // rows x aligned quads
+    int32_t item_begin;
     uint32_t mnq;
     int16_t xo, yo, w, h;
     int32_t order_base; // 0: 8x8-variance centre probe, 1: main search
@@ -691,7 +827,6 @@ struct FpRef {        // one full-pel search window of a reference slot
 };
 
 struct StC {
-    __attribute__((aligned(16))) uint8_t src[64 * 64];
     DevPlane pl[8][1];
     uint16_t dist[8];
     uint64_t refpic[8];
@@ -706,7 +841,7 @@ struct StC {
     int32_t req_stride[16];
     int8_t req_slot[8];
     uint32_t nxm[16];
-    int32_t nreq, nfp, k32;
+    int32_t nreq, nfp, k32, fp_items;
     FpRef fp[8];
     unsigned long long keys[8][SVTME_PU_COUNT];
     uint32_t best_sad[8][SVTME_PU_COUNT];
@@ -731,18 +866,31 @@ __device__ void make_fp(FpRef &F, const DevPlane &P, uint32_t ox, uint32_t oy, i
     F.nitems     = (int)h * F.nq;
 }
 
+// wave 0: item offsets of the compacted FpRefs (this lane's at k when mk)
+__device__ __forceinline__ void plan_fp(StC &st, bool mk, int k, int n) {
+    const int items = mk ? st.fp[k].nitems : 0;
+    const int incl  = wave_incl_scan(items);
+    if (mk)
+        st.fp[k].item_begin = incl - items;
+    if ((threadIdx.x & 63) == 63)
+        st.fp_items = incl;
+    if ((threadIdx.x & 63) == 0)
+        st.nfp = n;
+}
+
 // Full-pel search of the planned windows (motion_estimation.c:98-425, 781-817):
 // lane = 8x8 block in Z-order; one item = one aligned position quad of a
-// search row; 16x16 / 32x32 / 64x64 SADs are DPP lane sums. Keys are
-// (sad << 12 | order) in 32 bits when every order < 4096 (64x64 SAD < 2^20),
-// else (sad << 32 | order).
+// search row of one window; the items of all windows are dealt to the 4
+// waves DEPTH at a time with their loads issued together. 16x16 / 32x32 /
+// 64x64 SADs are DPP lane sums. Keys are (sad << 12 | order) in 32 bits when
+// every order < 4096 (64x64 SAD < 2^20), else (sad << 32 | order).
 template <bool SUB, bool K32>
-__device__ void fullpel_run(StC &st) {
+__device__ void fullpel_run(StC &st, const DevPlane &C, uint32_t ox, uint32_t oy) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int z16 = lane >> 2, k4 = lane & 3;
     const int by = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
     const int bx = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
-    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1;
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1, DEPTH = SUB ? 2 : 1;
     typedef typename std::conditional<K32, uint32_t, unsigned long long>::type key_t;
     for (int e = tid; e < st.nfp * SVTME_PU_COUNT; e += 256) {
         const int f = e / SVTME_PU_COUNT;
@@ -751,37 +899,78 @@ __device__ void fullpel_run(StC &st) {
     uint32_t src[ROWS][2];
 #pragma unroll
     for (int r = 0; r < ROWS; r++) {
-        const uint32_t *s = (const uint32_t *)(st.src + (by * 8 + r * RSTEP) * 64 + bx * 8);
-        src[r][0] = s[0];
-        src[r][1] = s[1];
+        const uint32_t *sp =
+            (const uint32_t *)(C.base + (ptrdiff_t)(oy + by * 8 + r * RSTEP) * C.stride + ox + bx * 8);
+        src[r][0] = sp[0];
+        src[r][1] = sp[1];
     }
     __syncthreads();
-    const int nfp = st.nfp;
-    for (int f = 0; f < nfp; f++) {
-        const FpRef &F   = st.fp[f];
-        const int nitems = UNI(F.nitems);
-        if (wid >= nitems)
-            continue; // wave-uniform
-        const int nq = UNI(F.nq), w = UNI(F.w), obase = UNI(F.order_base), sdw = UNI(F.sdw), sh = UNI(F.sh);
-        const uint32_t mnq = (uint32_t)UNI(F.mnq);
-        const uint32_t *ab = F.a + (ptrdiff_t)(by * 8) * sdw + bx * 2;
-        key_t b8 = (key_t)~0ull, b16 = (key_t)~0ull, b32 = (key_t)~0ull, b64 = (key_t)~0ull;
-        for (int i = wid; i < nitems; i += 4) {
-            const int y = mdiv(i, mnq), q = i - y * nq;
-            const uint32_t *rp = ab + (ptrdiff_t)y * sdw + q;
-            uint32_t d[ROWS][3];
+    const int nfp = st.nfp, total = st.fp_items;
+    int cur = -1;
+    key_t b8 = (key_t)~0ull, b16 = (key_t)~0ull, b32 = (key_t)~0ull, b64 = (key_t)~0ull;
+    auto wide = [](key_t kk) -> unsigned long long {
+        if (K32) {
+            const uint32_t v = (uint32_t)kk;
+            return v == 0xFFFFFFFFu ? ~0ull : (((unsigned long long)(v >> 12) << 32) | (v & 0xFFFu));
+        }
+        return (unsigned long long)kk;
+    };
+    auto flush = [&](int f) {
+        unsigned long long *pk = st.keys[UNI(st.fp[f].slot)];
+        atomicMin(&pk[21 + lane], wide(b8));
+        if ((lane & 3) == 0)
+            atomicMin(&pk[5 + (lane >> 2)], wide(b16));
+        if ((lane & 15) == 0)
+            atomicMin(&pk[1 + (lane >> 4)], wide(b32));
+        if (lane == 63)
+            atomicMin(&pk[0], wide(b64));
+    };
+    for (int base = wid * DEPTH; base < total; base += 4 * DEPTH) {
+        uint32_t d[DEPTH][ROWS][3];
+        int fi[DEPTH], yi[DEPTH], qi[DEPTH];
 #pragma unroll
-            for (int rr = 0; rr < ROWS; rr++) {
-                const uint32_t *rd = rp + (ptrdiff_t)(rr * RSTEP) * sdw;
-                d[rr][0] = rd[0];
-                d[rr][1] = rd[1];
-                d[rr][2] = rd[2];
+        for (int u = 0; u < DEPTH; u++) {
+            const int i = base + u;
+            int f = 0;
+            while (f + 1 < nfp && st.fp[f + 1].item_begin <= i) f++;
+            fi[u] = UNI(f);
+            if (i < total) {
+                const FpRef &F = st.fp[fi[u]];
+                const int li   = i - UNI(F.item_begin);
+                const int nq   = UNI(F.nq);
+                yi[u] = mdiv(li, (uint32_t)UNI(F.mnq));
+                qi[u] = li - yi[u] * nq;
+                const int sdw = UNI(F.sdw);
+                const uint32_t *rp = F.a + (ptrdiff_t)(yi[u] + by * 8) * sdw + qi[u] + bx * 2;
+#pragma unroll
+                for (int rr = 0; rr < ROWS; rr++) {
+                    const uint32_t *rd = rp + (ptrdiff_t)(rr * RSTEP) * sdw;
+                    d[u][rr][0] = rd[0];
+                    d[u][rr][1] = rd[1];
+                    d[u][rr][2] = rd[2];
+                }
             }
+        }
+#pragma unroll
+        for (int u = 0; u < DEPTH; u++) {
+            const int i = base + u;
+            if (i >= total)
+                break; // wave-uniform
+            const int f = fi[u];
+            if (f != cur) {
+                if (cur >= 0)
+                    flush(cur);
+                b8 = b16 = b32 = b64 = (key_t)~0ull;
+                cur = f;
+            }
+            const FpRef &F = st.fp[f];
+            const int w = UNI(F.w), sh = UNI(F.sh), obase = UNI(F.order_base);
+            const int y = yi[u], q = qi[u];
             unsigned long long a = 0;
 #pragma unroll
             for (int rr = 0; rr < ROWS; rr++) {
-                a = qsad(d[rr][0], d[rr][1], src[rr][0], a);
-                a = qsad(d[rr][1], d[rr][2], src[rr][1], a);
+                a = qsad(d[u][rr][0], d[u][rr][1], src[rr][0], a);
+                a = qsad(d[u][rr][1], d[u][rr][2], src[rr][1], a);
             }
             uint32_t acc[4] = {0, 0, 0, 0};
             qsad_unpack(a, acc);
@@ -791,9 +980,9 @@ __device__ void fullpel_run(StC &st) {
                 if (x < 0 || x >= w)
                     continue; // wave-uniform
                 const uint32_t s8  = SUB ? acc[k] << 1 : acc[k];
-                const uint32_t s16 = dpp_add<0x4E>(dpp_add<0xB1>(s8));                  // xor 1, xor 2
-                const uint32_t s32 = dpp_add<0x128>(dpp_add<0x124>(s16));               // row_ror 4, 8
-                const uint32_t s64 = dpp_add<0x143, 0xC>(dpp_add<0x142, 0xA>(s32));     // valid in row 3
+                const uint32_t s16 = dpp_add<0x4E>(dpp_add<0xB1>(s8));              // xor 1, xor 2
+                const uint32_t s32 = dpp_add<0x128>(dpp_add<0x124>(s16));           // row_ror 4, 8
+                const uint32_t s64 = dpp_add<0x143, 0xC>(dpp_add<0x142, 0xA>(s32)); // valid in row 3
                 const uint32_t o   = (uint32_t)(obase + y * w + x);
                 if (K32) {
                     b8  = min_u32((uint32_t)b8, (s8 << 12) | o);
@@ -812,22 +1001,9 @@ __device__ void fullpel_run(StC &st) {
                 }
             }
         }
-        unsigned long long *pk = st.keys[UNI(F.slot)];
-        auto wide = [](key_t kk) -> unsigned long long {
-            if (K32) {
-                const uint32_t v = (uint32_t)kk;
-                return v == 0xFFFFFFFFu ? ~0ull : (((unsigned long long)(v >> 12) << 32) | (v & 0xFFFu));
-            }
-            return (unsigned long long)kk;
-        };
-        atomicMin(&pk[21 + lane], wide(b8));
-        if ((lane & 3) == 0)
-            atomicMin(&pk[5 + (lane >> 2)], wide(b16));
-        if ((lane & 15) == 0)
-            atomicMin(&pk[1 + (lane >> 4)], wide(b32));
-        if (lane == 63)
-            atomicMin(&pk[0], wide(b64));
     }
+    if (cur >= 0)
+        flush(cur);
     __syncthreads();
     // decode: strict-< update of the running best (motion_estimation.c:1366, :137-205)
     for (int e = tid; e < st.nfp * SVTME_PU_COUNT; e += 256) {
@@ -847,11 +1023,11 @@ __device__ void fullpel_run(StC &st) {
 }
 
 template <bool SUB>
-__device__ void fullpel(StC &st) {
+__device__ void fullpel(StC &st, const DevPlane &C, uint32_t ox, uint32_t oy) {
     if (st.k32)
-        fullpel_run<SUB, true>(st);
+        fullpel_run<SUB, true>(st, C, ox, oy);
     else
-        fullpel_run<SUB, false>(st);
+        fullpel_run<SUB, false>(st, C, ox, oy);
 }
 
 // Candidate arrays + distortions + GM detection for one SB, all threads
@@ -1080,7 +1256,7 @@ __device__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t
 }
 
 template <bool SUB_ME>
-__global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_c(const DevJob dj) {
     __shared__ StC st;
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
@@ -1091,11 +1267,8 @@ __global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
     const uint32_t ox = G.ox, oy = G.oy, bw = G.bw, bh = G.bh;
     const uint32_t vmask = valid_mask(job);
 
-    { // full-resolution source block (me_process.c:183-214)
-        const DevPlane &F = dj.cur.lv[0];
-        const int r = tid >> 2, j = tid & 3;
-        ((uint4 *)st.src)[tid] = *(const uint4 *)(F.base + (ptrdiff_t)(oy + r) * F.stride + ox + 16 * j);
-    }
+    const DevPlane &C = dj.cur.lv[0]; // source block read in place (me_process.c:183-214)
+    STAMP(6);
     if (tid == 0) {
 #pragma unroll
         for (int s = 0; s < 8; s++) {
@@ -1116,6 +1289,7 @@ __global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
     }
     for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) (&st.best_mv[0][0])[e] = 0;
     __syncthreads();
+    STAMP(7);
 
     // ---- integer_search_b64 (motion_estimation.c:1249-1516); lane s of wave 0 owns slot s.
     // Two rounds when enable_me_sr_adjustment == 2: the other slots read slot 0's 64x64 SAD.
@@ -1177,9 +1351,11 @@ __global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
                 st.nreq = tot;
         }
         __syncthreads();
+        STAMP(8);
         if (st.nreq) {
             for (int q = wid; q < 2 * st.nreq; q += 4) {
-                const uint32_t v = wave_nxm(st.req[q], st.req_stride[q], st.src, 128, (int)(bh >> 1), (int)bw);
+                const uint32_t v = wave_nxm(st.req[q], st.req_stride[q], C.base + (ptrdiff_t)oy * C.stride + ox,
+                                            2 * C.stride, (int)(bh >> 1), (int)bw);
                 if (lane == 0)
                     st.nxm[q] = v;
             }
@@ -1224,19 +1400,20 @@ __global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
             const int k = wave_compact(probe, &tot);
             if (probe)
                 make_fp(st.fp[k], st.pl[s][0], ox, oy, s, st.is_xc[s], st.is_yc[s], 1, 1, 0);
-            if (lane == 0) {
-                st.nfp = tot;
+            plan_fp(st, probe, k, tot);
+            if (lane == 0)
                 st.k32 = 1; // a single position
-            }
         }
         __syncthreads();
+        STAMP(9);
         for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) {
             const int s = e / SVTME_PU_COUNT;
             if (st.in_round[s])
                 (&st.best_sad[0][0])[e] = SVTME_MAX_SAD_VALUE;
         }
         if (st.nfp) {
-            fullpel<SUB_ME>(st); // centre probe (motion_estimation.c:1414-1417)
+            fullpel<SUB_ME>(st, C, ox, oy); // centre probe (motion_estimation.c:1414-1417)
+            STAMP(10);
             // 8x8-variance resize (motion_estimation.c:1418-1438)
             if (w0 && lane < 8 && st.in_round[lane] && c.me_8x8_var_enabled && (st.is_w[lane] * st.is_h[lane] > 24)) {
                 const int s = lane;
@@ -1290,15 +1467,15 @@ __global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
             const int k = wave_compact(act, &tot);
             if (act)
                 make_fp(st.fp[k], st.pl[s][0], ox, oy, s, xo, yo, w, h, 1);
+            plan_fp(st, act, k, tot);
             const bool k32 = __all(!act || (1 + (int)w * (int)h <= 4096));
-            if (lane == 0) {
-                st.nfp = tot;
+            if (lane == 0)
                 st.k32 = k32;
-            }
         }
         __syncthreads();
+        STAMP(11);
         if (st.nfp)
-            fullpel<SUB_ME>(st);
+            fullpel<SUB_ME>(st, C, ox, oy);
     }
 
     // ---- me_prune_ref (motion_estimation.c:1522-1565)
@@ -1326,6 +1503,7 @@ __global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
         }
     }
     __syncthreads();
+    STAMP(12);
 
     // ---- records (sb_count x R, slots in list-0-then-list-1 order)
     {
@@ -1358,8 +1536,10 @@ __global__ void __launch_bounds__(256) k_stage_c(const DevJob dj) {
     }
     if (dj.out_sb) {
         __syncthreads();
+        STAMP(13);
         finish_sb(st, dj, sb_local, bw, bh);
     }
+    STAMP(14);
 }
 
 } // namespace svtme
