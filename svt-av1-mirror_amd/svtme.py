@@ -92,6 +92,25 @@ class Controls(C.Structure):
         ("prev_me_stage_based_exit_th", C.c_uint32),
     ]
 
+    @staticmethod
+    def from_dict(d: dict) -> "Controls":
+        """Inverse of as_dict (golden fixtures store controls as dicts)."""
+        c = Controls()
+        for name, v in d.items():
+            cur = getattr(c, name)
+            if isinstance(cur, AreaMinMax):
+                cur.sa_min.width, cur.sa_min.height = v[0]
+                cur.sa_max.width, cur.sa_max.height = v[1]
+            elif isinstance(cur, Area):
+                cur.width, cur.height = v
+            elif name == "prehme_sa_cfg":
+                for a, vv in zip(cur, v):
+                    a.sa_min.width, a.sa_min.height = vv[0]
+                    a.sa_max.width, a.sa_max.height = vv[1]
+            else:
+                setattr(c, name, v)
+        return c
+
     def as_dict(self):
         out = {}
         for name, _ in self._fields_:
@@ -268,6 +287,50 @@ class Synth:
         load_synth().svtme_synth_frame10_from_texture(self.tex.ctypes.data, self.w, self.h, t, out.ctypes.data,
                                                       self.w)
         return out
+
+
+def test_frames(kind: str, w: int, h: int, ts) -> dict:
+    """Deterministic test content {t: luma plane} shared by the parity tests and
+    the golden-fixture generator: a panning texture ("pan"), i.i.d. noise,
+    flat, saturated (0/255) and moving stripes (exact ties everywhere)."""
+    ts = list(ts)
+    if kind == "pan":
+        syn = Synth(w, h)
+        return {t: syn.frame(t) for t in ts}
+    rng = np.random.default_rng(1234)
+    if kind == "noise":
+        return {t: rng.integers(0, 256, (h, w), dtype=np.uint8) for t in ts}
+    if kind == "flat":
+        return {t: np.full((h, w), 128, np.uint8) for t in ts}
+    if kind == "sat":
+        return {t: (rng.integers(0, 2, (h, w)) * 255).astype(np.uint8) for t in ts}
+    if kind == "stripes":
+        base = ((np.arange(w)[None, :] // 4 + np.arange(h)[:, None] // 8) % 2 * 200).astype(np.uint8)
+        return {t: np.roll(base, t, axis=1) for t in ts}
+    raise ValueError(kind)
+
+
+def case_job(ctrl: Controls, w: int, h: int, cur: int, l0, l1, tl: int, gm: bool = False, is_ref: bool = True,
+             e8=None, sb_begin: int = 0, sb_count: int = 0) -> Job:
+    """The job of one test case: references ordered as given, lists sized to them."""
+    res = input_resolution_of(w, h)
+    return make_job(w, h, ctrl, cur, l0, l1, temporal_layer_index=tl, is_ref=is_ref,
+                    enable_me_8x8=(res <= RES_720P) if e8 is None else e8,
+                    ref_count_used=(max(len(l0), 1), len(l1)), gm_enabled=gm, sb_begin=sb_begin, sb_count=sb_count)
+
+
+def run_case_checker(kind: str, w: int, h: int, ctrl: Controls, cur: int, l0, l1, tl: int, checker: str = "oracle",
+                     nthreads: int = 8, **kw):
+    """One picture of test content through a CPU checker -> (records, sb_results)."""
+    frames = test_frames(kind, w, h, sorted(set([cur] + list(l0) + list(l1))))
+    pyr = {t: build_host_pyramid(f, checker) for t, f in frames.items()}
+    refs = {}
+    for i, t in enumerate(l0):
+        refs[(0, i)] = pyr[t]
+    for i, t in enumerate(l1):
+        refs[(1, i)] = pyr[t]
+    job = case_job(ctrl, w, h, cur, l0, l1, tl, **kw)
+    return run_checker(job, pyr[cur], refs, checker, nthreads=nthreads)
 
 
 # ----------------------------------------------------------------------------

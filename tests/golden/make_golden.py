@@ -1,0 +1,99 @@
+"""Generate the golden fixtures under tests/golden/ from the reference itself.
+
+The reference's own open-loop ME (motion_estimation.c and the kernels it
+dispatches to) and its svt_aom_sig_deriv_me (enc_mode_config.c) are compiled
+from the sources under /root/reference into oracle/_ref/libsvtref.so by
+oracle/Makefile (`make -C oracle ref`). This script drives that library on
+deterministic inputs (svtme.test_frames / the PCG32 synthetic texture) and
+stores inputs-as-parameters plus expected outputs:
+
+  controls.json      svt_aom_sig_deriv_me outputs over presets x resolutions x
+                     temporal layers x QPs (the product restates it in C++)
+  me_cases.json      the ME cases (content, size, preset, layer, references)
+  me_<name>.npz      expected per-SB reference records and SB results
+                     (raw bytes of REF_RECORD_DTYPE / SB_RESULT_DTYPE), plus
+                     sha256 digests of the reference's padded pyramids
+
+Run from the repo root in the build container (needs /root/reference for the
+library build only): python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
+
+import svtme as S  # noqa: E402
+
+ME_CASES = [
+    # name, content, w, h, preset, tl, l0, l1, extra
+    ("pan320_p8_tl1", "pan", 320, 192, 8, 1, (7, 6), (9, 10), {}),
+    ("pan640_p4_tl2", "pan", 640, 360, 4, 2, (7, 6), (9,), {}),
+    ("pan426_p6_tl0", "pan", 426, 240, 6, 0, (7, 6, 5), (9, 10), {}),
+    ("pan72_p8_edges", "pan", 72, 40, 8, 1, (7, 6), (9, 10), {}),
+    ("pan136x8_p6", "pan", 136, 8, 6, 1, (7,), (9,), {}),
+    ("noise320_p12_single", "noise", 320, 192, 12, 0, (7,), (), {}),
+    ("flat320_p4_ties", "flat", 320, 192, 4, 1, (7,), (9,), {}),
+    ("sat192_p6", "sat", 192, 128, 6, 1, (7, 6), (9,), {}),
+    ("stripes320_p8_7refs", "stripes", 320, 192, 8, 3, (7, 6, 4, 3), (9, 10, 12), {}),
+    ("pan640_p4_gm", "pan", 640, 360, 4, 1, (7, 6), (9,), {"gm": True}),
+    ("pan320_p8_band", "pan", 320, 192, 8, 1, (7, 6), (9, 10), {"sb_begin": 3, "sb_count": 7}),
+    ("pan64_p0", "pan", 64, 64, 0, 1, (7,), (9,), {}),
+    ("pan320_p8_nonref", "pan", 320, 192, 8, 2, (7,), (9,), {"is_ref": False}),
+]
+
+CTRL_GRID = dict(enc_mode=list(range(14)), input_resolution=list(range(7)), tl=[0, 1, 2, 3], qp=[35, 55])
+
+
+def controls_golden():
+    unique, index, rows = [], {}, []
+    for m in CTRL_GRID["enc_mode"]:
+        for res in CTRL_GRID["input_resolution"]:
+            for tl in CTRL_GRID["tl"]:
+                for qp in CTRL_GRID["qp"]:
+                    d = S.ref_derive_controls(m, qp, res, tl).as_dict()
+                    key = json.dumps(d, sort_keys=True)
+                    if key not in index:
+                        index[key] = len(unique)
+                        unique.append(d)
+                    rows.append([m, qp, res, tl, index[key]])
+    return {"args": ["enc_mode", "qp", "input_resolution", "temporal_layer_index", "unique_index"],
+            "unique": unique, "rows": rows}
+
+
+def digest(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def main():
+    ref = S.load_ref()
+    with open(os.path.join(HERE, "controls.json"), "w") as fh:
+        json.dump(controls_golden(), fh, indent=0)
+    meta = []
+    for name, kind, w, h, preset, tl, l0, l1, extra in ME_CASES:
+        ctrl = S.ref_derive_controls(preset, 35, S.input_resolution_of(w, h), tl)
+        out = {}
+        for simd in (0, 1):  # C kernels and AVX2 kernels must agree
+            ref.svtref_set_simd(simd)
+            out[simd] = S.run_case_checker(kind, w, h, ctrl, 8, l0, l1, tl, checker="ref", **extra)
+        recs, sbr = out[0]
+        assert not S.compare_records(recs, out[1][0], sbr, out[1][1]), name
+        frames = S.test_frames(kind, w, h, [8])
+        p = S.build_host_pyramid(frames[8], "ref")
+        np.savez_compressed(os.path.join(HERE, f"me_{name}.npz"), records=recs.view(np.uint8).reshape(len(recs), -1),
+                            sb=sbr.view(np.uint8).reshape(len(sbr), -1))
+        meta.append({"name": name, "content": kind, "w": w, "h": h, "preset": preset, "tl": tl, "l0": list(l0), "ctrl": ctrl.as_dict(),
+                     "l1": list(l1), "extra": extra, "checksum": S.records_checksum(recs, sbr),
+                     "pyramid_sha256": {k: digest(getattr(p, k)) for k in ("full", "quarter", "sixteenth")}})
+        print(name, recs.shape, meta[-1]["checksum"][:16])
+    with open(os.path.join(HERE, "me_cases.json"), "w") as fh:
+        json.dump(meta, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -12,25 +12,8 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def content(kind, w, h, ts, S):
-    if kind == "pan":
-        syn = S.Synth(w, h)
-        return {t: syn.frame(t) for t in ts}
-    rng = np.random.default_rng(1234)
-    if kind == "noise":
-        return {t: rng.integers(0, 256, (h, w), dtype=np.uint8) for t in ts}
-    if kind == "flat":
-        return {t: np.full((h, w), 128, np.uint8) for t in ts}
-    if kind == "sat":
-        return {t: (rng.integers(0, 2, (h, w)) * 255).astype(np.uint8) for t in ts}
-    if kind == "stripes":
-        base = ((np.arange(w)[None, :] // 4 + np.arange(h)[:, None] // 8) % 2 * 200).astype(np.uint8)
-        return {t: np.roll(base, t, axis=1) for t in ts}
-    raise ValueError(kind)
-
-
 def run_case(S, gpu, kind, w, h, mode, tl, l0, l1, cur=8, gm=False, is_ref=True, e8=None, sb_begin=0, sb_count=0):
-    frames = content(kind, w, h, sorted(set([cur] + list(l0) + list(l1))), S)
+    frames = S.test_frames(kind, w, h, sorted(set([cur] + list(l0) + list(l1))))
     res = S.input_resolution_of(w, h)
     ctrl = S.derive_controls(mode, 35, res, tl)
     job = S.make_job(w, h, ctrl, cur, l0, l1, temporal_layer_index=tl, is_ref=is_ref,
