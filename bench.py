@@ -34,12 +34,18 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 
 # bytes/SB = src 2688 + R x (ref windows + 680 output), nominal windows
 WINDOW_BYTES = {"p8": 16798, "p6": 38121, "p8_sa64": 28241}
+# the same bytes split over the three stage kernels (p8 stage breakdown of SURVEY.md 8(d):
+# zz 2048 + pre-HME 2645 + 1034 + HME-L0 1081 | HME-L1 5304 | full-pel 4686 + 680 out;
+# source 64x32 + 16x8 in stage A, 32x16 in stage B)
+STAGE_BYTES = {"p8": ((2176, 6808), (512, 5304), (0, 4686 + 680))}
+STAGE_NAMES = ("k_stage_a", "k_stage_b", "k_stage_c")
 
 WORKLOADS = {
     "4k_p8": dict(w=3840, h=2160, mode=8, tl=1, l0=(7, 6), l1=(9, 10), windows="p8", ten_bit=False,
                   desc="3840x2160 8-bit preset 8, 4 refs (L0 d=1,2; L1 d=1,2), open-loop ME"),
-    "1080p_p8": dict(w=1920, h=1080, mode=8, tl=1, l0=(7,), l1=(), windows="p8", ten_bit=False,
-                     desc="1920x1080 8-bit preset 8, 1 ref (L0 d=1), open-loop ME"),
+    "1080p_p8": dict(w=1920, h=1080, mode=8, tl=1, l0=(7,), l1=(), windows="p8_sa64", ten_bit=False, sa64=True,
+                     desc="1920x1080 8-bit preset 8, 1 ref (L0 d=1), ME area override 64x64 "
+                          "(8x8-variance resize and sr-adjust off: 4096 positions/SB), open-loop ME"),
     "4k10_p6": dict(w=3840, h=2160, mode=6, tl=1, l0=(7,), l1=(9,), windows="p6", ten_bit=True,
                     desc="3840x2160 10-bit preset 6 (8-bit MSB search), 2 refs, open-loop ME"),
     "8k_p8": dict(w=7680, h=4320, mode=8, tl=1, l0=(7, 6), l1=(9, 10), windows="p8", ten_bit=False,
@@ -91,6 +97,11 @@ def main():
         gpu.upload(base + t, f)
     res = S.input_resolution_of(W, H)
     ctrl = S.derive_controls(wl["mode"], 35, res, wl["tl"])
+    if wl.get("sa64"):  # fixed 64x64 full-pel area
+        ctrl.me_sa.sa_min.width = ctrl.me_sa.sa_min.height = 64
+        ctrl.me_sa.sa_max.width = ctrl.me_sa.sa_max.height = 64
+        ctrl.me_8x8_var_enabled = 0
+        ctrl.enable_me_sr_adjustment = 0
     job = S.make_job(W, H, ctrl, base + 8, [base + t for t in wl["l0"]], [base + t for t in wl["l1"]],
                      temporal_layer_index=wl["tl"], enable_me_8x8=(res <= S.RES_720P), ref_count_used=(3, 2))
     R = S.ref_slots(job)
@@ -134,14 +145,25 @@ def main():
 
     # dominant kernel: k_me_sb timed with HIP events on the library's stream
     gpu.set_timing(True)
-    kms = []
+    kms, sms = [], []
     for _ in range(args.kernel_samples):
-        gpu.submit_device(job, d_rec.data_ptr(), None)
+        gpu.submit_device(job, d_rec.data_ptr(), d_sb.data_ptr())
         kms.append(gpu.kernel_ms())
+        sms.append([gpu.stage_ms(i) for i in range(3)])
     gpu.set_timing(False)
     k_avg_ms = float(np.mean(kms))
+    s_avg_ms = np.mean(np.array(sms), axis=0)
     bps = bytes_per_sb(wl["windows"], R)
     achieved = bps * n_sb / (k_avg_ms * 1e-3) / 1e9
+    stages = {}
+    for i, name in enumerate(STAGE_NAMES):
+        st = {"avg_ms": round(float(s_avg_ms[i]), 4)}
+        if wl["windows"] in STAGE_BYTES:
+            src_b, per_ref = STAGE_BYTES[wl["windows"]][i]
+            b = (src_b + R * per_ref) * n_sb
+            st["bytes_per_launch"] = b
+            st["achieved_gbps"] = round(b / (float(s_avg_ms[i]) * 1e-3) / 1e9, 1)
+        stages[name] = st
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
     if os.path.exists(pmc_path):
@@ -175,8 +197,9 @@ def main():
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "k_me_sb", "kernel_avg_ms": round(k_avg_ms, 4),
-                         "bytes_per_launch": bps * n_sb},
+                         "kernel": "ME pass = k_stage_a + k_stage_b + k_stage_c (one picture job)",
+                         "kernel_avg_ms": round(k_avg_ms, 4), "bytes_per_launch": bps * n_sb,
+                         "stages": stages},
             "cpu_baseline": cpu_baseline,
             "parity_vs_cpu": parity,
         }

@@ -247,10 +247,14 @@ svtme_status svtme_fetch(svtme_ctx *ctx, svtme_ref_record *ref_records, svtme_sb
  * when d_sb_results is not NULL. */
 svtme_status svtme_submit_picture_device(svtme_ctx *ctx, const svtme_job *job, svtme_ref_record *d_ref_records,
                                          svtme_sb_result *d_sb_results);
-/* Time the per-SB ME kernel of every job with HIP events on the context's
- * stream (enable = 1); svtme_kernel_ms returns the last job's kernel time. */
+/* Time the ME kernels of every job with HIP events on the context's stream
+ * (enable = 1); svtme_kernel_ms returns the last job's time over all of its
+ * kernels, svtme_stage_ms the part of stage 0 (k_stage_a: zz / pre-HME /
+ * HME-L0), 1 (k_stage_b: HME-L1/L2 + centres) or 2 (k_stage_c: full-pel +
+ * candidates). */
 svtme_status svtme_set_timing(svtme_ctx *ctx, int enable);
 float svtme_kernel_ms(svtme_ctx *ctx);
+float svtme_stage_ms(svtme_ctx *ctx, int stage);
 /* Device pointer of the last job's record buffer (for RCCL all-gather). */
 void *svtme_device_records(svtme_ctx *ctx, uint64_t *bytes);
 /* The HIP stream (hipStream_t) the context launches on, for event timing. */

@@ -30,7 +30,7 @@ extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int l
                                               hipStream_t s);
 extern "C" hipError_t svtme_launch_me(const DevJob *dj, uint32_t sb_count, hipStream_t s);
 extern "C" hipError_t svtme_launch_me2(const DevJob *dj, uint32_t sb_count, hipStream_t s);
-extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s);
+extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 
 // ----------------------------------------------------------------------------
@@ -89,6 +89,7 @@ struct svtme_ctx {
     bool last_has_sb    = false;
     bool timing         = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_mid[2] = {nullptr, nullptr}; // after stage A, after stage B
     ARes *d_ares    = nullptr; // stage-A results [count][SVTME_A_N]
     size_t ares_cap = 0;
     BState *d_bst   = nullptr; // stage-B state [count]
@@ -145,6 +146,9 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         (void)hipEventDestroy(c->ev0);
     if (c->ev1)
         (void)hipEventDestroy(c->ev1);
+    for (auto &e : c->ev_mid)
+        if (e)
+            (void)hipEventDestroy(e);
 #ifdef SVTME_STAMPS
     if (c->stamp_n) {
         fprintf(stderr, "[svtme stamps] %llu SBs, mean cycles per phase (from previous stamp):",
@@ -419,7 +423,7 @@ static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_
     else if (kernel_version == 2)
         HIP_TRY(svtme_launch_me2(&dj, count, c->stream));
     else
-        HIP_TRY(svtme_launch_stages(&dj, count, c->stream));
+        HIP_TRY(svtme_launch_stages(&dj, count, c->stream, c->timing ? c->ev_mid : nullptr));
 #ifdef SVTME_STAMPS
     {
         std::vector<unsigned long long> h((size_t)count * 16);
@@ -462,6 +466,8 @@ extern "C" svtme_status svtme_set_timing(svtme_ctx *c, int enable) {
     if (enable && !c->ev0) {
         HIP_TRY(hipEventCreate(&c->ev0));
         HIP_TRY(hipEventCreate(&c->ev1));
+        HIP_TRY(hipEventCreate(&c->ev_mid[0]));
+        HIP_TRY(hipEventCreate(&c->ev_mid[1]));
     }
     c->timing = enable != 0;
     return SVTME_OK;
@@ -472,6 +478,17 @@ extern "C" float svtme_kernel_ms(svtme_ctx *c) {
         return -1.0f;
     float ms = -1.0f;
     if (hipEventSynchronize(c->ev1) != hipSuccess || hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess)
+        return -1.0f;
+    return ms;
+}
+
+extern "C" float svtme_stage_ms(svtme_ctx *c, int stage) {
+    if (!c || !c->timing || stage < 0 || stage > 2 || !c->ev_mid[0])
+        return -1.0f;
+    hipEvent_t a = stage == 0 ? c->ev0 : c->ev_mid[stage - 1];
+    hipEvent_t b = stage == 2 ? c->ev1 : c->ev_mid[stage];
+    float ms = -1.0f;
+    if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess)
         return -1.0f;
     return ms;
 }

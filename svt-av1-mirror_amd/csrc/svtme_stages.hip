@@ -1567,12 +1567,17 @@ extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t
     *count = n;
 }
 
-extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s) {
+// mid (optional): two events recorded after stage A and after stage B
+extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid) {
     if (dj->ta_count) {
         const uint32_t waves = sb_count * dj->ta_count;
         hipLaunchKernelGGL(svtme::k_stage_a, dim3((waves + 3) / 4), dim3(256), 0, s, *dj);
     }
+    if (mid)
+        (void)hipEventRecord(mid[0], s);
     hipLaunchKernelGGL(svtme::k_stage_b, dim3(sb_count), dim3(256), 0, s, *dj);
+    if (mid)
+        (void)hipEventRecord(mid[1], s);
     if (dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH)
         hipLaunchKernelGGL(svtme::k_stage_c<false>, dim3(sb_count), dim3(256), 0, s, *dj);
     else

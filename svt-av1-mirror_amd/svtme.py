@@ -500,6 +500,8 @@ def load_product():
         lib.svtme_set_timing.restype = C.c_int32
         lib.svtme_kernel_ms.argtypes = [vp]
         lib.svtme_kernel_ms.restype = C.c_float
+        lib.svtme_stage_ms.argtypes = [vp, C.c_int]
+        lib.svtme_stage_ms.restype = C.c_float
         lib.svtme_device_records.argtypes = [vp, C.POINTER(C.c_uint64)]
         lib.svtme_device_records.restype = vp
         lib.svtme_stream.argtypes = [vp]
@@ -587,6 +589,10 @@ class GpuME:
 
     def kernel_ms(self) -> float:
         return float(self.lib.svtme_kernel_ms(self.ctx))
+
+    def stage_ms(self, stage: int) -> float:
+        """Last job's time in stage 0 (k_stage_a), 1 (k_stage_b) or 2 (k_stage_c)."""
+        return float(self.lib.svtme_stage_ms(self.ctx, stage))
 
     def sync(self):
         self._check(self.lib.svtme_sync(self.ctx), "svtme_sync")
