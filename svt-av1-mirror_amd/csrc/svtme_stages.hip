@@ -44,8 +44,9 @@ namespace svtme {
 #define STAMP(k) do { } while (0)
 #endif
 
-#define STAGE_A_BUF_DW 1152 // per-wave window buffers (dwords)
+#define STAGE_A_BUF_DW 1664 // per-wave window buffers (dwords)
 #define STAGE_B_BUF_DW 1280
+#define STAGE_B_GROUP 2 // windows staged together per wave
 
 // ----------------------------------------------------------------------------
 // Wavefront SAD searches (sad_loop, compute_sad_c.c:58-101)
@@ -178,10 +179,9 @@ __device__ __forceinline__ SadGeo sad_geo(const uint8_t *pbase, int pstride, int
 }
 
 // Wave copy of a window (wrows x wdw dwords from dword-aligned plane rows gs
-// dwords apart) into LDS rows `pitch` dwords apart; loads are issued 8 deep
-// so a window costs about one memory round trip. No fence: the caller
-// publishes the LDS writes (wave_lds_fence) once everything is staged.
-__device__ __forceinline__ void wave_stage(uint32_t *buf, int pitch, const uint32_t *g, int gs, int wrows, int wdw) {
+// dwords apart) into LDS rows `pitch` dwords apart, general form (any width).
+__device__ __forceinline__ void wave_stage_generic(uint32_t *buf, int pitch, const uint32_t *g, int gs, int wrows,
+                                                   int wdw) {
     const int lane    = threadIdx.x & 63;
     const int n       = wrows * wdw;
     const uint32_t mw = magic_of(wdw);
@@ -206,16 +206,87 @@ __device__ __forceinline__ void wave_stage(uint32_t *buf, int pitch, const uint3
     }
 }
 
+// A window to stage (wave-uniform). Windows up to 64 dwords wide are copied
+// in passes of 8 row groups: lane -> (row in group, dword) once, rows clamped
+// to the last row (duplicate copies are harmless), no per-element division.
+struct Win {
+    const uint32_t *g; // first row in the plane (dword aligned)
+    uint32_t *dst;     // LDS
+    int gs, wrows, wdw, pitch, rpi, passes;
+};
+
+__device__ __forceinline__ Win make_win(const uint32_t *g, int gs, int wrows, int wdw, int pitch, uint32_t *dst) {
+    Win w;
+    w.g = g, w.gs = gs, w.wrows = wrows, w.wdw = wdw, w.pitch = pitch, w.dst = dst;
+    w.rpi    = wdw <= 64 ? mdiv(64, magic_of(wdw)) : 0;
+    w.passes = w.rpi ? (wrows + 8 * w.rpi - 1) / (8 * w.rpi) : 0;
+    return w;
+}
+
+__device__ __forceinline__ void win_lane(const Win &w, int *sub, int *d) {
+    const int lane = threadIdx.x & 63;
+    int s          = mdiv(lane, magic_of(w.wdw));
+    *d             = lane - s * w.wdw;
+    *sub           = s < w.rpi ? s : w.rpi - 1;
+}
+
+__device__ __forceinline__ void win_load(const Win &w, int pass, uint32_t v[8]) {
+    int sub, d;
+    win_lane(w, &sub, &d);
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const int r = min((pass * 8 + u) * w.rpi + sub, w.wrows - 1);
+        v[u]        = w.g[(ptrdiff_t)r * w.gs + d];
+    }
+}
+
+__device__ __forceinline__ void win_store(const Win &w, int pass, const uint32_t v[8]) {
+    int sub, d;
+    win_lane(w, &sub, &d);
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const int r                 = min((pass * 8 + u) * w.rpi + sub, w.wrows - 1);
+        w.dst[r * w.pitch + d]      = v[u];
+    }
+}
+
+// Stage the windows k of w[] with bit k of `mask` set, every pass's loads of
+// all windows in flight together (one memory round trip per pass). No fence
+// (see wave_lds_fence).
+template <int NW>
+__device__ __forceinline__ void stage_windows(const Win (&w)[NW], uint32_t mask) {
+    int maxp = 0;
+#pragma unroll
+    for (int k = 0; k < NW; k++)
+        if ((mask >> k) & 1u) {
+            if (w[k].rpi)
+                maxp = max(maxp, w[k].passes);
+            else
+                wave_stage_generic(w[k].dst, w[k].pitch, w[k].g, w[k].gs, w[k].wrows, w[k].wdw);
+        }
+    for (int pass = 0; pass < maxp; pass++) {
+        uint32_t v[NW][8];
+#pragma unroll
+        for (int k = 0; k < NW; k++)
+            if (((mask >> k) & 1u) && w[k].rpi && pass < w[k].passes)
+                win_load(w[k], pass, v[k]);
+#pragma unroll
+        for (int k = 0; k < NW; k++)
+            if (((mask >> k) & 1u) && w[k].rpi && pass < w[k].passes)
+                win_store(w[k], pass, v[k]);
+    }
+}
+
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void sad_stage(const SadGeo &g, uint32_t *buf) {
-    if (g.staged && g.nitems)
-        wave_stage(buf, g.pitch, g.g, g.gs, g.wrows, g.wdw);
+__device__ __forceinline__ Win sad_win(const SadGeo &g, uint32_t *buf) {
+    return make_win(g.g, g.gs, g.wrows, g.wdw, g.pitch, buf);
 }
+__device__ __forceinline__ bool sad_staged(const SadGeo &g) { return g.staged && g.nitems; }
 
 // The search itself; returns the wave-uniform best key (sad << 32 | y << 16 | x),
 // ~0 if nothing was searched.
@@ -332,6 +403,30 @@ __device__ __forceinline__ void copy_planes(const DevJob &dj, DevPlane (*pl)[NLV
 // ----------------------------------------------------------------------------
 // Stage A: every independent search of every SB, one wavefront each
 // ----------------------------------------------------------------------------
+// zz SAD of a full 64x64 SB (sub rows: 32 x 16 dwords), loads issued up front
+struct ZzLoads {
+    uint32_t r[8], c[8];
+};
+__device__ __forceinline__ void zz_issue(ZzLoads &z, const uint8_t *ref, int rstride, const uint8_t *cur, int cstride) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const int e = u * 64 + lane, row = e >> 4, j = e & 15;
+        z.r[u] = *((const uint32_t *)(ref + (ptrdiff_t)row * rstride) + j);
+        z.c[u] = *((const uint32_t *)(cur + (ptrdiff_t)row * cstride) + j);
+    }
+}
+__device__ __forceinline__ uint32_t zz_finish(const ZzLoads &z) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < 8; u++) acc = __builtin_amdgcn_sad_u8(z.r[u], z.c[u], acc);
+    return wave_sum_u32(acc);
+}
+
+// Stage A wave kinds (DevJob.ta_list entry = kind << 3 | slot)
+#define TA_HME 0 // zz SAD + the four HME-L0 quadrants of one slot
+#define TA_PH 1  // the two pre-HME regions of one slot
+
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_stage_a(const DevJob dj) {
     __shared__ __attribute__((aligned(16))) uint8_t srcb[4][256];
     __shared__ uint32_t wbuf[4][STAGE_A_BUF_DW];
@@ -343,60 +438,141 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     if (gw >= total)
         return;
     const uint32_t sb_local = UNI(gw / dj.ta_count);
-    const int t             = UNI(dj.ta_list[gw - sb_local * dj.ta_count]);
-    const SbGeo G           = sb_geo(dj, sb_local);
-    ARes *out               = dj.ares + (size_t)sb_local * SVTME_A_N + t;
-    const bool hsub         = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
-    if (t < SVTME_A_PH) { // zz SAD (init_zz_sad, motion_estimation.c:2382-2437)
-        const int s       = t;
-        const DevPlane &P = dj.ref[s >> 2][s & 3].lv[0];
-        const DevPlane &C = dj.cur.lv[0];
-        const uint32_t v  = wave_nxm(P.base + (ptrdiff_t)G.oy * P.stride + G.ox, 2 * P.stride,
-                                     C.base + (ptrdiff_t)G.oy * C.stride + G.ox, 2 * C.stride, (int)(G.bh >> 1),
-                                     (int)G.bw);
-        if (lane == 0)
-            *out = ARes{v, 0, 0};
-        return;
-    }
-    // sixteenth-resolution source block (16 x 16): issued now, stored with the window
+    const int entry         = UNI(dj.ta_list[gw - sb_local * dj.ta_count]);
+    const int kind = entry >> 3, s = entry & 7, l = s >> 2, r = s & 3;
+    const SbGeo G   = sb_geo(dj, sb_local);
+    ARes *out       = dj.ares + (size_t)sb_local * SVTME_A_N;
+    const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
+    const DevPlane &P   = dj.ref[l][r].lv[2];
+    const uint16_t dist = ref_dist_const(job, l, r);
+    uint32_t *buf       = wbuf[wid];
+
+    // sixteenth-resolution source block (16 x 16): issued first, stored with the windows
     const DevPlane &S = dj.cur.lv[2];
     uint4 sv          = make_uint4(0, 0, 0, 0);
     if (lane < 16)
         sv = *(const uint4 *)(S.base + (ptrdiff_t)((G.oy >> 2) + lane) * S.stride + (G.ox >> 2));
     const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
     const int bws = (int)(G.bw >> 2), bhs = hsub ? (int)(G.bh >> 2) >> 1 : (int)(G.bh >> 2);
-    const bool is_ph = t < SVTME_A_L0;
-    const int s      = is_ph ? (t - SVTME_A_PH) >> 1 : (t - SVTME_A_L0) >> 2;
-    const int l = s >> 2, r = s & 3;
-    const DevPlane &P   = dj.ref[l][r].lv[2];
-    const uint16_t dist = ref_dist_const(job, l, r);
-    int16_t xo, yo, sw, shh;
-    if (is_ph) { // pre-HME region (prehme_core, motion_estimation.c:1568-1636)
-        const int sr        = (t - SVTME_A_PH) & 1;
-        const uint32_t f    = scaled_dist(dist);
+
+    if (kind == TA_HME) {
+        // zz SAD (init_zz_sad, motion_estimation.c:2382-2437)
+        const bool zz   = c.me_early_exit_th || c.me_safe_limit_zz_th;
+        const bool zz64 = zz && G.bw == 64 && G.bh == 64;
+        const DevPlane &F = dj.ref[l][r].lv[0];
+        const DevPlane &C = dj.cur.lv[0];
+        const uint8_t *zr = F.base + (ptrdiff_t)G.oy * F.stride + G.ox;
+        const uint8_t *zc = C.base + (ptrdiff_t)G.oy * C.stride + G.ox;
+        ZzLoads zl;
+        if (zz64)
+            zz_issue(zl, zr, 2 * F.stride, zc, 2 * C.stride);
+        // the four HME-L0 quadrants (hme_level_0, motion_estimation.c:835-889), staged as one box
+        const bool l0 = c.enable_hme_flag && c.enable_hme_level0_flag;
+        SadGeo gq[4];
+        int16_t qxo[4], qyo[4];
+        int boxl = 0x7fff, boxt = 0x7fff, wdwb = 0, wrowsb = 0;
+        if (l0) {
+            int16_t sa_w, sa_h;
+            hme_l0_area(c, l, r, dist, 0, 0, &sa_w, &sa_h);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                int16_t sw, shh;
+                hme_l0_rect(c, P, sox, soy, sa_w, sa_h, q >> 1, q & 1, &qxo[q], &qyo[q], &sw, &shh);
+                gq[q] = sad_geo(P.base, P.stride, sox + qxo[q], soy + qyo[q], sw, shh, bws, bhs, hsub, false,
+                                0x7fffffff);
+                if (gq[q].nitems) {
+                    boxl = min(boxl, sox + qxo[q]);
+                    boxt = min(boxt, soy + qyo[q]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (gq[q].nitems) {
+                    const int dwo = ((sox + qxo[q]) >> 2) - (boxl >> 2), rwo = soy + qyo[q] - boxt;
+                    wdwb   = max(wdwb, dwo + gq[q].wdw);
+                    wrowsb = max(wrowsb, rwo + gq[q].wrows);
+                }
+        }
+        const int pitchb  = wdwb | 1;
+        const bool staged = l0 && wdwb > 0 && wrowsb * pitchb <= STAGE_A_BUF_DW;
+        if (staged) {
+            const Win w[1] = {make_win((const uint32_t *)(P.base + (ptrdiff_t)boxt * P.stride) + (boxl >> 2),
+                                       P.stride >> 2, wrowsb, wdwb, pitchb, buf)};
+            stage_windows<1>(w, 1u);
+        }
+        if (lane < 16)
+            ((uint4 *)srcb[wid])[lane] = sv;
+        wave_lds_fence();
+        if (zz) {
+            const uint32_t v = zz64 ? zz_finish(zl)
+                                    : wave_nxm(zr, 2 * F.stride, zc, 2 * C.stride, (int)(G.bh >> 1), (int)G.bw);
+            if (lane == 0)
+                out[SVTME_A_ZZ + s] = ARes{v, 0, 0};
+        }
+        if (l0) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                SadGeo g         = gq[q];
+                const uint32_t *o = buf;
+                if (staged) {
+                    g.staged = 1;
+                    g.pitch  = pitchb;
+                    o        = buf + (soy + qyo[q] - boxt) * pitchb + (((sox + qxo[q]) >> 2) - (boxl >> 2));
+                } else {
+                    g.staged = 0;
+                }
+                const unsigned long long k = sad_compute<RW_4>(g, o, srcb[wid], hsub ? 32 : 16);
+                if (lane == 0) {
+                    uint32_t best;
+                    int x, y;
+                    key_result(k, &best, &x, &y);
+                    out[SVTME_A_L0 + s * 4 + q] =
+                        ARes{hsub ? best * 2 : best, i16((x + qxo[q]) * 4), i16((y + qyo[q]) * 4)};
+                }
+            }
+        }
+        return;
+    }
+    // pre-HME: both regions (prehme_core, motion_estimation.c:1568-1636), staged together
+    SadGeo gr[2];
+    int16_t rxo[2], ryo[2];
+    int off = 0;
+    Win w[2];
+    uint32_t mask = 0;
+    const uint32_t f = scaled_dist(dist);
+#pragma unroll
+    for (int sr = 0; sr < 2; sr++) {
         const uint16_t sa_w = (uint16_t)min((uint32_t)c.prehme_sa_cfg[sr].sa_min.width * f,
                                             (uint32_t)c.prehme_sa_cfg[sr].sa_max.width);
         const uint16_t sa_h = (uint16_t)min((uint32_t)c.prehme_sa_cfg[sr].sa_min.height * f,
                                             (uint32_t)c.prehme_sa_cfg[sr].sa_max.height);
-        prehme_area(P, sox, soy, (int16_t)sa_w, (int16_t)sa_h, &xo, &yo, &sw, &shh);
-    } else { // HME level-0 quadrant (hme_level_0, motion_estimation.c:835-889)
-        const int q = (t - SVTME_A_L0) & 3;
-        int16_t sa_w, sa_h;
-        hme_l0_area(c, l, r, dist, 0, 0, &sa_w, &sa_h);
-        hme_l0_rect(c, P, sox, soy, sa_w, sa_h, q >> 1, q & 1, &xo, &yo, &sw, &shh);
+        int16_t sw, shh;
+        prehme_area(P, sox, soy, (int16_t)sa_w, (int16_t)sa_h, &rxo[sr], &ryo[sr], &sw, &shh);
+        gr[sr] = sad_geo(P.base, P.stride, sox + rxo[sr], soy + ryo[sr], sw, shh, bws, bhs, hsub,
+                         c.prehme_skip_search_line, STAGE_A_BUF_DW - off);
+        if (sad_staged(gr[sr])) {
+            w[sr] = sad_win(gr[sr], buf + off);
+            mask |= 1u << sr;
+            off += gr[sr].wrows * gr[sr].pitch;
+        }
     }
-    const SadGeo g = sad_geo(P.base, P.stride, sox + xo, soy + yo, sw, shh, bws, bhs, hsub,
-                             is_ph && c.prehme_skip_search_line, STAGE_A_BUF_DW);
-    sad_stage(g, wbuf[wid]);
+    stage_windows<2>(w, mask);
     if (lane < 16)
         ((uint4 *)srcb[wid])[lane] = sv;
     wave_lds_fence();
-    const unsigned long long k = sad_compute<RW_4>(g, wbuf[wid], srcb[wid], hsub ? 32 : 16);
-    if (lane == 0) {
-        uint32_t best;
-        int x, y;
-        key_result(k, &best, &x, &y);
-        *out = ARes{hsub ? best * 2 : best, i16((x + xo) * 4), i16((y + yo) * 4)};
+    off = 0;
+#pragma unroll
+    for (int sr = 0; sr < 2; sr++) {
+        const unsigned long long k = sad_compute<RW_4>(gr[sr], buf + off, srcb[wid], hsub ? 32 : 16);
+        if (sad_staged(gr[sr]))
+            off += gr[sr].wrows * gr[sr].pitch;
+        if (lane == 0) {
+            uint32_t best;
+            int x, y;
+            key_result(k, &best, &x, &y);
+            out[SVTME_A_PH + s * 2 + sr] =
+                ARes{hsub ? best * 2 : best, i16((x + rxo[sr]) * 4), i16((y + ryo[sr]) * 4)};
+        }
     }
 }
 
@@ -434,7 +610,7 @@ struct StB {
     uint32_t wbuf[4][STAGE_B_BUF_DW];
 };
 
-__global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_b(const DevJob dj) {
     __shared__ StB st;
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
@@ -610,7 +786,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
         }
     }
     __syncthreads();
-    STAMP(3);
+    STAMP(2);
 
     // ---- HME level 1 / 2 (motion_estimation.c:2041-2177)
     for (int level = 1; level <= 2; level++) {
@@ -677,7 +853,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
                 st.nbt = tot;
         }
         __syncthreads();
-        STAMP(4);
+        STAMP(3);
         {
             const int bwl = level == 1 ? (int)(bw >> 1) : (int)bw;
             const int bhl = level == 1 ? (int)(bh >> 1) : (int)bh;
@@ -692,14 +868,25 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
                                hsub ? bhl >> 1 : bhl, hsub, false, room);
             };
             int off = 0;
-            for (int t = wid; t < nbt; t += 4) {
-                const SadGeo g = geo(t, STAGE_B_BUF_DW - off);
-                if (g.staged && g.nitems) {
-                    sad_stage(g, st.wbuf[wid] + off);
-                    off += g.wrows * g.pitch;
+            for (int t0 = wid; t0 < nbt; t0 += 4 * STAGE_B_GROUP) { // this wave's tasks, a group at a time
+                Win w[STAGE_B_GROUP];
+                uint32_t mask = 0;
+#pragma unroll
+                for (int k = 0; k < STAGE_B_GROUP; k++) {
+                    const int t = t0 + 4 * k;
+                    if (t < nbt) {
+                        const SadGeo g = geo(t, STAGE_B_BUF_DW - off);
+                        if (sad_staged(g)) {
+                            w[k] = sad_win(g, st.wbuf[wid] + off);
+                            mask |= 1u << k;
+                            off += g.wrows * g.pitch;
+                        }
+                    }
                 }
+                stage_windows<STAGE_B_GROUP>(w, mask);
             }
             wave_lds_fence();
+            STAMP(4);
             off = 0;
             for (int t = wid; t < nbt; t += 4) {
                 const SadGeo g = geo(t, STAGE_B_BUF_DW - off);
@@ -709,6 +896,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
                 if (lane == 0)
                     st.bkey[t] = k;
             }
+            STAMP(5);
         }
         __syncthreads();
         if (w0 && lane < st.nbt) {
@@ -723,7 +911,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
             st.ly[level][s][q]     = i16((y + T.yo) * mul);
         }
         __syncthreads();
-        STAMP(5);
+        STAMP(6);
     }
 
     // ---- set_final_seach_centre_sb (motion_estimation.c:2182-2380) + hme_prune_ref_and_adjust_sr (:2477-2518)
@@ -809,6 +997,7 @@ __global__ void __launch_bounds__(256) k_stage_b(const DevJob dj) {
             b->do_ref[s]     = dref;
         }
     }
+    STAMP(7);
 }
 
 // ----------------------------------------------------------------------------
@@ -1268,7 +1457,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     const uint32_t vmask = valid_mask(job);
 
     const DevPlane &C = dj.cur.lv[0]; // source block read in place (me_process.c:183-214)
-    STAMP(6);
+    STAMP(8);
     if (tid == 0) {
 #pragma unroll
         for (int s = 0; s < 8; s++) {
@@ -1289,7 +1478,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
     for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) (&st.best_mv[0][0])[e] = 0;
     __syncthreads();
-    STAMP(7);
+    STAMP(9);
 
     // ---- integer_search_b64 (motion_estimation.c:1249-1516); lane s of wave 0 owns slot s.
     // Two rounds when enable_me_sr_adjustment == 2: the other slots read slot 0's 64x64 SAD.
@@ -1351,7 +1540,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 st.nreq = tot;
         }
         __syncthreads();
-        STAMP(8);
+        STAMP(10);
         if (st.nreq) {
             for (int q = wid; q < 2 * st.nreq; q += 4) {
                 const uint32_t v = wave_nxm(st.req[q], st.req_stride[q], C.base + (ptrdiff_t)oy * C.stride + ox,
@@ -1405,7 +1594,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 st.k32 = 1; // a single position
         }
         __syncthreads();
-        STAMP(9);
+        STAMP(11);
         for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) {
             const int s = e / SVTME_PU_COUNT;
             if (st.in_round[s])
@@ -1413,7 +1602,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
         if (st.nfp) {
             fullpel<SUB_ME>(st, C, ox, oy); // centre probe (motion_estimation.c:1414-1417)
-            STAMP(10);
+            STAMP(12);
             // 8x8-variance resize (motion_estimation.c:1418-1438)
             if (w0 && lane < 8 && st.in_round[lane] && c.me_8x8_var_enabled && (st.is_w[lane] * st.is_h[lane] > 24)) {
                 const int s = lane;
@@ -1473,7 +1662,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 st.k32 = k32;
         }
         __syncthreads();
-        STAMP(11);
+        STAMP(13);
         if (st.nfp)
             fullpel<SUB_ME>(st, C, ox, oy);
     }
@@ -1503,7 +1692,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
     }
     __syncthreads();
-    STAMP(12);
+    STAMP(14);
 
     // ---- records (sb_count x R, slots in list-0-then-list-1 order)
     {
@@ -1536,10 +1725,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
     if (dj.out_sb) {
         __syncthreads();
-        STAMP(13);
+        
         finish_sb(st, dj, sb_local, bw, bh);
     }
-    STAMP(14);
+    STAMP(15);
 }
 
 } // namespace svtme
@@ -1555,14 +1744,10 @@ extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t
             continue;
         if (!(job->temporal_layer_index > 0 || l == 0))
             continue;
-        if (c.me_early_exit_th || c.me_safe_limit_zz_th)
-            list[n++] = (uint8_t)(SVTME_A_ZZ + s);
-        if (c.prehme_enable) {
-            list[n++] = (uint8_t)(SVTME_A_PH + s * 2);
-            list[n++] = (uint8_t)(SVTME_A_PH + s * 2 + 1);
-        }
-        if (c.enable_hme_flag && c.enable_hme_level0_flag)
-            for (int q = 0; q < 4; q++) list[n++] = (uint8_t)(SVTME_A_L0 + s * 4 + q);
+        if (c.me_early_exit_th || c.me_safe_limit_zz_th || (c.enable_hme_flag && c.enable_hme_level0_flag))
+            list[n++] = (uint8_t)((TA_HME << 3) | s);
+        if (c.prehme_enable)
+            list[n++] = (uint8_t)((TA_PH << 3) | s);
     }
     *count = n;
 }
