@@ -539,3 +539,78 @@ void svtref_derive_controls(int enc_mode, int qp, int input_resolution, int temp
     free(pcs);
     free(scs);
 }
+
+/* ---------------------------------------------------------------------------
+ * Per-kernel entry points: the reference's rtcd pointers as selected by
+ * svtref_set_simd (C or AVX2), exported for the kernel-level parity tests.
+ * ------------------------------------------------------------------------- */
+void svtref_sad_loop_kernel(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                            uint32_t block_height, uint32_t block_width, uint64_t *best_sad, int16_t *x_search_center,
+                            int16_t *y_search_center, uint32_t src_stride_raw, uint8_t skip_search_line,
+                            int16_t search_area_width, int16_t search_area_height) {
+    ensure_kernels();
+    svt_sad_loop_kernel(src, src_stride, ref, ref_stride, block_height, block_width, best_sad, x_search_center,
+                        y_search_center, src_stride_raw, skip_search_line, search_area_width, search_area_height);
+}
+
+uint32_t svtref_nxm_sad_kernel(const uint8_t *src, uint32_t src_stride, const uint8_t *ref, uint32_t ref_stride,
+                               uint32_t height, uint32_t width) {
+    ensure_kernels();
+    return svt_nxm_sad_kernel(src, src_stride, ref, ref_stride, height, width);
+}
+
+uint32_t svt_aom_sad_16b_kernel_c(uint16_t *src, uint32_t src_stride, uint16_t *ref, uint32_t ref_stride,
+                                  uint32_t height, uint32_t width); /* compute_sad_c.c:39 */
+
+uint32_t svtref_sad_16b_kernel(uint16_t *src, uint32_t src_stride, uint16_t *ref, uint32_t ref_stride,
+                               uint32_t height, uint32_t width) {
+    return svt_aom_sad_16b_kernel_c(src, src_stride, ref, ref_stride, height, width);
+}
+
+void svtref_ext_sad_calculation_8x8_16x16(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                                          uint32_t *p_best_sad_8x8, uint32_t *p_best_sad_16x16,
+                                          uint32_t *p_best_mv8x8, uint32_t *p_best_mv16x16, uint32_t mv,
+                                          uint32_t *p_sad16x16, uint32_t *p_sad8x8, bool sub_sad) {
+    ensure_kernels();
+    svt_ext_sad_calculation_8x8_16x16(src, src_stride, ref, ref_stride, p_best_sad_8x8, p_best_sad_16x16,
+                                      p_best_mv8x8, p_best_mv16x16, mv, p_sad16x16, p_sad8x8, sub_sad);
+}
+
+void svtref_ext_sad_calculation_32x32_64x64(uint32_t *p_sad16x16, uint32_t *p_best_sad_32x32,
+                                            uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
+                                            uint32_t *p_best_mv64x64, uint32_t mv, uint32_t *p_sad32x32) {
+    ensure_kernels();
+    svt_ext_sad_calculation_32x32_64x64(p_sad16x16, p_best_sad_32x32, p_best_sad_64x64, p_best_mv32x32,
+                                        p_best_mv64x64, mv, p_sad32x32);
+}
+
+void svtref_ext_all_sad_calculation_8x8_16x16(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                                              uint32_t mv, uint32_t *p_best_sad_8x8, uint32_t *p_best_sad_16x16,
+                                              uint32_t *p_best_mv8x8, uint32_t *p_best_mv16x16,
+                                              uint32_t p_eight_sad16x16[16][8], uint32_t p_eight_sad8x8[64][8],
+                                              bool sub_sad) {
+    ensure_kernels();
+    svt_ext_all_sad_calculation_8x8_16x16(src, src_stride, ref, ref_stride, mv, p_best_sad_8x8, p_best_sad_16x16,
+                                          p_best_mv8x8, p_best_mv16x16, p_eight_sad16x16, p_eight_sad8x8, sub_sad);
+}
+
+void svtref_ext_eight_sad_calculation_32x32_64x64(uint32_t p_sad16x16[16][8], uint32_t *p_best_sad_32x32,
+                                                  uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
+                                                  uint32_t *p_best_mv64x64, uint32_t mv, uint32_t p_sad32x32[4][8]) {
+    ensure_kernels();
+    svt_ext_eight_sad_calculation_32x32_64x64(p_sad16x16, p_best_sad_32x32, p_best_sad_64x64, p_best_mv32x32,
+                                              p_best_mv64x64, mv, p_sad32x32);
+}
+
+void svtref_initialize_buffer_32bits(uint32_t *pointer, uint32_t count128, uint32_t count32, uint32_t value) {
+    ensure_kernels();
+    svt_initialize_buffer_32bits(pointer, count128, count32, value);
+}
+
+void svtref_downsample_2d(uint8_t *input_samples, uint32_t input_stride, uint32_t input_area_width,
+                          uint32_t input_area_height, uint8_t *decim_samples, uint32_t decim_stride,
+                          uint32_t decim_step) {
+    ensure_kernels();
+    downsample_2d(input_samples, input_stride, input_area_width, input_area_height, decim_samples, decim_stride,
+                  decim_step);
+}

@@ -70,8 +70,28 @@ def digest(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
+def rtcd_golden():
+    """Per-kernel outputs of the reference's C kernels (AVX2 must agree)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import rtcd_cases as R
+
+    ref = S.load_ref()
+    out = {}
+    for name, run in R.all_cases():
+        ref.svtref_set_simd(0)
+        a = run(ref, "svtref_")
+        ref.svtref_set_simd(1)
+        b = run(ref, "svtref_")
+        for k in a:
+            assert np.array_equal(a[k], b[k]), (name, k)
+            out[f"{name}/{k}"] = a[k]
+    np.savez_compressed(os.path.join(HERE, "rtcd_cases.npz"), **out)
+    print("rtcd cases", len(out))
+
+
 def main():
     ref = S.load_ref()
+    rtcd_golden()
     with open(os.path.join(HERE, "controls.json"), "w") as fh:
         json.dump(controls_golden(), fh, indent=0)
     meta = []
