@@ -157,6 +157,8 @@ def main():
     achieved = bps * n_sb / (k_avg_ms * 1e-3) / 1e9
     stages = {}
     for i, name in enumerate(STAGE_NAMES):
+        if s_avg_ms[i] <= 0:  # concurrent SB-band parts: no per-stage split
+            continue
         st = {"avg_ms": round(float(s_avg_ms[i]), 4)}
         if wl["windows"] in STAGE_BYTES:
             src_b, per_ref = STAGE_BYTES[wl["windows"]][i]

@@ -81,6 +81,15 @@ __device__ __forceinline__ int mdiv(int n, uint32_t m) { return m ? (int)__umulh
 
 #define UNI(x) __builtin_amdgcn_readfirstlane((int)(x))
 
+// a pointer known to be wave-uniform, moved to SGPRs (enables base + 32-bit offset addressing)
+template <typename T>
+__device__ __forceinline__ T *uni_ptr(T *p) {
+    const uint64_t v  = (uint64_t)(uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (T *)(uintptr_t)(((uint64_t)hi << 32) | lo);
+}
+
 // v_qsad_pk_u16_u8: 4 SADs of one source dword against the 4 byte shifts of a
 // reference dword pair, accumulated in 4 u16 lanes
 __device__ __forceinline__ unsigned long long qsad(uint32_t lo, uint32_t hi, uint32_t s, unsigned long long a) {

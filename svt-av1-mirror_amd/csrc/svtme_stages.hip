@@ -233,10 +233,11 @@ __device__ __forceinline__ void win_lane(const Win &w, int *sub, int *d) {
 __device__ __forceinline__ void win_load(const Win &w, int pass, uint32_t v[8]) {
     int sub, d;
     win_lane(w, &sub, &d);
+    const char *gb = (const char *)uni_ptr(w.g); // uniform base + 32-bit byte offsets
 #pragma unroll
     for (int u = 0; u < 8; u++) {
         const int r = min((pass * 8 + u) * w.rpi + sub, w.wrows - 1);
-        v[u]        = w.g[(ptrdiff_t)r * w.gs + d];
+        v[u]        = *(const uint32_t *)(gb + (uint32_t)(r * w.gs + d) * 4u);
     }
 }
 
