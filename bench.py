@@ -37,8 +37,9 @@ WINDOW_BYTES = {"p8": 16798, "p6": 38121, "p8_sa64": 28241}
 # the same bytes split over the three stage kernels (p8 stage breakdown of SURVEY.md 8(d):
 # zz 2048 + pre-HME 2645 + 1034 + HME-L0 1081 | HME-L1 5304 | full-pel 4686 + 680 out;
 # source 64x32 + 16x8 in stage A, 32x16 in stage B)
-STAGE_BYTES = {"p8": ((2176, 6808), (512, 5304), (0, 4686 + 680))}
-STAGE_NAMES = ("k_stage_a", "k_stage_b", "k_stage_c")
+# (stage D only reads stage A's 448-B result block per SB: no window bytes)
+STAGE_BYTES = {"p8": ((2176, 6808), (0, 0), (512, 5304), (0, 4686 + 680))}
+STAGE_NAMES = ("k_stage_a", "k_stage_d", "k_stage_b", "k_stage_c")
 
 WORKLOADS = {
     "4k_p8": dict(w=3840, h=2160, mode=8, tl=1, l0=(7, 6), l1=(9, 10), windows="p8", ten_bit=False,
@@ -149,7 +150,7 @@ def main():
     for _ in range(args.kernel_samples):
         gpu.submit_device(job, d_rec.data_ptr(), d_sb.data_ptr())
         kms.append(gpu.kernel_ms())
-        sms.append([gpu.stage_ms(i) for i in range(3)])
+        sms.append([gpu.stage_ms(i) for i in range(len(STAGE_NAMES))])
     gpu.set_timing(False)
     k_avg_ms = float(np.mean(kms))
     s_avg_ms = np.mean(np.array(sms), axis=0)
@@ -163,8 +164,9 @@ def main():
         if wl["windows"] in STAGE_BYTES:
             src_b, per_ref = STAGE_BYTES[wl["windows"]][i]
             b = (src_b + R * per_ref) * n_sb
-            st["bytes_per_launch"] = b
-            st["achieved_gbps"] = round(b / (float(s_avg_ms[i]) * 1e-3) / 1e9, 1)
+            if b:
+                st["bytes_per_launch"] = b
+                st["achieved_gbps"] = round(b / (float(s_avg_ms[i]) * 1e-3) / 1e9, 1)
         stages[name] = st
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
@@ -199,7 +201,7 @@ def main():
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "ME pass = k_stage_a + k_stage_b + k_stage_c (one picture job)",
+                         "kernel": "ME pass = k_stage_a + k_stage_d + k_stage_b + k_stage_c (one picture job)",
                          "kernel_avg_ms": round(k_avg_ms, 4), "bytes_per_launch": bps * n_sb,
                          "stages": stages},
             "cpu_baseline": cpu_baseline,

@@ -41,13 +41,17 @@ struct ARes {
 #define SVTME_A_L0 24
 #define SVTME_A_N 56
 
-// Stage-B output per SB: the SearchResults of every slot after HME and the
-// HME-based pruning (me_context.h:348-355), consumed by stage C.
+// Per-SB state between the stages (svtme_stages.hip). Stage D writes each
+// slot's zz SAD and do_ref after the zz / pre-HME pruning and the level-0
+// centres after the worst-quadrant replacement; stage B writes the level-1/2
+// refinement of every (slot, quadrant); stage C selects the search centre
+// from the highest enabled level (set_final_seach_centre_sb).
 struct BState {
-    uint64_t hme_sad[8];
+    uint64_t lsad[8][4]; // level 0, [slot][q = sx * 2 + sy]
+    uint64_t hsad[8][4]; // highest enabled level above 0
+    int16_t lx[8][4], ly[8][4];
+    int16_t hx[8][4], hy[8][4];
     uint32_t zz[8];
-    uint32_t reduce_div[8];
-    int16_t sc_x[8], sc_y[8];
     uint8_t do_ref[8];
 };
 
@@ -65,6 +69,8 @@ struct DevJob {
     BState *bst;                   // [sb_count] stage-B state
     uint32_t ta_count;             // stage-A searches per SB
     uint8_t ta_list[SVTME_A_N];    // their ARes indices
+    uint32_t tb_count;             // stage-B refinements per SB
+    uint8_t tb_list[32];           // their (slot << 2 | quadrant)
 };
 
 static inline uint32_t svtme_round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }

@@ -32,6 +32,7 @@ extern "C" hipError_t svtme_launch_me(const DevJob *dj, uint32_t sb_count, hipSt
 extern "C" hipError_t svtme_launch_me2(const DevJob *dj, uint32_t sb_count, hipStream_t s);
 extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
+extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 
 // ----------------------------------------------------------------------------
 // errors
@@ -89,7 +90,7 @@ struct svtme_ctx {
     bool last_has_sb    = false;
     bool timing         = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    hipEvent_t ev_mid[2] = {nullptr, nullptr}; // after stage A, after stage B
+    hipEvent_t ev_mid[3] = {nullptr, nullptr, nullptr}; // after stages A, D, B
     // SB-band parts of one job on side streams (stage kernels of different
     // bands overlap on the device); fork/join events on the main stream
     static constexpr int kMaxParts = 4;
@@ -430,6 +431,7 @@ static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_
     dj.ares = c->d_ares;
     dj.bst  = c->d_bst;
     svtme_stage_a_list(&dj.job, dj.ta_list, &dj.ta_count);
+    svtme_stage_b_list(&dj.job, dj.tb_list, &dj.tb_count);
     static const int kernel_version = [] {
         const char *e = getenv("SVTME_KERNEL");
         return e ? atoi(e + (e[0] == 'v')) : 3;
@@ -508,8 +510,8 @@ extern "C" svtme_status svtme_set_timing(svtme_ctx *c, int enable) {
     if (enable && !c->ev0) {
         HIP_TRY(hipEventCreate(&c->ev0));
         HIP_TRY(hipEventCreate(&c->ev1));
-        HIP_TRY(hipEventCreate(&c->ev_mid[0]));
-        HIP_TRY(hipEventCreate(&c->ev_mid[1]));
+        for (auto &e : c->ev_mid)
+            HIP_TRY(hipEventCreate(&e));
     }
     c->timing = enable != 0;
     return SVTME_OK;
@@ -525,10 +527,10 @@ extern "C" float svtme_kernel_ms(svtme_ctx *c) {
 }
 
 extern "C" float svtme_stage_ms(svtme_ctx *c, int stage) {
-    if (!c || !c->timing || stage < 0 || stage > 2 || !c->ev_mid[0] || c->parts > 1)
+    if (!c || !c->timing || stage < 0 || stage > 3 || !c->ev_mid[0] || c->parts > 1)
         return -1.0f; // stages of concurrent parts overlap: no per-stage split
     hipEvent_t a = stage == 0 ? c->ev0 : c->ev_mid[stage - 1];
-    hipEvent_t b = stage == 2 ? c->ev1 : c->ev_mid[stage];
+    hipEvent_t b = stage == 3 ? c->ev1 : c->ev_mid[stage];
     float ms = -1.0f;
     if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess)
         return -1.0f;

@@ -44,9 +44,8 @@ namespace svtme {
 #define STAMP(k) do { } while (0)
 #endif
 
-#define STAGE_A_BUF_DW 1664 // per-wave window buffers (dwords)
-#define STAGE_B_BUF_DW 1280
-#define STAGE_B_GROUP 2 // windows staged together per wave
+#define STAGE_A_BUF_DW 1024 // per-wave window buffers (dwords)
+#define STAGE_B_BUF_DW 640
 
 // ----------------------------------------------------------------------------
 // Wavefront SAD searches (sad_loop, compute_sad_c.c:58-101)
@@ -428,7 +427,7 @@ __device__ __forceinline__ uint32_t zz_finish(const ZzLoads &z) {
 #define TA_HME 0 // zz SAD + the four HME-L0 quadrants of one slot
 #define TA_PH 1  // the two pre-HME regions of one slot
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_stage_a(const DevJob dj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_stage_a(const DevJob dj) {
     __shared__ __attribute__((aligned(16))) uint8_t srcb[4][256];
     __shared__ uint32_t wbuf[4][STAGE_A_BUF_DW];
     const svtme_job &job    = dj.job;
@@ -578,8 +577,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 }
 
 // ----------------------------------------------------------------------------
-// Stage B: decisions of stage A in reference order, HME level 1 / 2, search
-// centre and HME pruning; one workgroup per SB
+// Stage D: the zz / pre-HME / level-0 decisions of stage A's results in the
+// reference's order, one wavefront per SB (lane = slot, or slot x quadrant)
 // ----------------------------------------------------------------------------
 struct PreHme {
     uint64_t sad;
@@ -588,417 +587,389 @@ struct PreHme {
     uint8_t pad[2];
 };
 
-struct BTask {
-    int16_t wx, wy, sa_w, sa_h;
-    int16_t xo, yo;
-    uint8_t slot, q;
-    uint8_t pad[2];
-};
-
-struct StB {
+struct Dec {
     ARes a[SVTME_A_N];
-    DevPlane pl[8][3];
-    uint16_t dist[8];
     uint32_t zz[8];
     uint8_t do_ref[8];
     PreHme ph[8][2];
-    int16_t lx[3][8][4], ly[3][8][4]; // [level][slot][q = sx * 2 + sy]
-    uint64_t lsad[3][8][4];
-    BTask bt[32];
-    unsigned long long bkey[32];
-    int32_t nbt;
-    __attribute__((aligned(16))) uint8_t src[64 * 64];
-    uint32_t wbuf[4][STAGE_B_BUF_DW];
+    int16_t lx[8][4], ly[8][4]; // level 0, [slot][q = sx * 2 + sy]
+    uint64_t lsad[8][4];
 };
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_b(const DevJob dj) {
-    __shared__ StB st;
+__global__ void __launch_bounds__(256) k_stage_d(const DevJob dj) {
+    __shared__ Dec dec[4];
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const bool w0           = wid == 0;
-    const uint32_t sb_local = xcd_remap(blockIdx.x, gridDim.x);
-    const SbGeo G           = sb_geo(dj, sb_local);
-    const uint32_t ox = G.ox, oy = G.oy, bw = G.bw, bh = G.bh;
-    const int nl     = job.num_lists;
-    const bool hsub  = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t sb_local = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (sb_local >= job.sb_count)
+        return;
+    Dec &d               = dec[wid];
+    const SbGeo G        = sb_geo(dj, sb_local);
+    const int nl         = job.num_lists;
     const uint32_t vmask = valid_mask(job);
-    STAMP(0);
-
-    if (tid < SVTME_A_N)
-        st.a[tid] = dj.ares[(size_t)sb_local * SVTME_A_N + tid];
-    if (tid == 0)
-        copy_planes<3>(dj, st.pl, st.dist);
-    if (tid < 8) { // init_me_hme_data (motion_estimation.c:3010-3070)
-        st.do_ref[tid] = 1;
-        st.zz[tid]     = U32MAX;
+    if (lane < SVTME_A_N)
+        d.a[lane] = dj.ares[(size_t)sb_local * SVTME_A_N + lane];
+    if (lane < 8) { // init_me_hme_data (motion_estimation.c:3010-3070)
+        d.do_ref[lane] = 1;
+        d.zz[lane]     = U32MAX;
         for (int k = 0; k < 2; k++) {
-            st.ph[tid][k].valid     = 0;
-            st.ph[tid][k].performed = 0;
-            st.ph[tid][k].sad       = 0;
-            st.ph[tid][k].col = st.ph[tid][k].row = 0;
+            d.ph[lane][k].valid     = 0;
+            d.ph[lane][k].performed = 0;
+            d.ph[lane][k].sad       = 0;
+            d.ph[lane][k].col = d.ph[lane][k].row = 0;
         }
     }
-    if (tid < 96) {
-        (&st.lx[0][0][0])[tid]   = 0;
-        (&st.ly[0][0][0])[tid]   = 0;
-        (&st.lsad[0][0][0])[tid] = 0;
+    if (lane < 32) {
+        (&d.lx[0][0])[lane]   = 0;
+        (&d.ly[0][0])[lane]   = 0;
+        (&d.lsad[0][0])[lane] = 0;
     }
-    if (c.enable_hme_flag && c.enable_hme_level1_flag && tid < 64) { // quarter source block 32 x 32
-        const DevPlane &Q = dj.cur.lv[1];
-        const int r = tid >> 1, j = tid & 1;
-        ((uint4 *)st.src)[tid] = *(const uint4 *)(Q.base + (ptrdiff_t)((oy >> 1) + r) * Q.stride + (ox >> 1) + 16 * j);
-    }
-    __syncthreads();
-    STAMP(1);
+    wave_lds_fence();
 
-    if (w0) {
-        // ---- init_zz_sad decisions (motion_estimation.c:2382-2437)
-        if (c.me_early_exit_th || c.me_safe_limit_zz_th) {
-            const int s = lane;
-            uint32_t zz = U32MAX;
-            const bool have = slot_valid(vmask, s) && tl_or_l0(job, s >> 2);
-            if (have) {
-                zz       = st.a[SVTME_A_ZZ + s].sad << 1;
-                zz       = (zz * 64 * 64) / (bw * bh);
-                st.zz[s] = zz;
-            }
-            const uint32_t best = wave_min_u32(zz);
-            if (have && (s & 3) > 0 && job.temporal_layer_index > 0 && best < c.zz_sad_th &&
-                (uint32_t)((zz - best) * 100u) > (uint32_t)(c.zz_sad_pct * best))
-                st.do_ref[s] = 0;
-            if (c.me_safe_limit_zz_th) {
-                const bool safe = job.hierarchical_levels > 0 && nl == 2 &&
-                    job.temporal_layer_index >= job.hierarchical_levels && job.similar_brightness_refs &&
-                    st.zz[0] < c.me_safe_limit_zz_th && st.zz[4] < c.me_safe_limit_zz_th;
-                if (safe && slot_valid(vmask, lane) && (lane & 3) > 0)
-                    st.do_ref[lane] = 0;
-            }
+    // ---- init_zz_sad decisions (motion_estimation.c:2382-2437)
+    if (c.me_early_exit_th || c.me_safe_limit_zz_th) {
+        const int s = lane;
+        uint32_t zz = U32MAX;
+        const bool have = slot_valid(vmask, s) && tl_or_l0(job, s >> 2);
+        if (have) {
+            zz      = d.a[SVTME_A_ZZ + s].sad << 1;
+            zz      = (zz * 64 * 64) / (G.bw * G.bh);
+            d.zz[s] = zz;
         }
-        // ---- pre-HME decisions (motion_estimation.c:1693-1796), list 0 then list 1
-        if (c.prehme_enable) {
-            for (int l = 0; l < nl; l++) {
-                const int r = lane >> 1, sr = lane & 1, s = l * 4 + r;
-                if (lane < 8 && slot_valid(vmask, s) && tl_or_l0(job, l)) {
-                    PreHme &d = st.ph[s][sr];
-                    bool done = false;
-                    if (c.me_early_exit_th && st.zz[s] < c.me_early_exit_th) { // check_prehme_early_exit
-                        d.col = d.row = 0;
-                        d.sad   = 0;
-                        d.valid = 1;
+        const uint32_t best = wave_min_u32(zz);
+        if (have && (s & 3) > 0 && job.temporal_layer_index > 0 && best < c.zz_sad_th &&
+            (uint32_t)((zz - best) * 100u) > (uint32_t)(c.zz_sad_pct * best))
+            d.do_ref[s] = 0;
+        wave_lds_fence();
+        if (c.me_safe_limit_zz_th) {
+            const bool safe = job.hierarchical_levels > 0 && nl == 2 &&
+                job.temporal_layer_index >= job.hierarchical_levels && job.similar_brightness_refs &&
+                d.zz[0] < c.me_safe_limit_zz_th && d.zz[4] < c.me_safe_limit_zz_th;
+            if (safe && slot_valid(vmask, lane) && (lane & 3) > 0)
+                d.do_ref[lane] = 0;
+        }
+        wave_lds_fence();
+    }
+    // ---- pre-HME decisions (motion_estimation.c:1693-1796), list 0 then list 1
+    if (c.prehme_enable) {
+        for (int l = 0; l < nl; l++) {
+            const int r = lane >> 1, sr = lane & 1, s = l * 4 + r;
+            if (lane < 8 && slot_valid(vmask, s) && tl_or_l0(job, l)) {
+                PreHme &p = d.ph[s][sr];
+                bool done = false;
+                if (c.me_early_exit_th && d.zz[s] < c.me_early_exit_th) { // check_prehme_early_exit
+                    p.col = p.row = 0;
+                    p.sad   = 0;
+                    p.valid = 1;
+                    done    = true;
+                }
+                if (!done && c.prehme_l1_early_exit && l == 1) {
+                    const PreHme &z = d.ph[r][sr];
+                    if (z.valid && ((z.sad < (32 * 32)) || ((absi(z.col) < 16) && (absi(z.row) < 16)))) {
+                        p.col   = (int16_t)-z.col;
+                        p.row   = (int16_t)-z.row;
+                        p.sad   = z.sad;
+                        p.valid = 1;
                         done    = true;
                     }
-                    if (!done && c.prehme_l1_early_exit && l == 1) {
-                        const PreHme &z = st.ph[r][sr];
-                        if (z.valid && ((z.sad < (32 * 32)) || ((absi(z.col) < 16) && (absi(z.row) < 16)))) {
-                            d.col   = (int16_t)-z.col;
-                            d.row   = (int16_t)-z.row;
-                            d.sad   = z.sad;
-                            d.valid = 1;
-                            done    = true;
-                        }
-                    }
-                    if (!done && !st.do_ref[s]) {
-                        d.col = d.row = 0;
-                        d.sad = U32MAX;
-                        done  = true;
-                    }
-                    if (!done) { // searched in stage A
-                        const ARes &a = st.a[SVTME_A_PH + s * 2 + sr];
-                        d.sad         = a.sad;
-                        d.col         = a.x;
-                        d.row         = a.y;
-                        d.valid       = 1;
-                        d.performed   = 1;
-                    }
                 }
-            }
-            uint32_t m  = U32MAX;
-            const int s = lane;
-            if (slot_valid(vmask, s)) {
-                if (tl_or_l0(job, s >> 2)) {
-                    m = (uint32_t)min_u64(st.ph[s][0].sad, st.ph[s][1].sad);
-                } else { // list 1 at the base layer mirrors list 0
-                    for (int k = 0; k < 2; k++) {
-                        st.ph[s][k].col = (int16_t)-st.ph[s & 3][k].col;
-                        st.ph[s][k].row = (int16_t)-st.ph[s & 3][k].row;
-                        st.ph[s][k].sad = st.ph[s & 3][k].sad;
-                    }
+                if (!done && !d.do_ref[s]) {
+                    p.col = p.row = 0;
+                    p.sad = U32MAX;
+                    done  = true;
                 }
-            }
-            const uint32_t best = wave_min_u32(m);
-            if (job.temporal_layer_index > 0 && best < c.phme_sad_th && slot_valid(vmask, s) && (s & 3) > 0 &&
-                st.do_ref[s] && (uint32_t)((m - best) * 100u) > (uint32_t)(c.phme_sad_pct * best))
-                st.do_ref[s] = 0;
-        }
-        // ---- HME level 0 decisions (motion_estimation.c:1906-2036)
-        if (c.enable_hme_flag && c.enable_hme_level0_flag) {
-            const int s = lane >> 2, q = lane & 3;
-            bool searched = false;
-            if (lane < 32 && slot_valid(vmask, s)) {
-                int16_t &X = st.lx[0][s][q], &Y = st.ly[0][s][q];
-                uint64_t &SD = st.lsad[0][s][q];
-                bool done = false;
-                if (c.me_early_exit_th && st.zz[s] < (c.me_early_exit_th >> 2)) {
-                    X = Y = 0;
-                    SD   = 0;
-                    done = true;
+                if (!done) { // searched in stage A
+                    const ARes &a = d.a[SVTME_A_PH + s * 2 + sr];
+                    p.sad         = a.sad;
+                    p.col         = a.x;
+                    p.row         = a.y;
+                    p.valid       = 1;
+                    p.performed   = 1;
                 }
-                if (!done && c.prev_me_stage_based_exit_th) {
-                    const int k = st.ph[s][0].sad <= st.ph[s][1].sad ? 0 : 1;
-                    if (st.ph[s][k].performed && st.ph[s][k].sad < (c.prev_me_stage_based_exit_th >> 4)) {
-                        X    = st.ph[s][k].col;
-                        Y    = st.ph[s][k].row;
-                        SD   = st.ph[s][k].sad;
-                        done = true;
-                    }
-                }
-                if (!done && !st.do_ref[s]) {
-                    X = Y = 0;
-                    SD   = U32MAX;
-                    done = true;
-                }
-                if (!done && tl_or_l0(job, s >> 2)) {
-                    const ARes &a = st.a[SVTME_A_L0 + s * 4 + q];
-                    X             = a.x;
-                    Y             = a.y;
-                    SD            = a.sad;
-                    searched      = true;
-                }
-            }
-            // pre-HME replaces the worst quadrant of each searched slot (:2005-2032)
-            const unsigned long long sm = __ballot(searched);
-            if (c.prehme_enable && lane < 8 && ((sm >> (4 * lane)) & 0xF)) {
-                const int s2 = lane;
-                uint64_t *S  = st.lsad[0][s2];
-                int wq       = 0; // get_worst_quadrant: strict > in (0,0),(1,0),(0,1),(1,1) order
-                uint64_t mx  = 0;
-                if (S[0] > mx) { mx = S[0]; wq = 0; }
-                if (S[2] > mx) { mx = S[2]; wq = 2; }
-                if (S[1] > mx) { mx = S[1]; wq = 1; }
-                if (S[3] > mx) { wq = 3; }
-                const int k = st.ph[s2][0].sad <= st.ph[s2][1].sad ? 0 : 1;
-                if (st.ph[s2][k].sad < S[wq]) {
-                    S[wq]            = st.ph[s2][k].sad;
-                    st.lx[0][s2][wq] = st.ph[s2][k].col;
-                    st.ly[0][s2][wq] = st.ph[s2][k].row;
-                }
-            }
-        }
-    }
-    __syncthreads();
-    STAMP(2);
-
-    // ---- HME level 1 / 2 (motion_estimation.c:2041-2177)
-    for (int level = 1; level <= 2; level++) {
-        if (!c.enable_hme_flag || (level == 1 && !c.enable_hme_level1_flag) ||
-            (level == 2 && !c.enable_hme_level2_flag))
-            continue;
-        if (level == 2) { // full-resolution source block
-            __syncthreads();
-            const DevPlane &F = dj.cur.lv[0];
-            const int r = tid >> 2, j = tid & 3;
-            ((uint4 *)st.src)[tid] = *(const uint4 *)(F.base + (ptrdiff_t)(oy + r) * F.stride + ox + 16 * j);
-        }
-        if (w0) {
-            const int s = lane >> 2, q = lane & 3;
-            bool mk = false;
-            BTask bt;
-            if (lane < 32 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2)) {
-                int16_t &X = st.lx[level][s][q], &Y = st.ly[level][s][q];
-                uint64_t &SD = st.lsad[level][s][q];
-                bool done = false;
-                if (level == 1) {
-                    if (c.me_early_exit_th && st.zz[s] < (c.me_early_exit_th >> 2)) {
-                        X = Y = 0;
-                        SD   = 0;
-                        done = true;
-                    }
-                    if (!done && !st.do_ref[s]) {
-                        X = Y = 0;
-                        SD   = U32MAX;
-                        done = true;
-                    }
-                    if (!done && c.prev_me_stage_based_exit_th &&
-                        st.lsad[0][s][q] < (c.prev_me_stage_based_exit_th >> 5)) {
-                        X    = st.lx[0][s][q];
-                        Y    = st.ly[0][s][q];
-                        SD   = st.lsad[0][s][q];
-                        done = true;
-                    }
-                } else if (c.prev_me_stage_based_exit_th && st.lsad[1][s][q] < (c.prev_me_stage_based_exit_th >> 2)) {
-                    X    = st.lx[1][s][q];
-                    Y    = st.ly[1][s][q];
-                    SD   = st.lsad[1][s][q];
-                    done = true;
-                }
-                if (!done) {
-                    const DevPlane &P   = st.pl[s][level == 1 ? 1 : 0];
-                    const int16_t cx    = level == 1 ? i16(st.lx[0][s][q] >> 1) : st.lx[1][s][q];
-                    const int16_t cy    = level == 1 ? i16(st.ly[0][s][q] >> 1) : st.ly[1][s][q];
-                    const int16_t qx    = level == 1 ? i16(((int16_t)ox) >> 1) : (int16_t)ox;
-                    const int16_t qy    = level == 1 ? i16(((int16_t)oy) >> 1) : (int16_t)oy;
-                    const svtme_area sa = level == 1 ? c.hme_l1_sa : c.hme_l2_sa;
-                    int16_t xo, yo, sw, sh2;
-                    hme_refine_rect(level, P, qx, qy, (int16_t)sa.width, (int16_t)sa.height, cx, cy, &xo, &yo, &sw,
-                                    &sh2);
-                    bt = BTask{i16(qx + xo), i16(qy + yo), sw, sh2, xo, yo, (uint8_t)s, (uint8_t)q, {0, 0}};
-                    mk = true;
-                }
-            }
-            int tot;
-            const int k = wave_compact(mk, &tot);
-            if (mk)
-                st.bt[k] = bt;
-            if (lane == 0)
-                st.nbt = tot;
-        }
-        __syncthreads();
-        STAMP(3);
-        {
-            const int bwl = level == 1 ? (int)(bw >> 1) : (int)bw;
-            const int bhl = level == 1 ? (int)(bh >> 1) : (int)bh;
-            const int sst = (level == 1 ? 32 : 64) * (hsub ? 2 : 1);
-            // every task of this wave staged together (one memory round trip), then searched
-            const int nbt = st.nbt;
-            auto geo = [&](int t, int room) {
-                const BTask &T    = st.bt[t];
-                const int s       = UNI(T.slot);
-                const DevPlane &P = st.pl[s][level == 1 ? 1 : 0];
-                return sad_geo(P.base, P.stride, UNI(T.wx), UNI(T.wy), UNI(T.sa_w), UNI(T.sa_h), bwl,
-                               hsub ? bhl >> 1 : bhl, hsub, false, room);
-            };
-            int off = 0;
-            for (int t0 = wid; t0 < nbt; t0 += 4 * STAGE_B_GROUP) { // this wave's tasks, a group at a time
-                Win w[STAGE_B_GROUP];
-                uint32_t mask = 0;
-#pragma unroll
-                for (int k = 0; k < STAGE_B_GROUP; k++) {
-                    const int t = t0 + 4 * k;
-                    if (t < nbt) {
-                        const SadGeo g = geo(t, STAGE_B_BUF_DW - off);
-                        if (sad_staged(g)) {
-                            w[k] = sad_win(g, st.wbuf[wid] + off);
-                            mask |= 1u << k;
-                            off += g.wrows * g.pitch;
-                        }
-                    }
-                }
-                stage_windows<STAGE_B_GROUP>(w, mask);
             }
             wave_lds_fence();
-            STAMP(4);
-            off = 0;
-            for (int t = wid; t < nbt; t += 4) {
-                const SadGeo g = geo(t, STAGE_B_BUF_DW - off);
-                const unsigned long long k = sad_compute<RW_8 | RW_16 | RW_4 | RW_2>(g, st.wbuf[wid] + off, st.src, sst);
-                if (g.staged && g.nitems)
-                    off += g.wrows * g.pitch;
-                if (lane == 0)
-                    st.bkey[t] = k;
-            }
-            STAMP(5);
         }
-        __syncthreads();
-        if (w0 && lane < st.nbt) {
-            const BTask &T = st.bt[lane];
-            const int s = T.slot, q = T.q;
-            uint32_t best;
-            int x, y;
-            key_result(st.bkey[lane], &best, &x, &y);
-            const int mul          = level == 1 ? 2 : 1;
-            st.lsad[level][s][q]   = hsub ? (uint64_t)best * 2 : best;
-            st.lx[level][s][q]     = i16((x + T.xo) * mul);
-            st.ly[level][s][q]     = i16((y + T.yo) * mul);
-        }
-        __syncthreads();
-        STAMP(6);
-    }
-
-    // ---- set_final_seach_centre_sb (motion_estimation.c:2182-2380) + hme_prune_ref_and_adjust_sr (:2477-2518)
-    if (w0) {
-        const int s      = lane;
-        const bool valid = slot_valid(vmask, s);
-        int lvl          = -1;
-        if (c.enable_hme_level0_flag && !c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
-            lvl = 0;
-        if (c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
-            lvl = 1;
-        if (c.enable_hme_level2_flag)
-            lvl = 2;
-        const bool hme_slot = valid && tl_or_l0(job, s >> 2) && c.enable_hme_flag;
-        int16_t hx = 0, hy = 0;
-        uint64_t hs    = 0;
-        const bool own = hme_slot && lvl >= 0;
-        if (own) {
-            const int16_t *X = st.lx[lvl][s], *Y = st.ly[lvl][s];
-            const uint64_t *S = st.lsad[lvl][s];
-            hx = X[0], hy = Y[0], hs = S[0];
-            // scan order (w, h): (1,0), (0,1), (1,1) = q 2, 1, 3
-            if (S[2] < hs) { hx = X[2]; hy = Y[2]; hs = S[2]; }
-            if (S[1] < hs) { hx = X[1]; hy = Y[1]; hs = S[1]; }
-            if (S[3] < hs) { hx = X[3]; hy = Y[3]; hs = S[3]; }
-        }
-        // the reference carries function-scope values across slots
-        int16_t cx = 0, cy = 0, scx = 0, scy = 0;
-        uint64_t cs = 0;
-        int16_t my_scx = 0, my_scy = 0;
-        uint64_t my_hs = 0;
-        for (int k = 0; k < 8; k++) {
-            if (!((vmask >> k) & 1u))
-                continue;
-            const bool ok = __shfl((int)own, k, 64) != 0;
-            const bool hk = __shfl((int)hme_slot, k, 64) != 0;
-            const bool tk = tl_or_l0(job, k >> 2);
-            const int16_t kx = (int16_t)__shfl((int)hx, k, 64), ky = (int16_t)__shfl((int)hy, k, 64);
-            const uint64_t ks = __shfl(hs, k, 64);
-            if (ok) {
-                cx = kx, cy = ky, cs = ks;
-            }
-            if (tk) {
-                if (hk) {
-                    scx = cx;
-                    scy = cy;
+        uint32_t m  = U32MAX;
+        const int s = lane;
+        if (slot_valid(vmask, s)) {
+            if (tl_or_l0(job, s >> 2)) {
+                m = (uint32_t)min_u64(d.ph[s][0].sad, d.ph[s][1].sad);
+            } else { // list 1 at the base layer mirrors list 0
+                for (int k = 0; k < 2; k++) {
+                    d.ph[s][k].col = (int16_t)-d.ph[s & 3][k].col;
+                    d.ph[s][k].row = (int16_t)-d.ph[s & 3][k].row;
+                    d.ph[s][k].sad = d.ph[s & 3][k].sad;
                 }
-            } else {
-                scx = 0;
-                scy = 0;
-            }
-            if (lane == k) {
-                my_scx = scx, my_scy = scy, my_hs = cs;
             }
         }
-        uint64_t hsad = U32MAX; // SearchResults init (hme_sad = MAX_U32)
-        if (valid)
-            hsad = my_hs;
-        uint32_t rdiv = 1;
-        uint8_t dref  = s < 8 ? st.do_ref[s] : 0;
-        if (c.enable_hme_flag) { // prune_ref = enable_hme_flag && me_type != ME_MCTF
-            const uint16_t th = c.prune_ref_if_hme_sad_dev_bigger_than_th;
-            if (c.enable_me_hme_ref_pruning && th != (uint16_t)~0) {
-                const uint64_t best = wave_min_u64(s < 8 ? hsad : ~0ull);
-                if (s < 8 && (s & 3) >= 1 && (hsad - best) * 100 > (th * best))
-                    dref = 0;
+        const uint32_t best = wave_min_u32(m);
+        if (job.temporal_layer_index > 0 && best < c.phme_sad_th && slot_valid(vmask, s) && (s & 3) > 0 &&
+            d.do_ref[s] && (uint32_t)((m - best) * 100u) > (uint32_t)(c.phme_sad_pct * best))
+            d.do_ref[s] = 0;
+        wave_lds_fence();
+    }
+    // ---- HME level 0 decisions (motion_estimation.c:1906-2036)
+    if (c.enable_hme_flag && c.enable_hme_level0_flag) {
+        const int s = lane >> 2, q = lane & 3;
+        bool searched = false;
+        if (lane < 32 && slot_valid(vmask, s)) {
+            int16_t &X = d.lx[s][q], &Y = d.ly[s][q];
+            uint64_t &SD = d.lsad[s][q];
+            bool done = false;
+            if (c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2)) {
+                X = Y = 0;
+                SD   = 0;
+                done = true;
             }
-            if (c.enable_me_sr_adjustment && s < 8) {
-                if (absi(my_scx) <= c.reduce_me_sr_based_on_mv_length_th &&
-                    absi(my_scy) <= c.reduce_me_sr_based_on_mv_length_th && hsad < c.stationary_hme_sad_abs_th)
-                    rdiv = c.stationary_me_sr_divisor;
-                else if (hsad < c.reduce_me_sr_based_on_hme_sad_abs_th)
-                    rdiv = c.me_sr_divisor_for_low_hme_sad;
+            if (!done && c.prev_me_stage_based_exit_th) {
+                const int k = d.ph[s][0].sad <= d.ph[s][1].sad ? 0 : 1;
+                if (d.ph[s][k].performed && d.ph[s][k].sad < (c.prev_me_stage_based_exit_th >> 4)) {
+                    X    = d.ph[s][k].col;
+                    Y    = d.ph[s][k].row;
+                    SD   = d.ph[s][k].sad;
+                    done = true;
+                }
+            }
+            if (!done && !d.do_ref[s]) {
+                X = Y = 0;
+                SD   = U32MAX;
+                done = true;
+            }
+            if (!done && tl_or_l0(job, s >> 2)) {
+                const ARes &a = d.a[SVTME_A_L0 + s * 4 + q];
+                X             = a.x;
+                Y             = a.y;
+                SD            = a.sad;
+                searched      = true;
             }
         }
-        if (s < 8) {
-            BState *b        = dj.bst + sb_local;
-            b->hme_sad[s]    = hsad;
-            b->zz[s]         = st.zz[s];
-            b->reduce_div[s] = rdiv;
-            b->sc_x[s]       = valid ? my_scx : 0;
-            b->sc_y[s]       = valid ? my_scy : 0;
-            b->do_ref[s]     = dref;
+        wave_lds_fence();
+        // pre-HME replaces the worst quadrant of each searched slot (:2005-2032)
+        const unsigned long long sm = __ballot(searched);
+        if (c.prehme_enable && lane < 8 && ((sm >> (4 * lane)) & 0xF)) {
+            const int s2 = lane;
+            uint64_t *S  = d.lsad[s2];
+            int wq       = 0; // get_worst_quadrant: strict > in (0,0),(1,0),(0,1),(1,1) order
+            uint64_t mx  = 0;
+            if (S[0] > mx) { mx = S[0]; wq = 0; }
+            if (S[2] > mx) { mx = S[2]; wq = 2; }
+            if (S[1] > mx) { mx = S[1]; wq = 1; }
+            if (S[3] > mx) { wq = 3; }
+            const int k = d.ph[s2][0].sad <= d.ph[s2][1].sad ? 0 : 1;
+            if (d.ph[s2][k].sad < S[wq]) {
+                S[wq]         = d.ph[s2][k].sad;
+                d.lx[s2][wq] = d.ph[s2][k].col;
+                d.ly[s2][wq] = d.ph[s2][k].row;
+            }
+        }
+        wave_lds_fence();
+    }
+    BState *b = dj.bst + sb_local;
+    if (lane < 32) {
+        (&b->lx[0][0])[lane]   = (&d.lx[0][0])[lane];
+        (&b->ly[0][0])[lane]   = (&d.ly[0][0])[lane];
+        (&b->lsad[0][0])[lane] = (&d.lsad[0][0])[lane];
+    }
+    if (lane < 8) {
+        b->zz[lane]     = d.zz[lane];
+        b->do_ref[lane] = d.do_ref[lane];
+    }
+}
+
+// ----------------------------------------------------------------------------
+// Stage B: HME level 1 (and 2) refinement of one (SB, slot, quadrant) per
+// wavefront (hme_level1_b64 / hme_level2_b64, motion_estimation.c:2041-2177)
+// ----------------------------------------------------------------------------
+// one refinement search (hme_level_1 / hme_level_2, :923-1113); the window is
+// staged in LDS when it fits, the result is scaled to full-pel units
+__device__ __forceinline__ void hme_refine(int level, const DevPlane &P, int16_t qx, int16_t qy, const svtme_area &sa,
+                                           int16_t cx, int16_t cy, int bwl, int bhl, bool hsub, const uint8_t *src,
+                                           int sst, uint32_t *buf, int16_t *X, int16_t *Y, uint64_t *SD) {
+    int16_t xo, yo, sw, sh;
+    hme_refine_rect(level, P, qx, qy, (int16_t)sa.width, (int16_t)sa.height, cx, cy, &xo, &yo, &sw, &sh);
+    const SadGeo g = sad_geo(P.base, P.stride, qx + xo, qy + yo, sw, sh, bwl, hsub ? bhl >> 1 : bhl, hsub, false,
+                             STAGE_B_BUF_DW);
+    if (sad_staged(g)) {
+        const Win w[1] = {sad_win(g, buf)};
+        stage_windows<1>(w, 1u);
+    }
+    wave_lds_fence();
+    const unsigned long long k = sad_compute<RW_8 | RW_16 | RW_4 | RW_2>(g, buf, src, sst);
+    uint32_t best;
+    int x, y;
+    key_result(k, &best, &x, &y);
+    const int mul = level == 1 ? 2 : 1;
+    *SD           = hsub ? (uint64_t)best * 2 : best;
+    *X            = i16((x + xo) * mul);
+    *Y            = i16((y + yo) * mul);
+}
+
+template <bool L2>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L2 ? 4 : 6, 8))) k_stage_b(const DevJob dj) {
+    __shared__ __attribute__((aligned(16))) uint8_t srcb[4][L2 ? 64 * 64 : 32 * 32];
+    __shared__ uint32_t wbuf[4][STAGE_B_BUF_DW];
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t total = job.sb_count * dj.tb_count;
+    const uint32_t gw    = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (gw >= total)
+        return;
+    const uint32_t sb_local = UNI(gw / dj.tb_count);
+    const int e             = UNI(dj.tb_list[gw - sb_local * dj.tb_count]);
+    const int s = e >> 2, q = e & 3, l = s >> 2, r = s & 3;
+    const SbGeo G   = sb_geo(dj, sb_local);
+    const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH;
+    uint8_t *src    = srcb[wid];
+    uint32_t *buf   = wbuf[wid];
+    BState *b       = dj.bst + sb_local;
+
+    int16_t X = 0, Y = 0; // level-1 result (0 when level 1 is off: init_me_hme_data)
+    uint64_t SD = 0;
+    if (c.enable_hme_level1_flag) {
+        // quarter-resolution source block (32 x 32), issued before the decided state is read
+        const DevPlane &Qc = dj.cur.lv[1];
+        const uint4 sv     = *(const uint4 *)(Qc.base + (ptrdiff_t)((G.oy >> 1) + (lane >> 1)) * Qc.stride +
+                                          (G.ox >> 1) + 16 * (lane & 1));
+        const uint32_t zz    = b->zz[s];
+        const uint8_t dref   = b->do_ref[s];
+        const int16_t X0     = b->lx[s][q], Y0 = b->ly[s][q];
+        const uint64_t S0    = b->lsad[s][q];
+        ((uint4 *)src)[lane] = sv;
+        bool done            = false;
+        if (c.me_early_exit_th && zz < (c.me_early_exit_th >> 2)) {
+            X = Y = 0;
+            SD   = 0;
+            done = true;
+        }
+        if (!done && !dref) {
+            X = Y = 0;
+            SD   = U32MAX;
+            done = true;
+        }
+        if (!done && c.prev_me_stage_based_exit_th && S0 < (c.prev_me_stage_based_exit_th >> 5)) {
+            X = X0, Y = Y0, SD = S0;
+            done = true;
+        }
+        if (!done)
+            hme_refine(1, dj.ref[l][r].lv[1], i16(((int16_t)G.ox) >> 1), i16(((int16_t)G.oy) >> 1), c.hme_l1_sa,
+                       i16(X0 >> 1), i16(Y0 >> 1), (int)(G.bw >> 1), (int)(G.bh >> 1), hsub, src, hsub ? 64 : 32,
+                       buf, &X, &Y, &SD);
+    }
+    if (L2 && c.enable_hme_level2_flag) {
+        if (!(c.prev_me_stage_based_exit_th && SD < (c.prev_me_stage_based_exit_th >> 2))) {
+            const DevPlane &F = dj.cur.lv[0]; // full-resolution source block (64 x 64)
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int t = u * 64 + lane, rr = t >> 2, j = t & 3;
+                ((uint4 *)src)[t] = *(const uint4 *)(F.base + (ptrdiff_t)(G.oy + rr) * F.stride + G.ox + 16 * j);
+            }
+            hme_refine(2, dj.ref[l][r].lv[0], (int16_t)G.ox, (int16_t)G.oy, c.hme_l2_sa, X, Y, (int)G.bw, (int)G.bh,
+                       hsub, src, hsub ? 128 : 64, buf, &X, &Y, &SD);
         }
     }
-    STAMP(7);
+    if (lane == 0) {
+        b->hx[s][q]   = X;
+        b->hy[s][q]   = Y;
+        b->hsad[s][q] = SD;
+    }
+}
+
+// set_final_seach_centre_sb (motion_estimation.c:2182-2380) and
+// hme_prune_ref_and_adjust_sr (:2477-2518) of one SB from the state stages D
+// and B left, by one whole wavefront; lane s < 8 returns slot s
+struct SlotCentre {
+    uint64_t hme_sad;
+    uint32_t zz, reduce_div;
+    int16_t sc_x, sc_y;
+    uint8_t do_ref;
+};
+
+__device__ SlotCentre final_centre(const DevJob &dj, uint32_t sb_local, uint32_t vmask) {
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const int s             = threadIdx.x & 63;
+    const BState *b         = dj.bst + sb_local;
+    const bool valid        = slot_valid(vmask, s);
+    int lvl                 = -1;
+    if (c.enable_hme_level0_flag && !c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
+        lvl = 0;
+    if (c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
+        lvl = 1;
+    if (c.enable_hme_level2_flag)
+        lvl = 2;
+    const bool hme_slot = valid && tl_or_l0(job, s >> 2) && c.enable_hme_flag;
+    int16_t hx = 0, hy = 0;
+    uint64_t hs    = 0;
+    const bool own = hme_slot && lvl >= 0;
+    if (own) {
+        const int16_t *X  = lvl ? b->hx[s] : b->lx[s];
+        const int16_t *Y  = lvl ? b->hy[s] : b->ly[s];
+        const uint64_t *S = lvl ? b->hsad[s] : b->lsad[s];
+        hx = X[0], hy = Y[0], hs = S[0];
+        // scan order (w, h): (1,0), (0,1), (1,1) = q 2, 1, 3
+        if (S[2] < hs) { hx = X[2]; hy = Y[2]; hs = S[2]; }
+        if (S[1] < hs) { hx = X[1]; hy = Y[1]; hs = S[1]; }
+        if (S[3] < hs) { hx = X[3]; hy = Y[3]; hs = S[3]; }
+    }
+    // the reference carries function-scope values across slots
+    int16_t cx = 0, cy = 0, scx = 0, scy = 0;
+    uint64_t cs = 0;
+    int16_t my_scx = 0, my_scy = 0;
+    uint64_t my_hs = 0;
+    for (int k = 0; k < 8; k++) {
+        if (!((vmask >> k) & 1u))
+            continue;
+        const bool ok = __shfl((int)own, k, 64) != 0;
+        const bool hk = __shfl((int)hme_slot, k, 64) != 0;
+        const bool tk = tl_or_l0(job, k >> 2);
+        const int16_t kx = (int16_t)__shfl((int)hx, k, 64), ky = (int16_t)__shfl((int)hy, k, 64);
+        const uint64_t ks = __shfl(hs, k, 64);
+        if (ok) {
+            cx = kx, cy = ky, cs = ks;
+        }
+        if (tk) {
+            if (hk) {
+                scx = cx;
+                scy = cy;
+            }
+        } else {
+            scx = 0;
+            scy = 0;
+        }
+        if (s == k) {
+            my_scx = scx, my_scy = scy, my_hs = cs;
+        }
+    }
+    uint64_t hsad = U32MAX; // SearchResults init (hme_sad = MAX_U32)
+    if (valid)
+        hsad = my_hs;
+    uint32_t rdiv = 1;
+    uint8_t dref  = s < 8 ? b->do_ref[s] : 0;
+    if (c.enable_hme_flag) { // prune_ref = enable_hme_flag && me_type != ME_MCTF
+        const uint16_t th = c.prune_ref_if_hme_sad_dev_bigger_than_th;
+        if (c.enable_me_hme_ref_pruning && th != (uint16_t)~0) {
+            const uint64_t best = wave_min_u64(s < 8 ? hsad : ~0ull);
+            if (s < 8 && (s & 3) >= 1 && (hsad - best) * 100 > (th * best))
+                dref = 0;
+        }
+        if (c.enable_me_sr_adjustment && s < 8) {
+            if (absi(my_scx) <= c.reduce_me_sr_based_on_mv_length_th &&
+                absi(my_scy) <= c.reduce_me_sr_based_on_mv_length_th && hsad < c.stationary_hme_sad_abs_th)
+                rdiv = c.stationary_me_sr_divisor;
+            else if (hsad < c.reduce_me_sr_based_on_hme_sad_abs_th)
+                rdiv = c.me_sr_divisor_for_low_hme_sad;
+        }
+    }
+    SlotCentre o;
+    o.hme_sad    = hsad;
+    o.zz         = s < 8 ? b->zz[s] : U32MAX;
+    o.reduce_div = rdiv;
+    o.sc_x       = valid ? my_scx : 0;
+    o.sc_y       = valid ? my_scy : 0;
+    o.do_ref     = dref;
+    return o;
 }
 
 // ----------------------------------------------------------------------------
@@ -1467,15 +1438,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             st.refpic[s] = job.ref_picture_number[s >> 2][s & 3];
         }
     }
-    if (tid < 8) {
-        const BState *b    = dj.bst + sb_local;
-        st.hme_sad[tid]    = b->hme_sad[tid];
-        st.zz[tid]         = b->zz[tid];
-        st.reduce_div[tid] = b->reduce_div[tid];
-        st.sc_x[tid]       = b->sc_x[tid];
-        st.sc_y[tid]       = b->sc_y[tid];
-        st.do_ref[tid]     = b->do_ref[tid];
-        st.searched[tid]   = b->do_ref[tid];
+    if (w0) {
+        const SlotCentre sc = final_centre(dj, sb_local, vmask);
+        if (lane < 8) {
+            st.hme_sad[lane]    = sc.hme_sad;
+            st.zz[lane]         = sc.zz;
+            st.reduce_div[lane] = sc.reduce_div;
+            st.sc_x[lane]       = sc.sc_x;
+            st.sc_y[lane]       = sc.sc_y;
+            st.do_ref[lane]     = sc.do_ref;
+            st.searched[lane]   = sc.do_ref;
+        }
     }
     for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) (&st.best_mv[0][0])[e] = 0;
     __syncthreads();
@@ -1486,7 +1459,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int rounds = c.enable_me_sr_adjustment == 2 ? 2 : 1;
     for (int round = 0; round < rounds; round++) {
         if (w0) { // search area up to the 8x8-variance decision
-            const int s = lane, l = s >> 2, r = s & 3;
+            const int s = lane, r = s & 3;
             const bool act = slot_valid(vmask, s) && (rounds == 1 || ((s == 0) == (round == 0))) && st.do_ref[s];
             bool need = false;
             if (act) {
@@ -1753,7 +1726,25 @@ extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t
     *count = n;
 }
 
-// mid (optional): two events recorded after stage A and after stage B
+// Stage-B refinement list of a job: every (slot, quadrant) HME level 1/2
+// refines (hme_level1_b64 / hme_level2_b64 loop over valid slots with
+// temporal_layer_index > 0 || list 0). Host-side, pure.
+extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count) {
+    const svtme_controls &c = job->ctrl;
+    uint32_t n = 0;
+    if (c.enable_hme_flag && (c.enable_hme_level1_flag || c.enable_hme_level2_flag))
+        for (int s = 0; s < 8; s++) {
+            const int l = s >> 2, r = s & 3;
+            if (l >= job->num_lists || r >= job->num_refs[l])
+                continue;
+            if (!(job->temporal_layer_index > 0 || l == 0))
+                continue;
+            for (int q = 0; q < 4; q++) list[n++] = (uint8_t)((s << 2) | q);
+        }
+    *count = n;
+}
+
+// mid (optional): three events recorded after stages A, D and B
 extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid) {
     if (dj->ta_count) {
         const uint32_t waves = sb_count * dj->ta_count;
@@ -1761,9 +1752,18 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, h
     }
     if (mid)
         (void)hipEventRecord(mid[0], s);
-    hipLaunchKernelGGL(svtme::k_stage_b, dim3(sb_count), dim3(256), 0, s, *dj);
+    hipLaunchKernelGGL(svtme::k_stage_d, dim3((sb_count + 3) / 4), dim3(256), 0, s, *dj);
     if (mid)
         (void)hipEventRecord(mid[1], s);
+    if (dj->tb_count) {
+        const uint32_t waves = sb_count * dj->tb_count;
+        if (dj->job.ctrl.enable_hme_level2_flag)
+            hipLaunchKernelGGL(svtme::k_stage_b<true>, dim3((waves + 3) / 4), dim3(256), 0, s, *dj);
+        else
+            hipLaunchKernelGGL(svtme::k_stage_b<false>, dim3((waves + 3) / 4), dim3(256), 0, s, *dj);
+    }
+    if (mid)
+        (void)hipEventRecord(mid[2], s);
     if (dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH)
         hipLaunchKernelGGL(svtme::k_stage_c<false>, dim3(sb_count), dim3(256), 0, s, *dj);
     else

@@ -591,7 +591,7 @@ class GpuME:
         return float(self.lib.svtme_kernel_ms(self.ctx))
 
     def stage_ms(self, stage: int) -> float:
-        """Last job's time in stage 0 (k_stage_a), 1 (k_stage_b) or 2 (k_stage_c)."""
+        """Last job's time in stage 0 (k_stage_a), 1 (k_stage_d), 2 (k_stage_b) or 3 (k_stage_c)."""
         return float(self.lib.svtme_stage_ms(self.ctx, stage))
 
     def sync(self):
