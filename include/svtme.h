@@ -42,6 +42,9 @@ extern "C" {
 #define SVTME_MAX_SAD_VALUE (128u * 128u * 255u) /* motion_estimation.h:85 */
 #define SVTME_SUB_SAD_SEARCH 0      /* definitions.h:2071 */
 #define SVTME_FULL_SAD_SEARCH 1     /* definitions.h:2072 */
+/* svtme_job.me_type: the EbMeType values of me_context.h:44-51 */
+#define SVTME_ME_MCTF 1             /* temporal-filtering ME (temporal_filtering.c:3169) */
+#define SVTME_ME_OPEN_LOOP 3        /* pre-analysis open-loop ME (me_process.c:266) */
 #define SVTME_PAD_FULL 72           /* PA full-res padding (enc_handle.c:4057-4069) */
 #define SVTME_PAD_QUARTER 32        /* b64_size >> 1, reference_object.c:272 */
 #define SVTME_PAD_SIXTEENTH 16      /* b64_size >> 2, reference_object.c:287 */
@@ -156,7 +159,14 @@ typedef struct svtme_job {
     uint8_t input_resolution; /* EbInputResolution: 0=240p .. 6=8K (definitions.h:2079-2085) */
     uint8_t gm_enabled;       /* pcs->gm_ctrls.enabled */
     uint8_t gm_use_distance_based_active_th;
-    uint8_t pad[3];
+    /* SVTME_ME_OPEN_LOOP (0 is accepted as the same) or SVTME_ME_MCTF. MCTF jobs
+     * (one list, one reference) skip the HME/ME reference pruning, search the
+     * full-pel area unscaled by distance (motion_estimation.c:1300-1302), stop
+     * after HME when the list-0 ref-0 HME SAD is below tf_me_exit_th (:3109-3113)
+     * and build no candidate arrays (:3126) */
+    uint8_t me_type;
+    uint8_t pad;
+    uint16_t tf_me_exit_th; /* MeContext.tf_me_exit_th (me_context.h:495) */
     /* SB range [sb_begin, sb_begin + sb_count) in raster b64 order; sb_count 0 = all */
     uint32_t sb_begin;
     uint32_t sb_count;
@@ -177,7 +187,8 @@ typedef struct svtme_ref_record {
     uint32_t zz_sad;     /* zz_sad[l][r] (0xFFFFFFFF if not computed) */
     uint8_t searched;    /* do_ref when the integer search ran */
     uint8_t do_ref;      /* final do_ref */
-    uint8_t pad[6];
+    uint8_t tf_early_exit; /* MCTF only: HME-only exit taken (tf_use_pred_64x64_only_th = ~0, :3111) */
+    uint8_t pad[5];
 } svtme_ref_record; /* 704 bytes */
 
 /* Per SB candidate list + distortions (MeSbResults, me_sb_results.h:44, and the
@@ -271,6 +282,12 @@ const char *svtme_last_error(void);
  * path (enc_mode_config.c:671-808) for preset `enc_mode`, qp and resolution. */
 void svtme_derive_controls(int enc_mode, int qp, int input_resolution, int temporal_layer_index,
                            int hierarchical_levels, int frame_rate_q16, svtme_controls *ctrl);
+
+/* Fill `ctrl` as the reference does for one temporal-filtering ME job
+ * (me_type SVTME_ME_MCTF): svt_aom_sig_deriv_me_tf (enc_mode_config.c:814-854)
+ * for tf_ctrls.hme_me_level 0..4 and tf_ctrls.qp_opt, the tf HME enables
+ * (:1620-1645) and set_hme_search_params_mctf(ctx, 0) (temporal_filtering.c:2759). */
+void svtme_derive_controls_tf(int hme_me_level, int qp_opt, int qp, int input_resolution, svtme_controls *ctrl);
 
 /* ---------------------------------------------------------------------------
  * Per-kernel rtcd variants. Signatures identical to the pointers declared in

@@ -230,7 +230,8 @@ static void run_range(RefJob *rj) {
     const uint32_t R = svtme_job_ref_slots(job);
     MeContext *me = (MeContext *)calloc(1, sizeof(MeContext));
     apply_controls(me, &job->ctrl);
-    me->me_type                     = ME_OPEN_LOOP;
+    me->me_type                     = job->me_type == SVTME_ME_MCTF ? ME_MCTF : ME_OPEN_LOOP;
+    me->tf_me_exit_th               = job->tf_me_exit_th;
     me->num_of_list_to_search       = job->num_lists;
     me->num_of_ref_pic_to_search[0] = job->num_refs[0];
     me->num_of_ref_pic_to_search[1] = job->num_lists == 2 ? job->num_refs[1] : 0;
@@ -268,6 +269,7 @@ static void run_range(RefJob *rj) {
         memset(r->me_candidate_array, 0, sizeof(MeCandidate) * SVTME_PU_COUNT * SVTME_MAX_PA_ME_CAND);
         memset(r->me_mv_array, 0, sizeof(MvCandidate) * SVTME_PU_COUNT * SVTME_MAX_PA_ME_MV);
         memset(me->me_distortion, 0, sizeof(me->me_distortion));
+        me->tf_use_pred_64x64_only_th = 0;
 
         svt_aom_motion_estimation_b64(rj->pcs, b64_index, ox, oy, me, rj->input_pic);
 
@@ -284,8 +286,11 @@ static void run_range(RefJob *rj) {
                 rec->zz_sad   = me->zz_sad[l][ri];
                 rec->searched = rec->best_sad[0] != 0xFFFFFFFFu;
                 rec->do_ref   = me->search_results[l][ri].do_ref;
+                rec->tf_early_exit = me->tf_use_pred_64x64_only_th == (uint8_t)~0;
             }
-        if (rj->sbres) {
+        if (rj->sbres && me->me_type == ME_MCTF) /* no candidates / distortions (motion_estimation.c:3126) */
+            memset(rj->sbres + (b64_index - job->sb_begin), 0, sizeof(svtme_sb_result));
+        else if (rj->sbres) {
             svtme_sb_result *s = rj->sbres + (b64_index - job->sb_begin);
             memset(s, 0, sizeof(*s));
             memcpy(s->total_me_candidate_index, r->total_me_candidate_index, SVTME_PU_COUNT);
@@ -508,6 +513,34 @@ static void export_controls(const MeContext *m, svtme_controls *c) {
     c->me_early_exit_th            = m->me_early_exit_th;
     c->me_safe_limit_zz_th         = m->me_safe_limit_zz_th;
     c->prev_me_stage_based_exit_th = m->prev_me_stage_based_exit_th;
+}
+
+void svt_aom_sig_deriv_me_tf(PictureParentControlSet *pcs, MeContext *me_ctx);
+
+/* TF-ME controls as the reference sets them for one temporal-filtering ME call:
+ * the tf HME enables by tf_ctrls.hme_me_level (enc_mode_config.c:1620-1645),
+ * svt_aom_sig_deriv_me_tf (:814-854), then set_hme_search_params_mctf(ctx, 0)
+ * (temporal_filtering.c:2759-2767, static there: its level-0 copy restated). */
+void svtref_derive_controls_tf(int hme_me_level, int qp_opt, int qp, int input_resolution, svtme_controls *ctrl) {
+    SequenceControlSet *scs      = (SequenceControlSet *)calloc(1, sizeof(SequenceControlSet));
+    PictureParentControlSet *pcs = (PictureParentControlSet *)calloc(1, sizeof(PictureParentControlSet));
+    MeContext *me                = (MeContext *)calloc(1, sizeof(MeContext));
+    scs->input_resolution          = (EbInputResolution)input_resolution;
+    scs->static_config.qp          = (uint32_t)qp;
+    pcs->scs                       = scs;
+    pcs->tf_ctrls.hme_me_level     = (uint8_t)hme_me_level;
+    pcs->tf_ctrls.qp_opt           = (uint8_t)qp_opt;
+    pcs->tf_enable_hme_flag        = 1;
+    pcs->tf_enable_hme_level0_flag = 1;
+    pcs->tf_enable_hme_level1_flag = hme_me_level <= 2;
+    pcs->tf_enable_hme_level2_flag = hme_me_level == 0;
+    svt_aom_sig_deriv_me_tf(pcs, me);
+    me->hme_l0_sa.sa_min = me->hme_l0_sa_default_tf.sa_min;
+    me->hme_l0_sa.sa_max = me->hme_l0_sa_default_tf.sa_max;
+    export_controls(me, ctrl);
+    free(me);
+    free(pcs);
+    free(scs);
 }
 
 void svtref_derive_controls(int enc_mode, int qp, int input_resolution, int temporal_layer_index,

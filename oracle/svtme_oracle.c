@@ -736,7 +736,8 @@ static void ora_integer_search(OraCtx *x, uint32_t b64_ox, uint32_t b64_oy) {
                 continue;
             int16_t xc = x->sr[l][r].hme_sc_x, yc = x->sr[l][r].hme_sc_y;
             int16_t w = (int16_t)c->me_sa.sa_min.width, h = (int16_t)c->me_sa.sa_min.height;
-            dist      = ora_scaled_dist(dist); /* me_type != ME_MCTF */
+            if (x->job->me_type != SVTME_ME_MCTF) /* motion_estimation.c:1300-1302 */
+                dist = ora_scaled_dist(dist);
             w         = (int16_t)MIN((w * dist), c->me_sa.sa_max.width);
             h         = (int16_t)MIN((h * dist), c->me_sa.sa_max.height);
             if (c->mv_sa_adj_enabled && (!c->mv_sa_adj_nearest_ref_only || r == 0)) {
@@ -1091,7 +1092,8 @@ static void ora_me_b64(OraCtx *x, uint32_t b64_index, uint32_t ox, uint32_t oy, 
     const svtme_controls *c = x->c;
     x->b64_w = (job->width - ox) < 64 ? job->width - ox : 64;
     x->b64_h = (job->height - oy) < 64 ? job->height - oy : 64;
-    const int prune_ref = c->enable_hme_flag; /* && me_type != ME_MCTF */
+    const int mctf      = job->me_type == SVTME_ME_MCTF;
+    const int prune_ref = c->enable_hme_flag && !mctf; /* motion_estimation.c:3103 */
     ora_init_me_hme_data(x);
     /* hme_b64 (motion_estimation.c:2441-2475) */
     if (c->me_early_exit_th || c->me_safe_limit_zz_th)
@@ -1107,14 +1109,19 @@ static void ora_me_b64(OraCtx *x, uint32_t b64_index, uint32_t ox, uint32_t oy, 
             ora_hme_level2_b64(x, ox, oy);
     }
     ora_set_final_centre(x);
-    if (prune_ref)
-        ora_hme_prune_and_adjust_sr(x);
+    /* MCTF: HME-only exit (motion_estimation.c:3109-3113) */
+    const int tf_exit = mctf && x->sr[0][0].hme_sad < job->tf_me_exit_th;
     uint8_t searched[2][4];
-    for (int l = 0; l < 2; l++)
-        for (int r = 0; r < 4; r++) searched[l][r] = x->sr[l][r].do_ref;
-    ora_integer_search(x, ox, oy);
-    if (prune_ref && c->enable_me_hme_ref_pruning)
-        ora_me_prune_ref(x);
+    memset(searched, 0, sizeof(searched));
+    if (!tf_exit) {
+        if (prune_ref)
+            ora_hme_prune_and_adjust_sr(x);
+        for (int l = 0; l < 2; l++)
+            for (int r = 0; r < 4; r++) searched[l][r] = x->sr[l][r].do_ref;
+        ora_integer_search(x, ox, oy);
+        if (prune_ref && c->enable_me_hme_ref_pruning)
+            ora_me_prune_ref(x);
+    }
 
     int slot = 0;
     for (int l = 0; l < x->num_lists; l++)
@@ -1132,9 +1139,11 @@ static void ora_me_b64(OraCtx *x, uint32_t b64_index, uint32_t ox, uint32_t oy, 
             o->zz_sad   = x->zz_sad[l][r];
             o->searched = searched[l][r];
             o->do_ref   = x->sr[l][r].do_ref;
+            o->tf_early_exit = (uint8_t)tf_exit;
         }
-    if (sbres) {
+    if (sbres)
         memset(sbres, 0, sizeof(*sbres));
+    if (sbres && !mctf) { /* motion_estimation.c:3126-3151 */
         if (x->num_refs[0] == 1 && x->num_refs[1] == 0)
             ora_candidates_single_ref(x, sbres);
         else if (x->num_refs[0] == 1 && x->num_refs[1] == 1)

@@ -52,6 +52,9 @@ void svtref_set_simd(int simd);
  * them (enc_mode_config.c:671), for validating svtme_derive_controls. */
 void svtref_derive_controls(int enc_mode, int qp, int input_resolution, int temporal_layer_index,
                             int hierarchical_levels, int frame_rate_q16, svtme_controls *ctrl);
+/* svtref only: TF-ME controls (svt_aom_sig_deriv_me_tf, enc_mode_config.c:814) for
+ * tf_ctrls.hme_me_level / qp_opt, for validating svtme_derive_controls_tf. */
+void svtref_derive_controls_tf(int hme_me_level, int qp_opt, int qp, int input_resolution, svtme_controls *ctrl);
 
 #ifdef __cplusplus
 }

@@ -358,6 +358,11 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
         job->ctrl.reduce_hme_l0_sr_th_min && job->ctrl.reduce_hme_l0_sr_th_max)
         return fail(SVTME_ERR_BAD_PARAMETER, "reduce_hme_l0_sr_th_min/max (real-time tune, enc_mode_config.c:690-703) "
                                              "are not supported");
+    if (job->me_type != 0 && job->me_type != SVTME_ME_OPEN_LOOP && job->me_type != SVTME_ME_MCTF)
+        return fail(SVTME_ERR_BAD_PARAMETER, "me_type %u is neither SVTME_ME_OPEN_LOOP nor SVTME_ME_MCTF",
+                    job->me_type);
+    if (job->me_type == SVTME_ME_MCTF)
+        return fail(SVTME_ERR_BAD_PARAMETER, "MCTF (temporal-filtering) jobs are not run by this build's kernels");
     if (job->width > 16384 || job->height > 16384)
         return fail(SVTME_ERR_BAD_PARAMETER, "picture too large for int16 search arithmetic");
     const uint32_t total = svtme_sb_total(job->width, job->height);
@@ -765,4 +770,77 @@ extern "C" void svtme_derive_controls(int enc_mode, int qp, int res, int tl, int
     c->me_early_exit_th           = enc_mode <= 4 ? 0 : 64 * 64 * 8;
     c->me_safe_limit_zz_th        = 0; // safe_limit_nref == 2 at mrp levels 9-10 (enc_handle.c:3542-3543)
     c->prev_me_stage_based_exit_th = 0;
+}
+
+// ----------------------------------------------------------------------------
+// TF-ME (ME_MCTF) controls: the tf HME enables by tf_ctrls.hme_me_level
+// (enc_mode_config.c:1620-1645), svt_aom_sig_deriv_me_tf (:814-854) with
+// tf_set_me_hme_params_oq (:588-665), and set_hme_search_params_mctf(ctx, 0)
+// (temporal_filtering.c:2759-2767)
+// ----------------------------------------------------------------------------
+extern "C" void svtme_derive_controls_tf(int hme_me_level, int qp_opt, int qp, int res, svtme_controls *c) {
+    memset(c, 0, sizeof(*c));
+    auto sa = [](svtme_area_minmax &a, int w0, int h0, int w1, int h1) {
+        a.sa_min = {(uint16_t)w0, (uint16_t)h0};
+        a.sa_max = {(uint16_t)w1, (uint16_t)h1};
+    };
+    c->num_hme_sa_w = 2;
+    c->num_hme_sa_h = 2;
+    switch (hme_me_level) {
+    case 0:
+        sa(c->hme_l0_sa, 30, 30, 60, 60);
+        c->hme_l1_sa = {16, 16};
+        c->hme_l2_sa = {16, 16};
+        sa(c->me_sa, 60, 60, 120, 120);
+        break;
+    case 1:
+        sa(c->hme_l0_sa, 16, 16, 32, 32);
+        c->hme_l1_sa = {16, 16};
+        c->hme_l2_sa = {16, 16};
+        sa(c->me_sa, 16, 16, 32, 32);
+        break;
+    case 2:
+        if (res <= 1) { // INPUT_SIZE_360p_RANGE
+            sa(c->hme_l0_sa, 8, 8, 8, 8);
+            c->hme_l1_sa = {8, 8};
+        } else if (res <= 2) { // INPUT_SIZE_480p_RANGE
+            sa(c->hme_l0_sa, 8, 8, 16, 16);
+            c->hme_l1_sa = {8, 8};
+        } else {
+            sa(c->hme_l0_sa, 16, 16, 32, 32);
+            c->hme_l1_sa = {16, 16};
+        }
+        c->hme_l2_sa = {16, 16};
+        sa(c->me_sa, 8, 8, 8, 8);
+        break;
+    case 3:
+        sa(c->hme_l0_sa, 8, 8, 8, 8);
+        c->hme_l1_sa = {8, 8};
+        c->hme_l2_sa = {8, 8};
+        sa(c->me_sa, 8, 8, 8, 8);
+        break;
+    default: // 4
+        sa(c->hme_l0_sa, 4, 4, 4, 4);
+        c->hme_l1_sa = {8, 8};
+        c->hme_l2_sa = {8, 8};
+        sa(c->me_sa, 8, 8, 8, 8);
+        break;
+    }
+    if (qp_opt) {
+        const int qw = clip3(250, 1000, (int)((8 * qp) - 125));
+        c->me_sa.sa_min.width  = (uint16_t)std::max(8, (c->me_sa.sa_min.width * qw) / 1000);
+        c->me_sa.sa_min.height = (uint16_t)std::max(8, (c->me_sa.sa_min.height * qw) / 1000);
+        c->me_sa.sa_max.width  = (uint16_t)std::max(8, (c->me_sa.sa_max.width * qw) / 1000);
+        c->me_sa.sa_max.height = (uint16_t)std::max(8, (c->me_sa.sa_max.height * qw) / 1000);
+    }
+    c->enable_hme_flag        = 1;
+    c->enable_hme_level0_flag = 1;
+    c->enable_hme_level1_flag = hme_me_level <= 2 ? 1 : 0;
+    c->enable_hme_level2_flag = hme_me_level == 0 ? 1 : 0;
+    c->hme_search_method = c->me_search_method = hme_me_level <= 2 ? SVTME_FULL_SAD_SEARCH : SVTME_SUB_SAD_SEARCH;
+    // pre-HME, reference pruning, sr adjustment, mv-based area and 8x8 variance: level 0 (off)
+    c->prune_ref_if_hme_sad_dev_bigger_than_th = 0xFFFF;
+    c->prune_ref_if_me_sad_dev_bigger_than_th  = 0xFFFF;
+    c->me_early_exit_th            = hme_me_level <= 1 ? 0 : 64 * 64 * 4;
+    c->prev_me_stage_based_exit_th = hme_me_level <= 1 ? 0 : 64 * 64 * 4;
 }

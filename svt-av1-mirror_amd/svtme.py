@@ -24,6 +24,7 @@ PU_COUNT = 85
 MAX_SAD_VALUE = 128 * 128 * 255
 PAD_FULL, PAD_QUARTER, PAD_SIXTEENTH = 72, 32, 16
 SUB_SAD_SEARCH, FULL_SAD_SEARCH = 0, 1
+ME_MCTF, ME_OPEN_LOOP = 1, 3  # EbMeType (me_context.h:44-51)
 # EbInputResolution (definitions.h:2079-2085)
 RES_240P, RES_360P, RES_480P, RES_720P, RES_1080P, RES_4K, RES_8K = range(7)
 
@@ -148,7 +149,9 @@ class Job(C.Structure):
         ("input_resolution", C.c_uint8),
         ("gm_enabled", C.c_uint8),
         ("gm_use_distance_based_active_th", C.c_uint8),
-        ("pad", C.c_uint8 * 3),
+        ("me_type", C.c_uint8),
+        ("pad", C.c_uint8),
+        ("tf_me_exit_th", C.c_uint16),
         ("sb_begin", C.c_uint32),
         ("sb_count", C.c_uint32),
         ("ctrl", Controls),
@@ -169,7 +172,8 @@ REF_RECORD_DTYPE = np.dtype(
         ("zz_sad", "<u4"),
         ("searched", "u1"),
         ("do_ref", "u1"),
-        ("pad", "u1", (6,)),
+        ("tf_early_exit", "u1"),
+        ("pad", "u1", (5,)),
     ]
 )
 assert REF_RECORD_DTYPE.itemsize == 704
@@ -246,6 +250,7 @@ def load_ref():
         _proto_common(lib, "svtref")
         lib.svtref_set_simd.argtypes = [C.c_int]
         lib.svtref_derive_controls.argtypes = [C.c_int] * 6 + [C.POINTER(Controls)]
+        lib.svtref_derive_controls_tf.argtypes = [C.c_int] * 4 + [C.POINTER(Controls)]
         lib._svtme_protos = True
     return lib
 
@@ -311,12 +316,14 @@ def test_frames(kind: str, w: int, h: int, ts) -> dict:
 
 
 def case_job(ctrl: Controls, w: int, h: int, cur: int, l0, l1, tl: int, gm: bool = False, is_ref: bool = True,
-             e8=None, sb_begin: int = 0, sb_count: int = 0) -> Job:
-    """The job of one test case: references ordered as given, lists sized to them."""
+             e8=None, sb_begin: int = 0, sb_count: int = 0, **kw) -> Job:
+    """The job of one test case: references ordered as given, lists sized to them
+    (kw: me_type / tf_me_exit_th for temporal-filtering jobs)."""
     res = input_resolution_of(w, h)
     return make_job(w, h, ctrl, cur, l0, l1, temporal_layer_index=tl, is_ref=is_ref,
                     enable_me_8x8=(res <= RES_720P) if e8 is None else e8,
-                    ref_count_used=(max(len(l0), 1), len(l1)), gm_enabled=gm, sb_begin=sb_begin, sb_count=sb_count)
+                    ref_count_used=(max(len(l0), 1), len(l1)), gm_enabled=gm, sb_begin=sb_begin, sb_count=sb_count,
+                    **kw)
 
 
 def run_case_checker(kind: str, w: int, h: int, ctrl: Controls, cur: int, l0, l1, tl: int, checker: str = "oracle",
@@ -413,6 +420,20 @@ def derive_controls(enc_mode: int, qp: int, input_resolution: int, temporal_laye
     return c
 
 
+def derive_controls_tf(hme_me_level: int, qp_opt: int, qp: int, input_resolution: int) -> Controls:
+    """The product's restatement of the TF-ME controls (svt_aom_sig_deriv_me_tf,
+    enc_mode_config.c:814-854) for a temporal-filtering (ME_MCTF) job."""
+    c = Controls()
+    load_product().svtme_derive_controls_tf(hme_me_level, qp_opt, qp, input_resolution, C.byref(c))
+    return c
+
+
+def ref_derive_controls_tf(hme_me_level: int, qp_opt: int, qp: int, input_resolution: int) -> Controls:
+    c = Controls()
+    load_ref().svtref_derive_controls_tf(hme_me_level, qp_opt, qp, input_resolution, C.byref(c))
+    return c
+
+
 def input_resolution_of(width: int, height: int) -> int:
     """svt_aom_derive_input_resolution (sequence_control_set.c:113-131) on the
     8-aligned luma size (resource_coordination_process.c:689)."""
@@ -432,7 +453,8 @@ def max_allocated_me_refs(l0: int, l1: int):
 def make_job(width: int, height: int, ctrl: Controls, picture_number: int, refs_l0=(), refs_l1=(),
              temporal_layer_index: int = 1, is_ref: bool = True, hierarchical_levels: int = 5,
              enable_me_8x8: bool = False, input_resolution: int | None = None, ref_count_used=(2, 2),
-             only_l_bwd: bool = True, gm_enabled: bool = False, sb_begin: int = 0, sb_count: int = 0) -> Job:
+             only_l_bwd: bool = True, gm_enabled: bool = False, sb_begin: int = 0, sb_count: int = 0,
+             me_type: int = ME_OPEN_LOOP, tf_me_exit_th: int = 0) -> Job:
     j = Job()
     j.picture_number = picture_number
     j.width, j.height = align8(width), align8(height)
@@ -455,6 +477,7 @@ def make_job(width: int, height: int, ctrl: Controls, picture_number: int, refs_
     j.input_resolution = input_resolution if input_resolution is not None else input_resolution_of(width, height)
     j.gm_enabled = 1 if gm_enabled else 0
     j.sb_begin, j.sb_count = sb_begin, sb_count
+    j.me_type, j.tf_me_exit_th = me_type, tf_me_exit_th
     j.ctrl = ctrl
     return j
 
@@ -510,6 +533,8 @@ def load_product():
         lib.svtme_last_error.restype = C.c_char_p
         lib.svtme_derive_controls.argtypes = [C.c_int] * 6 + [C.POINTER(Controls)]
         lib.svtme_derive_controls.restype = None
+        lib.svtme_derive_controls_tf.argtypes = [C.c_int] * 4 + [C.POINTER(Controls)]
+        lib.svtme_derive_controls_tf.restype = None
         lib.svtme_sb_total.argtypes = [C.c_uint32, C.c_uint32]
         lib.svtme_sb_total.restype = C.c_uint32
         lib._svtme_protos = True
@@ -622,7 +647,7 @@ def compare_records(a: np.ndarray, b: np.ndarray, sa=None, sb=None) -> list:
     """Bit-exact comparison on the fields the reference defines; returns a list
     of human-readable mismatch descriptions (empty = identical)."""
     errs = []
-    for f in ("searched", "do_ref", "hme_sad", "hme_sc_x", "hme_sc_y", "zz_sad", "best_mv"):
+    for f in ("searched", "do_ref", "tf_early_exit", "hme_sad", "hme_sc_x", "hme_sc_y", "zz_sad", "best_mv"):
         if not np.array_equal(a[f], b[f]):
             idx = np.argwhere(a[f] != b[f])[0]
             errs.append(f"{f} differs at {tuple(idx)}: {a[f][tuple(idx)]} vs {b[f][tuple(idx)]}")

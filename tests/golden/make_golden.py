@@ -13,9 +13,13 @@ stores inputs-as-parameters plus expected outputs:
   me_<name>.npz      expected per-SB reference records and SB results
                      (raw bytes of REF_RECORD_DTYPE / SB_RESULT_DTYPE), plus
                      sha256 digests of the reference's padded pyramids
+  controls_tf.json   svt_aom_sig_deriv_me_tf outputs (TF-ME controls) over
+                     hme_me_level x qp_opt x QP x resolution
+  tf_cases.json      temporal-filtering ME cases (me_type ME_MCTF: one list,
+                     one reference, HME-only exits) -> me_tf_<name>.npz
 
 Run from the repo root in the build container (needs /root/reference for the
-library build only): python tests/golden/make_golden.py
+library build only): python tests/golden/make_golden.py [tf]   (tf: TF fixtures only)
 """
 import hashlib
 import json
@@ -45,6 +49,17 @@ ME_CASES = [
     ("pan320_p8_band", "pan", 320, 192, 8, 1, (7, 6), (9, 10), {"sb_begin": 3, "sb_count": 7}),
     ("pan64_p0", "pan", 64, 64, 0, 1, (7,), (9,), {}),
     ("pan320_p8_nonref", "pan", 320, 192, 8, 2, (7,), (9,), {"is_ref": False}),
+]
+
+TF_CASES = [
+    # name, content, w, h, tf hme_me_level, qp_opt, qp, cur, ref, tl, tf_me_exit_th
+    ("tf_pan320_lvl0", "pan", 320, 192, 0, 0, 35, 8, 7, 1, 0),
+    ("tf_pan320_lvl1_fwd2", "pan", 320, 192, 1, 0, 35, 8, 10, 1, 0),
+    ("tf_pan640_lvl2_qp20_exit", "pan", 640, 360, 2, 1, 20, 8, 9, 0, 9800),
+    ("tf_pan320_lvl3_exit", "pan", 320, 192, 3, 0, 35, 8, 7, 1, 2600),
+    ("tf_noise192_lvl3", "noise", 192, 128, 3, 0, 35, 8, 6, 2, 0),
+    ("tf_flat192_lvl4_exit", "flat", 192, 128, 4, 0, 35, 8, 7, 1, 1),
+    ("tf_stripes320_lvl2_exit", "stripes", 320, 192, 2, 0, 35, 8, 9, 1, 50000),
 ]
 
 CTRL_GRID = dict(enc_mode=list(range(14)), input_resolution=list(range(7)), tl=[0, 1, 2, 3], qp=[35, 55])
@@ -89,6 +104,45 @@ def rtcd_golden():
     print("rtcd cases", len(out))
 
 
+def tf_golden():
+    """TF-ME (me_type ME_MCTF) fixtures: controls of svt_aom_sig_deriv_me_tf and
+    the reference's svt_aom_motion_estimation_b64 run as temporal_filtering.c:3127-3174
+    runs it (one list, one reference)."""
+    ref = S.load_ref()
+    unique, index, rows = [], {}, []
+    for lvl in range(5):
+        for qp_opt in (0, 1):
+            for qp in (10, 20, 35, 55):
+                for res in range(7):
+                    d = S.ref_derive_controls_tf(lvl, qp_opt, qp, res).as_dict()
+                    key = json.dumps(d, sort_keys=True)
+                    if key not in index:
+                        index[key] = len(unique)
+                        unique.append(d)
+                    rows.append([lvl, qp_opt, qp, res, index[key]])
+    with open(os.path.join(HERE, "controls_tf.json"), "w") as fh:
+        json.dump({"args": ["hme_me_level", "qp_opt", "qp", "input_resolution", "unique_index"], "unique": unique,
+                   "rows": rows}, fh, indent=0)
+    meta = []
+    for name, kind, w, h, lvl, qp_opt, qp, cur, refp, tl, th in TF_CASES:
+        ctrl = S.ref_derive_controls_tf(lvl, qp_opt, qp, S.input_resolution_of(w, h))
+        extra = {"me_type": S.ME_MCTF, "tf_me_exit_th": th}
+        out = {}
+        for simd in (0, 1):  # C kernels and AVX2 kernels must agree
+            ref.svtref_set_simd(simd)
+            out[simd] = S.run_case_checker(kind, w, h, ctrl, cur, (refp,), (), tl, checker="ref", **extra)
+        recs, sbr = out[0]
+        assert not S.compare_records(recs, out[1][0], sbr, out[1][1]), name
+        np.savez_compressed(os.path.join(HERE, f"me_{name}.npz"), records=recs.view(np.uint8).reshape(len(recs), -1),
+                            sb=sbr.view(np.uint8).reshape(len(sbr), -1))
+        meta.append({"name": name, "content": kind, "w": w, "h": h, "cur": cur, "tl": tl, "l0": [refp], "l1": [],
+                     "hme_me_level": lvl, "qp_opt": qp_opt, "qp": qp, "ctrl": ctrl.as_dict(), "extra": extra,
+                     "checksum": S.records_checksum(recs, sbr), "tf_exits": int(recs["tf_early_exit"].sum())})
+        print(name, recs.shape, "exits", meta[-1]["tf_exits"], meta[-1]["checksum"][:16])
+    with open(os.path.join(HERE, "tf_cases.json"), "w") as fh:
+        json.dump(meta, fh, indent=1)
+
+
 def main():
     ref = S.load_ref()
     rtcd_golden()
@@ -116,4 +170,6 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] != ["tf"]:
+        main()
+    tf_golden()

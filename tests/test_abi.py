@@ -48,6 +48,7 @@ int main(void) {
     O(svtme_job, ctrl); O(svtme_job, sb_begin); O(svtme_job, sb_count); O(svtme_job, ref_picture_number);
     O(svtme_ref_record, best_mv); O(svtme_ref_record, hme_sad); O(svtme_ref_record, hme_sc_x);
     O(svtme_ref_record, zz_sad); O(svtme_ref_record, searched); O(svtme_ref_record, do_ref);
+    O(svtme_ref_record, tf_early_exit); O(svtme_job, me_type); O(svtme_job, tf_me_exit_th);
     O(svtme_sb_result, me_candidate_array); O(svtme_sb_result, me_mv_array); O(svtme_sb_result, me_distortion);
     O(svtme_sb_result, me_8x8_cost_variance); O(svtme_sb_result, rc_me_allow_gm);
     O(svtme_controls, prehme_sa_cfg); O(svtme_controls, me_early_exit_th);
@@ -74,7 +75,9 @@ def test_struct_layouts_match_mirrors(svtme, tmp_path):
     assert got["svtme_job.sb_begin"] == S.Job.sb_begin.offset
     assert got["svtme_job.sb_count"] == S.Job.sb_count.offset
     assert got["svtme_job.ref_picture_number"] == S.Job.ref_picture_number.offset
-    for f in ("best_mv", "hme_sad", "hme_sc_x", "zz_sad", "searched", "do_ref"):
+    assert got["svtme_job.me_type"] == S.Job.me_type.offset
+    assert got["svtme_job.tf_me_exit_th"] == S.Job.tf_me_exit_th.offset
+    for f in ("best_mv", "hme_sad", "hme_sc_x", "zz_sad", "searched", "do_ref", "tf_early_exit"):
         assert got[f"svtme_ref_record.{f}"] == S.REF_RECORD_DTYPE.fields[f][1], f
     for f in ("me_candidate_array", "me_mv_array", "me_distortion", "me_8x8_cost_variance", "rc_me_allow_gm"):
         assert got[f"svtme_sb_result.{f}"] == S.SB_RESULT_DTYPE.fields[f][1], f

@@ -106,3 +106,20 @@ def test_10bit_msb_parity(svtme, gpu):
     assert not S.compare_records(orecs, recs, osbr, sbr)
     for t in f10:
         gpu.release(2000 + t)
+
+
+def test_mctf_job_fails_loudly(svtme, gpu):
+    """TF-ME jobs are checked on the CPU side (tests/test_oracle.py); this
+    build's kernels do not run them and must refuse rather than return
+    open-loop results."""
+    S = svtme
+    w, h = 128, 64
+    f = S.Synth(w, h)
+    for t in (7, 8):
+        gpu.upload(3000 + t, f.frame(t))
+    ctrl = S.derive_controls_tf(2, 0, 35, S.input_resolution_of(w, h))
+    job = S.make_job(w, h, ctrl, 3008, (3007,), (), ref_count_used=(1, 0), me_type=S.ME_MCTF)
+    with pytest.raises(RuntimeError):
+        gpu.submit(job)
+    for t in (7, 8):
+        gpu.release(3000 + t)

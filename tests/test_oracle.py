@@ -86,3 +86,55 @@ def test_oracle_vs_ref(svtme, preset, tl, size, kind):
     b = S.run_case_checker(kind, w, h, ctrl, 8, l0, l1, tl, checker="ref", nthreads=4)
     errs = S.compare_records(b[0], a[0], b[1], a[1])
     assert not errs, errs[:5]
+
+
+# ---------------------------------------------------------------------------
+# TF-ME (me_type ME_MCTF, temporal_filtering.c:3127-3174): same path, other
+# controls (svt_aom_sig_deriv_me_tf) and flow (no pruning, undistanced full-pel
+# area, HME-only exit, no candidates)
+# ---------------------------------------------------------------------------
+with open(os.path.join(GOLD, "tf_cases.json")) as _fh:
+    TF_CASES = json.load(_fh)
+
+
+@pytest.mark.parametrize("case", TF_CASES, ids=lambda c: c["name"])
+def test_oracle_tf_vs_golden(svtme, case):
+    S = svtme
+    ctrl = S.Controls.from_dict(case["ctrl"])
+    recs, sbr = S.run_case_checker(case["content"], case["w"], case["h"], ctrl, case["cur"], tuple(case["l0"]), (),
+                                   case["tl"], checker="oracle", nthreads=4, **case["extra"])
+    z = np.load(os.path.join(GOLD, f"me_{case['name']}.npz"))
+    exp_recs = z["records"].view(S.REF_RECORD_DTYPE).reshape(recs.shape)
+    exp_sb = z["sb"].view(S.SB_RESULT_DTYPE).reshape(sbr.shape)
+    errs = S.compare_records(exp_recs, recs, exp_sb, sbr)
+    assert not errs, errs[:5]
+    assert int(recs["tf_early_exit"].sum()) == case["tf_exits"]
+    assert S.records_checksum(recs, sbr) == case["checksum"]
+
+
+def test_product_derive_controls_tf_vs_golden(svtme):
+    """svtme_derive_controls_tf (product host code) == svt_aom_sig_deriv_me_tf."""
+    S = svtme
+    with open(os.path.join(GOLD, "controls_tf.json")) as fh:
+        gold = json.load(fh)
+    bad = []
+    for lvl, qp_opt, qp, res, idx in gold["rows"]:
+        got = json.loads(json.dumps(S.derive_controls_tf(lvl, qp_opt, qp, res).as_dict()))
+        if got != gold["unique"][idx]:
+            diff = {k: (got.get(k), v) for k, v in gold["unique"][idx].items() if got.get(k) != v}
+            bad.append(((lvl, qp_opt, qp, res), diff))
+    assert not bad, bad[:3]
+
+
+@pytest.mark.skipif(not ref_available(), reason="oracle/_ref not built (needs /root/reference)")
+@pytest.mark.parametrize("lvl,th,kind", [(0, 0, "pan"), (2, 30000, "noise"), (4, 3000, "pan")])
+def test_oracle_tf_vs_ref(svtme, lvl, th, kind):
+    S = svtme
+    w, h = 256, 144
+    ctrl = S.ref_derive_controls_tf(lvl, 1, 35, S.input_resolution_of(w, h))
+    kw = dict(me_type=S.ME_MCTF, tf_me_exit_th=th)
+    a = S.run_case_checker(kind, w, h, ctrl, 8, (6,), (), 1, checker="oracle", nthreads=4, **kw)
+    S.load_ref().svtref_set_simd(1)
+    b = S.run_case_checker(kind, w, h, ctrl, 8, (6,), (), 1, checker="ref", nthreads=4, **kw)
+    errs = S.compare_records(b[0], a[0], b[1], a[1])
+    assert not errs, errs[:5]
