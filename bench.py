@@ -39,7 +39,7 @@ WINDOW_BYTES = {"p8": 16798, "p6": 38121, "p8_sa64": 28241}
 # source 64x32 + 16x8 in stage A, 32x16 in stage B)
 # (stage D only reads stage A's 448-B result block per SB: no window bytes)
 STAGE_BYTES = {"p8": ((2176, 6808), (0, 0), (512, 5304), (0, 4686 + 680))}
-STAGE_NAMES = ("k_stage_a", "k_stage_d", "k_stage_b", "k_stage_c")
+STAGE_NAMES = ("k_stage_a", "k_stage_d", "k_stage_b", "k_stage_c1+k_stage_e")
 
 WORKLOADS = {
     "4k_p8": dict(w=3840, h=2160, mode=8, tl=1, l0=(7, 6), l1=(9, 10), windows="p8", ten_bit=False,
@@ -201,7 +201,7 @@ def main():
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "ME pass = k_stage_a + k_stage_d + k_stage_b + k_stage_c (one picture job)",
+                         "kernel": "ME pass = k_stage_a + k_stage_d + k_stage_b + k_stage_c1 + k_stage_e (one picture job)",
                          "kernel_avg_ms": round(k_avg_ms, 4), "bytes_per_launch": bps * n_sb,
                          "stages": stages},
             "cpu_baseline": cpu_baseline,

@@ -261,8 +261,8 @@ svtme_status svtme_submit_picture_device(svtme_ctx *ctx, const svtme_job *job, s
 /* Time the ME kernels of every job with HIP events on the context's stream
  * (enable = 1); svtme_kernel_ms returns the last job's time over all of its
  * kernels, svtme_stage_ms the part of stage 0 (k_stage_a: zz / pre-HME /
- * HME-L0), 1 (k_stage_b: HME-L1/L2 + centres) or 2 (k_stage_c: full-pel +
- * candidates). */
+ * HME-L0), 1 (k_stage_d: their decisions), 2 (k_stage_b: HME-L1/L2) or 3
+ * (full-pel search + candidates: k_stage_c1 + k_stage_e, or k_stage_c). */
 svtme_status svtme_set_timing(svtme_ctx *ctx, int enable);
 float svtme_kernel_ms(svtme_ctx *ctx);
 float svtme_stage_ms(svtme_ctx *ctx, int stage);

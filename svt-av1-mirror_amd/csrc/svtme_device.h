@@ -55,6 +55,16 @@ struct BState {
     uint8_t do_ref[8];
 };
 
+// Per (SB, reference record) state the wide full-pel stage (k_stage_c1)
+// leaves for the per-SB decode (k_stage_e), svtme_stages.hip.
+struct CSlot {
+    uint64_t hme_sad;
+    uint32_t zz;
+    int16_t sc_x, sc_y;        // HME search centre (record fields)
+    int16_t xo, yo, w, xc, yc; // full-pel window origin and width, probe centre
+    uint8_t searched, do_ref, probe, tf_exit;
+};
+
 // Parameters of one picture job as the kernel sees them.
 struct DevJob {
     svtme_job job;                 // controls + picture description (host copy)
@@ -71,6 +81,9 @@ struct DevJob {
     uint8_t ta_list[SVTME_A_N];    // their ARes indices
     uint32_t tb_count;             // stage-B refinements per SB
     uint8_t tb_list[32];           // their (slot << 2 | quadrant)
+    unsigned long long *keys;      // [sb_count][R][85] full-pel argmin keys (sad << 32 | order)
+    CSlot *cslot;                  // [sb_count][R]
+    uint32_t parts;                // search-row bands per (SB, reference) in k_stage_c1; 0 = per-SB k_stage_c
 };
 
 static inline uint32_t svtme_round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }

@@ -33,6 +33,7 @@ extern "C" hipError_t svtme_launch_me2(const DevJob *dj, uint32_t sb_count, hipS
 extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
+extern "C" uint32_t svtme_fp_parts(const svtme_controls *c);
 
 // ----------------------------------------------------------------------------
 // errors
@@ -101,6 +102,11 @@ struct svtme_ctx {
     size_t ares_cap = 0;
     BState *d_bst   = nullptr; // stage-B state [count]
     size_t bst_cap  = 0;
+    unsigned long long *d_keys = nullptr; // wide full-pel argmin keys [count][R][85]
+    size_t keys_cap            = 0;
+    bool keys_rest             = false; // every key is ~0 (banded jobs accumulate with atomic min)
+    CSlot *d_cslot             = nullptr; // [count][R]
+    size_t cslot_cap           = 0;
 #ifdef SVTME_STAMPS
     unsigned long long *d_stamps = nullptr;
     size_t stamps_cap            = 0;
@@ -182,6 +188,10 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         (void)hipFree(c->d_ares);
     if (c->d_bst)
         (void)hipFree(c->d_bst);
+    if (c->d_keys)
+        (void)hipFree(c->d_keys);
+    if (c->d_cslot)
+        (void)hipFree(c->d_cslot);
     (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -361,8 +371,6 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
     if (job->me_type != 0 && job->me_type != SVTME_ME_OPEN_LOOP && job->me_type != SVTME_ME_MCTF)
         return fail(SVTME_ERR_BAD_PARAMETER, "me_type %u is neither SVTME_ME_OPEN_LOOP nor SVTME_ME_MCTF",
                     job->me_type);
-    if (job->me_type == SVTME_ME_MCTF)
-        return fail(SVTME_ERR_BAD_PARAMETER, "MCTF (temporal-filtering) jobs are not run by this build's kernels");
     if (job->width > 16384 || job->height > 16384)
         return fail(SVTME_ERR_BAD_PARAMETER, "picture too large for int16 search arithmetic");
     const uint32_t total = svtme_sb_total(job->width, job->height);
@@ -435,6 +443,25 @@ static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_
         return st;
     dj.ares = c->d_ares;
     dj.bst  = c->d_bst;
+    dj.parts = svtme_fp_parts(&dj.job.ctrl);
+    if (dj.parts) { // wide full-pel stage (k_stage_c1 + k_stage_e)
+        const size_t kb = (size_t)count * dj.R * SVTME_PU_COUNT * sizeof(unsigned long long);
+        if (c->keys_cap < kb) {
+            if ((st = ensure_buf((void **)&c->d_keys, &c->keys_cap, kb)))
+                return st;
+            c->keys_rest = false;
+        }
+        if ((st = ensure_buf((void **)&c->d_cslot, &c->cslot_cap, (size_t)count * dj.R * sizeof(CSlot))))
+            return st;
+        if (dj.parts > 1 && !c->keys_rest) {
+            HIP_TRY(hipMemsetAsync(c->d_keys, 0xFF, c->keys_cap, c->stream));
+            c->keys_rest = true;
+        }
+        if (dj.parts == 1)
+            c->keys_rest = false; // plain stores leave keys behind
+        dj.keys  = c->d_keys;
+        dj.cslot = c->d_cslot;
+    }
     svtme_stage_a_list(&dj.job, dj.ta_list, &dj.ta_count);
     svtme_stage_b_list(&dj.job, dj.tb_list, &dj.tb_count);
     static const int kernel_version = [] {
@@ -466,6 +493,8 @@ static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_
             djk.out_sb       = dj.out_sb ? dj.out_sb + b0 : nullptr;
             djk.ares         = dj.ares + (size_t)b0 * SVTME_A_N;
             djk.bst          = dj.bst + b0;
+            djk.keys         = dj.keys ? dj.keys + (size_t)b0 * dj.R * SVTME_PU_COUNT : nullptr;
+            djk.cslot        = dj.cslot ? dj.cslot + (size_t)b0 * dj.R : nullptr;
             djk.stamps       = dj.stamps ? dj.stamps + (size_t)b0 * 16 : nullptr;
             HIP_TRY(hipStreamWaitEvent(c->side[k], c->ev_fork, 0));
             HIP_TRY(svtme_launch_stages(&djk, b1 - b0, c->side[k], nullptr));

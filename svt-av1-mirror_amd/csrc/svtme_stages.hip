@@ -947,7 +947,7 @@ __device__ SlotCentre final_centre(const DevJob &dj, uint32_t sb_local, uint32_t
         hsad = my_hs;
     uint32_t rdiv = 1;
     uint8_t dref  = s < 8 ? b->do_ref[s] : 0;
-    if (c.enable_hme_flag) { // prune_ref = enable_hme_flag && me_type != ME_MCTF
+    if (c.enable_hme_flag && job.me_type != SVTME_ME_MCTF) { // prune_ref (motion_estimation.c:3103)
         const uint16_t th = c.prune_ref_if_hme_sad_dev_bigger_than_th;
         if (c.enable_me_hme_ref_pruning && th != (uint16_t)~0) {
             const uint64_t best = wave_min_u64(s < 8 ? hsad : ~0ull);
@@ -996,6 +996,7 @@ struct StC {
     uint32_t reduce_div[8];
     int16_t sc_x[8], sc_y[8];
     uint8_t do_ref[8], searched[8], in_round[8];
+    uint8_t tf_exit; // MCTF HME-only exit (motion_estimation.c:3109-3113)
     int16_t is_w[8], is_h[8], is_wb[8], is_hb[8], is_xc[8], is_yc[8];
     uint64_t is_best_hme[8];
     const uint8_t *req[16]; // check_00_center n x m requests
@@ -1201,6 +1202,8 @@ __device__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t
     uint32_t *ow = (uint32_t *)o; // zero the result (sizeof is a multiple of 4)
     for (int i = tid; i < (int)(sizeof(svtme_sb_result) / 4); i += 256) ow[i] = 0;
     __syncthreads();
+    if (job.me_type == SVTME_ME_MCTF) // no candidates / distortions (motion_estimation.c:3126)
+        return;
     const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
     const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
     if (mode != 2 && tid < npus)
@@ -1416,6 +1419,76 @@ __device__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t
     }
 }
 
+// me_prune_ref, the per-reference records and the candidate arrays /
+// distortions / GM detection of one SB from its searched best SADs and MVs
+// (motion_estimation.c:1522-1565, 2520-3007); all threads of the workgroup
+__device__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh, uint32_t vmask) {
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const bool w0 = (tid >> 6) == 0;
+    // ---- me_prune_ref (motion_estimation.c:1522-1565)
+    if (job.me_type != SVTME_ME_MCTF && c.enable_hme_flag && c.enable_me_hme_ref_pruning && w0) {
+        const int s = lane;
+        uint64_t v  = ~0ull;
+        if (s < 8) {
+            v = st.hme_sad[s];
+            if (slot_valid(vmask, s)) {
+                if (!st.do_ref[s])
+                    v = (uint64_t)SVTME_MAX_SAD_VALUE * 64;
+                else {
+                    uint64_t sum = 0;
+                    for (int i = 0; i < 64; i++) sum += st.best_sad[s][21 + i];
+                    v = sum;
+                }
+                st.hme_sad[s] = v;
+            }
+        }
+        const uint16_t th = c.prune_ref_if_me_sad_dev_bigger_than_th;
+        if (th != (uint16_t)~0) {
+            const uint64_t best = wave_min_u64(v);
+            if (s < 8 && (s & 3) >= 1 && (v - best) * 100 > (th * best))
+                st.do_ref[s] = 0;
+        }
+    }
+    __syncthreads();
+    STAMP(14);
+
+    // ---- records (sb_count x R, slots in list-0-then-list-1 order)
+    {
+        svtme_ref_record *out = dj.out_records + (size_t)sb_local * dj.R;
+        const int R = (int)dj.R;
+        for (int k = 0; k < R; k++) { // 704 bytes = 176 dwords per record
+            const int s = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
+            const int w = tid;
+            if (w >= 176)
+                continue;
+            uint32_t v;
+            if (w < 85)
+                v = st.searched[s] ? st.best_sad[s][w] : U32MAX;
+            else if (w < 170)
+                v = st.best_mv[s][w - 85];
+            else if (w == 170)
+                v = (uint32_t)st.hme_sad[s];
+            else if (w == 171)
+                v = (uint32_t)(st.hme_sad[s] >> 32);
+            else if (w == 172)
+                v = (uint32_t)(uint16_t)st.sc_x[s] | ((uint32_t)(uint16_t)st.sc_y[s] << 16);
+            else if (w == 173)
+                v = st.zz[s];
+            else if (w == 174)
+                v = (uint32_t)st.searched[s] | ((uint32_t)st.do_ref[s] << 8) | ((uint32_t)st.tf_exit << 16);
+            else
+                v = 0;
+            ((uint32_t *)(out + k))[w] = v;
+        }
+    }
+    if (dj.out_sb) {
+        __syncthreads();
+        finish_sb(st, dj, sb_local, bw, bh);
+    }
+}
+
 template <bool SUB_ME>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_c(const DevJob dj) {
     __shared__ StC st;
@@ -1440,6 +1513,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
     if (w0) {
         const SlotCentre sc = final_centre(dj, sb_local, vmask);
+        const uint64_t h0   = __shfl(sc.hme_sad, 0, 64);
+        const bool tf_exit  = job.me_type == SVTME_ME_MCTF && h0 < job.tf_me_exit_th;
         if (lane < 8) {
             st.hme_sad[lane]    = sc.hme_sad;
             st.zz[lane]         = sc.zz;
@@ -1447,8 +1522,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             st.sc_x[lane]       = sc.sc_x;
             st.sc_y[lane]       = sc.sc_y;
             st.do_ref[lane]     = sc.do_ref;
-            st.searched[lane]   = sc.do_ref;
+            st.searched[lane]   = tf_exit ? 0 : sc.do_ref;
         }
+        if (lane == 0)
+            st.tf_exit = tf_exit;
     }
     for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) (&st.best_mv[0][0])[e] = 0;
     __syncthreads();
@@ -1460,12 +1537,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     for (int round = 0; round < rounds; round++) {
         if (w0) { // search area up to the 8x8-variance decision
             const int s = lane, r = s & 3;
-            const bool act = slot_valid(vmask, s) && (rounds == 1 || ((s == 0) == (round == 0))) && st.do_ref[s];
+            const bool act = slot_valid(vmask, s) && (rounds == 1 || ((s == 0) == (round == 0))) && st.searched[s];
             bool need = false;
             if (act) {
                 int16_t xc = st.sc_x[s], yc = st.sc_y[s];
                 int16_t w = (int16_t)c.me_sa.sa_min.width, h = (int16_t)c.me_sa.sa_min.height;
-                const uint16_t dist = scaled_dist(st.dist[s]);
+                const uint16_t dist = job.me_type == SVTME_ME_MCTF ? st.dist[s] : scaled_dist(st.dist[s]);
                 w = i16(min((int)(w * dist), (int)c.me_sa.sa_max.width));
                 h = i16(min((int)(h * dist), (int)c.me_sa.sa_max.height));
                 if (c.mv_sa_adj_enabled && (!c.mv_sa_adj_nearest_ref_only || r == 0)) {
@@ -1641,68 +1718,349 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             fullpel<SUB_ME>(st, C, ox, oy);
     }
 
-    // ---- me_prune_ref (motion_estimation.c:1522-1565)
-    if (c.enable_hme_flag && c.enable_me_hme_ref_pruning && w0) {
-        const int s = lane;
-        uint64_t v  = ~0ull;
-        if (s < 8) {
-            v = st.hme_sad[s];
-            if (slot_valid(vmask, s)) {
-                if (!st.do_ref[s])
-                    v = (uint64_t)SVTME_MAX_SAD_VALUE * 64;
-                else {
-                    uint64_t sum = 0;
-                    for (int i = 0; i < 64; i++) sum += st.best_sad[s][21 + i];
-                    v = sum;
+    stage_c_tail(st, dj, sb_local, bw, bh, vmask);
+    STAMP(15);
+}
+
+// ----------------------------------------------------------------------------
+// Stage C, wide form: one wavefront per (SB, reference slot, band of search
+// rows) runs that slot's integer_search_b64 (motion_estimation.c:1249-1516);
+// k_stage_e then decodes the 85-PU argmins per SB and runs me_prune_ref, the
+// records and the candidate arrays. A slot's search area depends on no other
+// slot's search unless enable_me_sr_adjustment == 2 (slot 0's 64x64 SAD,
+// :1355-1364), which keeps the per-SB k_stage_c.
+// ----------------------------------------------------------------------------
+// Running 85-PU minima of one lane (lane = 8x8 block in Z order). The 16x16,
+// 32x32 and 64x64 SADs are DPP lane sums (64x64 valid in lanes 48-63). Keys
+// are (sad << 12 | order) in 32 bits when every order < 4096 (a 64x64 SAD is
+// below 2^20), else (sad << 32 | order).
+template <bool K32>
+struct PuMin {
+    typedef typename std::conditional<K32, uint32_t, unsigned long long>::type key_t;
+    key_t b8, b16, b32, b64;
+    __device__ __forceinline__ void clear() { b8 = b16 = b32 = b64 = (key_t)~0ull; }
+    __device__ __forceinline__ static key_t make(uint32_t sad, uint32_t o) {
+        if (K32)
+            return (key_t)((sad << 12) | o);
+        return (key_t)(((unsigned long long)sad << 32) | o);
+    }
+    __device__ __forceinline__ static unsigned long long wide(key_t k) {
+        if (K32) {
+            const uint32_t v = (uint32_t)k;
+            return v == 0xFFFFFFFFu ? ~0ull : (((unsigned long long)(v >> 12) << 32) | (v & 0xFFFu));
+        }
+        return (unsigned long long)k;
+    }
+    __device__ __forceinline__ void add(uint32_t s8, uint32_t o) {
+        const uint32_t s16 = dpp_add<0x4E>(dpp_add<0xB1>(s8));              // xor 1, xor 2
+        const uint32_t s32 = dpp_add<0x128>(dpp_add<0x124>(s16));           // row_ror 4, 8
+        const uint32_t s64 = dpp_add<0x143, 0xC>(dpp_add<0x142, 0xA>(s32)); // valid in row 3
+        const key_t k8 = make(s8, o), k16 = make(s16, o), k32 = make(s32, o), k64 = make(s64, o);
+        b8  = k8 < b8 ? k8 : b8;
+        b16 = k16 < b16 ? k16 : b16;
+        b32 = k32 < b32 ? k32 : b32;
+        b64 = k64 < b64 ? k64 : b64;
+    }
+};
+
+// Full-pel SADs of this lane's 8x8 block (source rows src) at search rows
+// [y0, y1) x columns [0, w) of a window (a = dword-aligned address of window
+// row 0, sh = byte offset of column 0, nq = aligned position quads per row),
+// in TY x TQ tiles: the reference rows and dwords of a tile are loaded once,
+// all in flight together, and shared by its TY x TQ position quads. Orders are
+// obase + y * w + x (raster order, motion_estimation.c:781-817).
+template <bool SUB, bool K32, int TQ>
+__device__ __forceinline__ void fp_rows(PuMin<K32> &M, const uint32_t *a, int sdw, int sh, int w, int nq, int y0,
+                                        int y1, uint32_t obase, const uint32_t (&src)[SUB ? 4 : 8][2], int by,
+                                        int bx) {
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1, TY = 1; // taller tiles cost registers (aligned qsad pairs)
+    constexpr int NR = TY + (ROWS - 1) * RSTEP, ND = TQ + 2;
+    // uniform row bases (SGPRs) + one per-lane dword offset: every load is
+    // saddr + voffset + immediate
+    const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2);
+    for (int ty = y0; ty < y1; ty += TY) {
+        const int ny       = min(TY, y1 - ty);
+        const int last_row = ny - 1 + (ROWS - 1) * RSTEP;
+        for (int tq = 0; tq < nq; tq += TQ) {
+            const int nqq = min(TQ, nq - tq);
+            uint32_t T[NR][ND];
+#pragma unroll
+            for (int i = 0; i < NR; i++) {
+                const uint32_t *rowp = uni_ptr(a + (ptrdiff_t)(ty + min(i, last_row)) * sdw + tq);
+#pragma unroll
+                for (int j = 0; j < ND; j++) T[i][j] = rowp[lo + (uint32_t)min(j, nqq + 1)];
+            }
+#pragma unroll
+            for (int iy = 0; iy < TY; iy++) {
+                if (iy >= ny)
+                    break; // wave-uniform
+#pragma unroll
+                for (int iq = 0; iq < TQ; iq++) {
+                    if (iq >= nqq)
+                        break; // wave-uniform
+                    unsigned long long acc = 0;
+#pragma unroll
+                    for (int rr = 0; rr < ROWS; rr++) {
+                        acc = qsad(T[iy + rr * RSTEP][iq], T[iy + rr * RSTEP][iq + 1], src[rr][0], acc);
+                        acc = qsad(T[iy + rr * RSTEP][iq + 1], T[iy + rr * RSTEP][iq + 2], src[rr][1], acc);
+                    }
+                    uint32_t s4[4] = {0, 0, 0, 0};
+                    qsad_unpack(acc, s4);
+                    const int y = ty + iy;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        const int x = 4 * (tq + iq) - sh + k;
+                        if (x >= 0 && x < w) // wave-uniform
+                            M.add(SUB ? s4[k] << 1 : s4[k], obase + (uint32_t)(y * w + x));
+                    }
                 }
-                st.hme_sad[s] = v;
             }
         }
-        const uint16_t th = c.prune_ref_if_me_sad_dev_bigger_than_th;
-        if (th != (uint16_t)~0) {
-            const uint64_t best = wave_min_u64(v);
-            if (s < 8 && (s & 3) >= 1 && (v - best) * 100 > (th * best))
-                st.do_ref[s] = 0;
+    }
+}
+
+#define FP_TQ 3 // position quads per full-pel tile (sub-sampled rows; 2 for full rows)
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+}
+
+// K32: every order fits 12 bits (the host bounds the area, svtme_fp_k32)
+template <bool SUB, bool K32>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 5 : 4, 8))) k_stage_c1(const DevJob dj) {
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t parts  = dj.parts;
+    const uint32_t per_sb = dj.R * parts;
+    const uint32_t gw     = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (gw >= job.sb_count * per_sb)
+        return;
+    const uint32_t sb_local = UNI(gw / per_sb);
+    const uint32_t rem      = gw - sb_local * per_sb;
+    const int k             = UNI(rem / parts);
+    const int part          = UNI(rem - (uint32_t)k * parts);
+    const int s             = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
+    const int l = s >> 2, r = s & 3;
+    const SbGeo G     = sb_geo(dj, sb_local);
+    const uint32_t ox = G.ox, oy = G.oy;
+    const bool mctf   = job.me_type == SVTME_ME_MCTF;
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1;
+    const int z16 = lane >> 2, k4 = lane & 3;
+    const int by  = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
+    const int bx  = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
+
+    // this lane's 8x8 source block, read in place (me_process.c:183-214), issued first
+    const DevPlane &C = dj.cur.lv[0];
+    uint32_t src[ROWS][2];
+#pragma unroll
+    for (int rr = 0; rr < ROWS; rr++) {
+        const uint32_t *sp =
+            (const uint32_t *)(C.base + (ptrdiff_t)(oy + by * 8 + rr * RSTEP) * C.stride + ox + bx * 8);
+        src[rr][0] = sp[0];
+        src[rr][1] = sp[1];
+    }
+    // search centre and HME pruning of the SB (lane = slot)
+    const SlotCentre scv   = final_centre(dj, sb_local, valid_mask(job));
+    const uint64_t hme_sad = rl64(scv.hme_sad, s);
+    const uint32_t zz = rl32(scv.zz, s), rdiv = rl32(scv.reduce_div, s);
+    const int16_t sc_x = (int16_t)rl32((uint32_t)(int32_t)scv.sc_x, s);
+    const int16_t sc_y = (int16_t)rl32((uint32_t)(int32_t)scv.sc_y, s);
+    const uint8_t dref = (uint8_t)rl32(scv.do_ref, s);
+    const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
+    CSlot *cs = dj.cslot + (size_t)sb_local * dj.R + k;
+    if (!dref || tf_exit) {
+        if (part == 0 && lane == 0)
+            *cs = CSlot{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
+        return;
+    }
+
+    // search area (integer_search_b64, :1282-1351)
+    const DevPlane &P = dj.ref[l][r].lv[0];
+    int16_t xc = sc_x, yc = sc_y;
+    uint16_t dist = ref_dist_const(job, l, r);
+    if (!mctf) // :1300-1302
+        dist = scaled_dist(dist);
+    int16_t w = i16(min((int)(c.me_sa.sa_min.width * dist), (int)c.me_sa.sa_max.width));
+    int16_t h = i16(min((int)(c.me_sa.sa_min.height * dist), (int)c.me_sa.sa_max.height));
+    if (c.mv_sa_adj_enabled && (!c.mv_sa_adj_nearest_ref_only || r == 0)) {
+        if (absi(xc) > c.mv_sa_adj_mv_size_th)
+            w = i16(w * c.mv_sa_adj_sa_multiplier);
+        if (absi(yc) > c.mv_sa_adj_mv_size_th)
+            h = i16(h * c.mv_sa_adj_sa_multiplier);
+    }
+    w = i16((max(1u, ((uint32_t)(int32_t)w / rdiv)) + 7) & ~0x07u);
+    h = i16(max(3u, ((uint32_t)(int32_t)h / rdiv)));
+    const int16_t pad = 63, org_x = (int16_t)ox, org_y = (int16_t)oy;
+    if (c.me_early_exit_th) {
+        if (zz < (c.me_early_exit_th / 6)) {
+            w = 1;
+            h = 1;
         }
+    } else if ((xc != 0 || yc != 0) && job.is_ref) { // check_00_center (:1139-1206)
+        const int16_t pw = i16(P.width), ph = i16(P.height);
+        xc = ((org_x + xc) < -pad) ? i16(-pad - org_x) : xc;
+        xc = ((org_x + xc) > pw - 1) ? i16(xc - ((org_x + xc) - (pw - 1))) : xc;
+        yc = ((org_y + yc) < -pad) ? i16(-pad - org_y) : yc;
+        yc = ((org_y + yc) > ph - 1) ? i16(yc - ((org_y + yc) - (ph - 1))) : yc;
+        const uint8_t *cb = C.base + (ptrdiff_t)oy * C.stride + ox;
+        const uint32_t zero_sad =
+            wave_nxm(P.base + (ptrdiff_t)oy * P.stride + ox, 2 * P.stride, cb, 2 * C.stride, (int)(G.bh >> 1),
+                     (int)G.bw)
+            << 1;
+        const uint32_t hme_mv_sad = wave_nxm(P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc),
+                                             2 * P.stride, cb, 2 * C.stride, (int)(G.bh >> 1), (int)G.bw)
+            << 1;
+        const uint64_t zc = (uint64_t)zero_sad << 8, hc = (uint64_t)hme_mv_sad << 8;
+        if (min_u64(zc, hc) == zc) {
+            xc = 0;
+            yc = 0;
+        }
+    }
+    // 8x8-variance centre probe and search-area resize (:1391-1439); the probe's
+    // keys (order 0) stay in M, so the centre wins ties against the main search
+    PuMin<K32> M;
+    M.clear();
+    const bool probe = c.me_8x8_var_enabled && (w * h > 24);
+    if (probe) {
+        const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc);
+        const int sh     = (int)((uintptr_t)g & 3);
+        fp_rows<SUB, K32, 1>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
+        const uint32_t p8   = (uint32_t)(PuMin<K32>::wide(M.b8) >> 32);
+        const uint32_t p64  = rl32((uint32_t)(PuMin<K32>::wide(M.b64) >> 32), 63);
+        const uint32_t mean = p64 / 64;
+        const int32_t diff  = (int32_t)p8 - (int32_t)mean;
+        const uint32_t var  = wave_sum_u32((uint32_t)(diff * diff)) / 64;
+        if (var > c.me_sr_mult2_th) {
+            w = i16((max(1, w * 3 / 2) + 7) & ~0x7);
+            h = i16(max(1, h * 3 / 2));
+        }
+        if (var < c.me_sr_div4_th) {
+            w = i16((max(1, w >> 2) + 7) & ~0x7);
+            h = i16(max(1, h >> 2));
+            h = i16(max(3, (int)h));
+        } else if (var < c.me_sr_div2_th) {
+            w = i16((min((int)w, w >> 1) + 7) & ~0x7);
+            h = i16(min((int)h, h >> 1));
+            h = i16(max(3, (int)h));
+        }
+    }
+    // final area clamp (:1440-1482)
+    const int16_t pic_w = (int16_t)job.width, pic_h = (int16_t)job.height;
+    int16_t xo = i16(xc - (w >> 1));
+    int16_t yo = i16(yc - (h >> 1));
+    xo = ((org_x + xo) < -pad) ? i16(-pad - org_x) : xo;
+    w  = ((org_x + xo) < -pad) ? i16(w - (-pad - (org_x + xo))) : w;
+    xo = ((org_x + xo) > pic_w - 1) ? i16(xo - ((org_x + xo) - (pic_w - 1))) : xo;
+    w  = ((org_x + xo + w) > pic_w) ? i16(max(1, w - ((org_x + xo + w) - pic_w))) : w;
+    w  = (w < 8) ? w : i16(w & ~0x07);
+    yo = ((org_y + yo) < -pad) ? i16(-pad - org_y) : yo;
+    h  = ((org_y + yo) < -pad) ? i16(h - (-pad - (org_y + yo))) : h;
+    yo = ((org_y + yo) > pic_h - 1) ? i16(yo - ((org_y + yo) - (pic_h - 1))) : yo;
+    h  = (org_y + yo + h > pic_h) ? i16(max(1, h - ((org_y + yo + h) - pic_h))) : h;
+
+    // full-pel search of this part's rows (open_loop_me_fullpel_search_sblock, :781-817)
+    const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yo) * P.stride + ((int)ox + xo);
+    const int sh     = (int)((uintptr_t)g & 3);
+    const int nq     = (sh + w + 3) >> 2;
+    const int y0 = (int)(((uint32_t)h * part) / parts), y1 = (int)(((uint32_t)h * (part + 1)) / parts);
+    const uint32_t obase = probe ? 1u : 0u; // the centre probe wins ties: order 0
+    fp_rows<SUB, K32, SUB ? FP_TQ : 2>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
+    const unsigned long long k8 = PuMin<K32>::wide(M.b8), k16 = PuMin<K32>::wide(M.b16);
+    const unsigned long long k32 = PuMin<K32>::wide(M.b32), k64 = PuMin<K32>::wide(M.b64);
+    unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
+    if (parts == 1) {
+        kp[21 + lane] = k8;
+        if ((lane & 3) == 0)
+            kp[5 + (lane >> 2)] = k16;
+        if ((lane & 15) == 0)
+            kp[1 + (lane >> 4)] = k32;
+        if (lane == 63)
+            kp[0] = k64;
+    } else {
+        atomicMin(&kp[21 + lane], k8);
+        if ((lane & 3) == 0)
+            atomicMin(&kp[5 + (lane >> 2)], k16);
+        if ((lane & 15) == 0)
+            atomicMin(&kp[1 + (lane >> 4)], k32);
+        if (lane == 63)
+            atomicMin(&kp[0], k64);
+    }
+    if (part == 0 && lane == 0)
+        *cs = CSlot{hme_sad, zz, sc_x, sc_y, xo, yo, w, xc, yc, 1, dref, (uint8_t)probe, 0};
+}
+
+// Per SB: decode the argmin keys into best SAD / MV per PU (strict-< first
+// minimum in search order), then stage_c_tail
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_e(const DevJob dj) {
+    __shared__ StC st;
+    __shared__ CSlot csl[8];
+    const svtme_job &job    = dj.job;
+    const int tid           = threadIdx.x;
+    const uint32_t sb_local = xcd_remap(blockIdx.x, gridDim.x);
+    const SbGeo G           = sb_geo(dj, sb_local);
+    const uint32_t vmask    = valid_mask(job);
+    const int R             = (int)dj.R;
+    if (tid == 0) {
+#pragma unroll
+        for (int s = 0; s < 8; s++) {
+            st.pl[s][0]  = dj.ref[s >> 2][s & 3].lv[0];
+            st.dist[s]   = ref_dist_const(job, s >> 2, s & 3);
+            st.refpic[s] = job.ref_picture_number[s >> 2][s & 3];
+        }
+        st.tf_exit = 0;
+    }
+    if (tid < 8) {
+        st.searched[tid] = 0;
+        st.do_ref[tid]   = 0;
+        st.hme_sad[tid]  = U32MAX;
+        st.zz[tid]       = U32MAX;
+        st.sc_x[tid] = st.sc_y[tid] = 0;
     }
     __syncthreads();
-    STAMP(14);
-
-    // ---- records (sb_count x R, slots in list-0-then-list-1 order)
-    {
-        svtme_ref_record *out = dj.out_records + (size_t)sb_local * dj.R;
-        const int R = (int)dj.R;
-        for (int k = 0; k < R; k++) { // 704 bytes = 176 dwords per record
-            const int s = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
-            const int w = tid;
-            if (w >= 176)
-                continue;
-            uint32_t v;
-            if (w < 85)
-                v = st.searched[s] ? st.best_sad[s][w] : U32MAX;
-            else if (w < 170)
-                v = st.best_mv[s][w - 85];
-            else if (w == 170)
-                v = (uint32_t)st.hme_sad[s];
-            else if (w == 171)
-                v = (uint32_t)(st.hme_sad[s] >> 32);
-            else if (w == 172)
-                v = (uint32_t)(uint16_t)st.sc_x[s] | ((uint32_t)(uint16_t)st.sc_y[s] << 16);
-            else if (w == 173)
-                v = st.zz[s];
-            else if (w == 174)
-                v = (uint32_t)st.searched[s] | ((uint32_t)st.do_ref[s] << 8);
-            else
-                v = 0;
-            ((uint32_t *)(out + k))[w] = v;
+    if (tid < R) {
+        const int s     = tid < job.num_refs[0] ? tid : 4 + (tid - job.num_refs[0]);
+        const CSlot v   = dj.cslot[(size_t)sb_local * R + tid];
+        csl[s]          = v;
+        st.hme_sad[s]   = v.hme_sad;
+        st.zz[s]        = v.zz;
+        st.sc_x[s]      = v.sc_x;
+        st.sc_y[s]      = v.sc_y;
+        st.searched[s]  = v.searched;
+        st.do_ref[s]    = v.do_ref;
+        if (tid == 0)
+            st.tf_exit = v.tf_exit;
+    }
+    __syncthreads();
+    unsigned long long *kb = dj.keys + (size_t)sb_local * R * SVTME_PU_COUNT;
+    for (int e = tid; e < R * SVTME_PU_COUNT; e += 256) {
+        const int kk = e / SVTME_PU_COUNT, pu = e - kk * SVTME_PU_COUNT;
+        const int s  = kk < job.num_refs[0] ? kk : 4 + (kk - job.num_refs[0]);
+        uint32_t sad = U32MAX, mv = 0;
+        if (st.searched[s]) {
+            const unsigned long long key = kb[e];
+            if (dj.parts > 1)
+                kb[e] = ~0ull; // keys rest at ~0 for the next banded job
+            const CSlot &v   = csl[s];
+            const uint32_t o = (uint32_t)key;
+            sad              = (uint32_t)(key >> 32);
+            int16_t mx, my;
+            if (v.probe && o == 0) {
+                mx = v.xc;
+                my = v.yc;
+            } else {
+                const int p = (int)o - (int)v.probe;
+                my          = i16(v.yo + p / v.w);
+                mx          = i16(v.xo + p % v.w);
+            }
+            mv = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
         }
+        st.best_sad[s][pu] = sad;
+        st.best_mv[s][pu]  = mv;
     }
-    if (dj.out_sb) {
-        __syncthreads();
-        
-        finish_sb(st, dj, sb_local, bw, bh);
-    }
-    STAMP(15);
+    __syncthreads();
+    stage_c_tail(st, dj, sb_local, G.bw, G.bh, vmask);
 }
 
 } // namespace svtme
@@ -1744,6 +2102,44 @@ extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t
     *count = n;
 }
 
+// Wide full-pel stage geometry, host-side and pure. The largest search area
+// integer_search_b64 can reach (me_sa max, x mv multiplier, x 3/2 variance
+// growth, rounded up to 8 columns) decides 32-bit argmin keys, and the number
+// of search-row bands per (SB, reference).
+static void fp_area_bound(const svtme_controls *c, uint32_t *w, uint32_t *h) {
+    // min(sa_min x distance, sa_max) (:1303-1304), x mv multiplier (:1305-1310),
+    // rounded up to 8 (:1318), then x 3/2 and rounded again by the variance
+    // growth (:1424-1427) when its threshold can be passed
+    uint32_t mw = c->me_sa.sa_max.width, mh = c->me_sa.sa_max.height;
+    if (c->mv_sa_adj_enabled) {
+        mw *= c->mv_sa_adj_sa_multiplier;
+        mh *= c->mv_sa_adj_sa_multiplier;
+    }
+    mw += 7;
+    mh = mh < 3 ? 3 : mh;
+    if (c->me_8x8_var_enabled && c->me_sr_mult2_th != 0xFFFFFFFFu) {
+        mw = mw * 3 / 2 + 7;
+        mh = mh * 3 / 2;
+    }
+    *w = mw;
+    *h = mh;
+}
+
+extern "C" bool svtme_fp_k32(const svtme_controls *c) {
+    uint32_t w, h;
+    fp_area_bound(c, &w, &h);
+    return 1u + w * h <= 4096u;
+}
+
+extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {
+    if (c->enable_me_sr_adjustment == 2)
+        return 0; // slot 0's 64x64 SAD feeds the other slots' areas: per-SB k_stage_c
+    uint32_t w, h;
+    fp_area_bound(c, &w, &h);
+    const uint32_t parts = (w * h) / 512;
+    return parts < 1 ? 1 : (parts > 16 ? 16 : parts);
+}
+
 // mid (optional): three events recorded after stages A, D and B
 extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid) {
     if (dj->ta_count) {
@@ -1764,7 +2160,21 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, h
     }
     if (mid)
         (void)hipEventRecord(mid[2], s);
-    if (dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH)
+    const bool full = dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
+    if (dj->parts) { // wide full-pel stage + per-SB decode
+        const uint32_t waves = sb_count * dj->R * dj->parts;
+        const dim3 grid((waves + 3) / 4);
+        const bool k32 = svtme_fp_k32(&dj->job.ctrl);
+        if (full && k32)
+            hipLaunchKernelGGL((svtme::k_stage_c1<false, true>), grid, dim3(256), 0, s, *dj);
+        else if (full)
+            hipLaunchKernelGGL((svtme::k_stage_c1<false, false>), grid, dim3(256), 0, s, *dj);
+        else if (k32)
+            hipLaunchKernelGGL((svtme::k_stage_c1<true, true>), grid, dim3(256), 0, s, *dj);
+        else
+            hipLaunchKernelGGL((svtme::k_stage_c1<true, false>), grid, dim3(256), 0, s, *dj);
+        hipLaunchKernelGGL(svtme::k_stage_e, dim3(sb_count), dim3(256), 0, s, *dj);
+    } else if (full)
         hipLaunchKernelGGL(svtme::k_stage_c<false>, dim3(sb_count), dim3(256), 0, s, *dj);
     else
         hipLaunchKernelGGL(svtme::k_stage_c<true>, dim3(sb_count), dim3(256), 0, s, *dj);

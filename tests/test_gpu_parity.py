@@ -108,18 +108,75 @@ def test_10bit_msb_parity(svtme, gpu):
         gpu.release(2000 + t)
 
 
-def test_mctf_job_fails_loudly(svtme, gpu):
-    """TF-ME jobs are checked on the CPU side (tests/test_oracle.py); this
-    build's kernels do not run them and must refuse rather than return
-    open-loop results."""
+MCTF_CASES = [  # content, w, h, tf hme_me_level, qp_opt, cur, ref, tl, tf_me_exit_th
+    ("pan", 320, 192, 0, 0, 8, 7, 1, 0),
+    ("pan", 320, 192, 1, 0, 8, 10, 1, 0),
+    ("pan", 640, 360, 2, 1, 8, 9, 0, 9800),
+    ("pan", 320, 192, 3, 0, 8, 7, 1, 2600),
+    ("noise", 192, 128, 3, 0, 8, 6, 2, 0),
+    ("flat", 192, 128, 4, 0, 8, 7, 1, 1),
+    ("stripes", 320, 192, 2, 0, 8, 9, 1, 50000),
+]
+
+
+@pytest.mark.parametrize("case", MCTF_CASES, ids=lambda c: f"{c[0]}-{c[1]}x{c[2]}-lvl{c[3]}-th{c[8]}")
+def test_mctf_parity(svtme, gpu, case):
+    """TF-ME jobs (me_type ME_MCTF) on the GPU == the oracle (pinned to the
+    reference by tests/golden/tf_cases.json)."""
     S = svtme
-    w, h = 128, 64
-    f = S.Synth(w, h)
-    for t in (7, 8):
-        gpu.upload(3000 + t, f.frame(t))
-    ctrl = S.derive_controls_tf(2, 0, 35, S.input_resolution_of(w, h))
-    job = S.make_job(w, h, ctrl, 3008, (3007,), (), ref_count_used=(1, 0), me_type=S.ME_MCTF)
-    with pytest.raises(RuntimeError):
-        gpu.submit(job)
-    for t in (7, 8):
-        gpu.release(3000 + t)
+    kind, w, h, lvl, qp_opt, cur, ref, tl, th = case
+    frames = S.test_frames(kind, w, h, [cur, ref])
+    ctrl = S.derive_controls_tf(lvl, qp_opt, 35, S.input_resolution_of(w, h))
+    for t, f in frames.items():
+        gpu.upload(4000 + t, f)
+    job = S.case_job(ctrl, w, h, 4000 + cur, (4000 + ref,), (), tl, me_type=S.ME_MCTF, tf_me_exit_th=th)
+    recs, sbr = gpu.submit(job)
+    pyr = {t: S.build_host_pyramid(f, "oracle") for t, f in frames.items()}
+    ojob = S.case_job(ctrl, w, h, cur, (ref,), (), tl, me_type=S.ME_MCTF, tf_me_exit_th=th)
+    orecs, osbr = S.run_checker(ojob, pyr[cur], {(0, 0): pyr[ref]}, "oracle", nthreads=8)
+    for t in frames:
+        gpu.release(4000 + t)
+    errs = S.compare_records(orecs, recs, osbr, sbr)
+    assert not errs, errs[:5]
+
+
+def _controls_case(S, gpu, ctrl, w, h, l0, l1, tl=1, kind="pan"):
+    frames = S.test_frames(kind, w, h, sorted(set([8] + list(l0) + list(l1))))
+    for t, f in frames.items():
+        gpu.upload(5000 + t, f)
+    job = S.case_job(ctrl, w, h, 5008, tuple(5000 + t for t in l0), tuple(5000 + t for t in l1), tl)
+    recs, sbr = gpu.submit(job)
+    pyr = {t: S.build_host_pyramid(f, "oracle") for t, f in frames.items()}
+    refs = {(0, i): pyr[t] for i, t in enumerate(l0)}
+    refs.update({(1, i): pyr[t] for i, t in enumerate(l1)})
+    orecs, osbr = S.run_checker(S.case_job(ctrl, w, h, 8, l0, l1, tl), pyr[8], refs, "oracle", nthreads=8)
+    for t in frames:
+        gpu.release(5000 + t)
+    return S.compare_records(orecs, recs, osbr, sbr)
+
+
+def test_sr_adjustment_level2_parity(svtme, gpu):
+    """enable_me_sr_adjustment == 2 (slot 0's 64x64 SAD resizes the other
+    slots' areas, motion_estimation.c:1355-1364): the per-SB full-pel kernel."""
+    S = svtme
+    ctrl = S.derive_controls(4, 35, S.input_resolution_of(640, 360), 1)
+    ctrl.enable_me_sr_adjustment = 2
+    assert not _controls_case(S, gpu, ctrl, 640, 360, (7, 6), (9,))
+
+
+def test_banded_fullpel_parity(svtme, gpu):
+    """A fixed 64 x 64 full-pel area (the 1080p bench override): the search
+    rows of every (SB, reference) are split over several wavefronts whose
+    argmin keys merge with atomic min; run twice to check the keys' reset."""
+    S = svtme
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(640, 360), 1)
+    ctrl.me_sa.sa_min.width = ctrl.me_sa.sa_min.height = 64
+    ctrl.me_sa.sa_max.width = ctrl.me_sa.sa_max.height = 64
+    ctrl.me_8x8_var_enabled = 0
+    ctrl.enable_me_sr_adjustment = 0
+    for _ in range(2):
+        assert not _controls_case(S, gpu, ctrl, 640, 360, (7,), ())
+    # then a single-band job, then banded again (keys left behind by plain stores)
+    assert not _controls_case(S, gpu, S.derive_controls(8, 35, S.input_resolution_of(640, 360), 1), 640, 360,
+                              (7, 6), (9, 10))
+    assert not _controls_case(S, gpu, ctrl, 640, 360, (7,), ())
