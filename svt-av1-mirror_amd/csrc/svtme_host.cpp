@@ -28,8 +28,6 @@ extern "C" hipError_t svtme_launch_build_full(const void *src, uint32_t src_stri
                                               DevPlane dst, int left, int top, int rows, hipStream_t s);
 extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int left, int top, int rows,
                                               hipStream_t s);
-extern "C" hipError_t svtme_launch_me(const DevJob *dj, uint32_t sb_count, hipStream_t s);
-extern "C" hipError_t svtme_launch_me2(const DevJob *dj, uint32_t sb_count, hipStream_t s);
 extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
@@ -92,12 +90,6 @@ struct svtme_ctx {
     bool timing         = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_mid[3] = {nullptr, nullptr, nullptr}; // after stages A, D, B
-    // SB-band parts of one job on side streams (stage kernels of different
-    // bands overlap on the device); fork/join events on the main stream
-    static constexpr int kMaxParts = 4;
-    int parts = 1;
-    hipStream_t side[kMaxParts] = {};
-    hipEvent_t ev_fork = nullptr, ev_join[kMaxParts] = {};
     ARes *d_ares    = nullptr; // stage-A results [count][SVTME_A_N]
     size_t ares_cap = 0;
     BState *d_bst   = nullptr; // stage-B state [count]
@@ -134,8 +126,6 @@ extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
     HIP_TRY(hipSetDevice(device));
     svtme_ctx *c = new svtme_ctx();
     c->device    = device;
-    if (const char *e = getenv("SVTME_PARTS"))
-        c->parts = std::max(1, std::min(svtme_ctx::kMaxParts, atoi(e)));
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -164,14 +154,6 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
     for (auto &e : c->ev_mid)
         if (e)
             (void)hipEventDestroy(e);
-    for (int k = 0; k < svtme_ctx::kMaxParts; k++) {
-        if (c->side[k])
-            (void)hipStreamDestroy(c->side[k]);
-        if (c->ev_join[k])
-            (void)hipEventDestroy(c->ev_join[k]);
-    }
-    if (c->ev_fork)
-        (void)hipEventDestroy(c->ev_fork);
 #ifdef SVTME_STAMPS
     if (c->stamp_n) {
         fprintf(stderr, "[svtme stamps] %llu SBs, mean cycles per phase (from previous stamp):",
@@ -464,44 +446,7 @@ static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_
     }
     svtme_stage_a_list(&dj.job, dj.ta_list, &dj.ta_count);
     svtme_stage_b_list(&dj.job, dj.tb_list, &dj.tb_count);
-    static const int kernel_version = [] {
-        const char *e = getenv("SVTME_KERNEL");
-        return e ? atoi(e + (e[0] == 'v')) : 3;
-    }();
-    if (kernel_version == 1)
-        HIP_TRY(svtme_launch_me(&dj, count, c->stream));
-    else if (kernel_version == 2)
-        HIP_TRY(svtme_launch_me2(&dj, count, c->stream));
-    else if (c->parts <= 1 || count < 2 * (uint32_t)c->parts)
-        HIP_TRY(svtme_launch_stages(&dj, count, c->stream, c->timing ? c->ev_mid : nullptr));
-    else {
-        const int parts = c->parts;
-        if (!c->ev_fork) {
-            HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-            for (int k = 0; k < parts; k++) {
-                HIP_TRY(hipStreamCreateWithFlags(&c->side[k], hipStreamNonBlocking));
-                HIP_TRY(hipEventCreateWithFlags(&c->ev_join[k], hipEventDisableTiming));
-            }
-        }
-        HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
-        for (int k = 0; k < parts; k++) {
-            const uint32_t b0 = (uint32_t)((uint64_t)count * k / parts), b1 = (uint32_t)((uint64_t)count * (k + 1) / parts);
-            DevJob djk       = dj;
-            djk.job.sb_begin = dj.job.sb_begin + b0;
-            djk.job.sb_count = b1 - b0;
-            djk.out_records  = dj.out_records + (size_t)b0 * dj.R;
-            djk.out_sb       = dj.out_sb ? dj.out_sb + b0 : nullptr;
-            djk.ares         = dj.ares + (size_t)b0 * SVTME_A_N;
-            djk.bst          = dj.bst + b0;
-            djk.keys         = dj.keys ? dj.keys + (size_t)b0 * dj.R * SVTME_PU_COUNT : nullptr;
-            djk.cslot        = dj.cslot ? dj.cslot + (size_t)b0 * dj.R : nullptr;
-            djk.stamps       = dj.stamps ? dj.stamps + (size_t)b0 * 16 : nullptr;
-            HIP_TRY(hipStreamWaitEvent(c->side[k], c->ev_fork, 0));
-            HIP_TRY(svtme_launch_stages(&djk, b1 - b0, c->side[k], nullptr));
-            HIP_TRY(hipEventRecord(c->ev_join[k], c->side[k]));
-            HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_join[k], 0));
-        }
-    }
+    HIP_TRY(svtme_launch_stages(&dj, count, c->stream, c->timing ? c->ev_mid : nullptr));
 #ifdef SVTME_STAMPS
     {
         std::vector<unsigned long long> h((size_t)count * 16);
@@ -561,8 +506,8 @@ extern "C" float svtme_kernel_ms(svtme_ctx *c) {
 }
 
 extern "C" float svtme_stage_ms(svtme_ctx *c, int stage) {
-    if (!c || !c->timing || stage < 0 || stage > 3 || !c->ev_mid[0] || c->parts > 1)
-        return -1.0f; // stages of concurrent parts overlap: no per-stage split
+    if (!c || !c->timing || stage < 0 || stage > 3 || !c->ev_mid[0])
+        return -1.0f;
     hipEvent_t a = stage == 0 ? c->ev0 : c->ev_mid[stage - 1];
     hipEvent_t b = stage == 3 ? c->ev1 : c->ev_mid[stage];
     float ms = -1.0f;

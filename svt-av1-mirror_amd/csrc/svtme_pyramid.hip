@@ -1,0 +1,84 @@
+// svtme_pyramid.hip — the padded three-level luma pyramid of one picture.
+//
+//   k_build_full<TEN_BIT> : full-resolution plane, pad-to-8 + edge replication
+//                           (10-bit input reduced to its MSB plane, enc_handle.c:4964-4972)
+//   k_build_down          : 1/4 and 1/16 planes, (a+b+c+d+2)>>2 of the level above
+//                           (svt_aom_downsample_2d_c, pic_analysis_process.c:130-158;
+//                            svt_aom_downsample_filtering_input_picture :1945-2002;
+//                            svt_aom_generate_padding, pic_operators.c:338-383)
+//
+// One thread writes one dword of the padded plane (margins included), so every
+// store is a full coalesced dword; margins are produced by clamping the source
+// coordinate, which is the reference's edge replication.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "svtme_device.h"
+
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// level 0: from the caller's picture (8-bit or 10-bit MSB), pad-to-8 + edge replicate.
+// One thread writes 4 bytes of the padded plane (margins included).
+template <bool TEN_BIT>
+__global__ void __launch_bounds__(256) k_build_full(const void *__restrict__ src, uint32_t src_stride, int w, int h,
+                                                    DevPlane dst, int left, int top, int rows) {
+    const int dw_per_row = dst.stride >> 2;
+    const int idx        = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= dw_per_row * rows)
+        return;
+    const int ry = idx / dw_per_row, rx4 = (idx - ry * dw_per_row) * 4;
+    const int y  = clampi(ry - top, 0, h - 1);
+    uint32_t v   = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int x = clampi(rx4 + k - left, 0, w - 1);
+        uint32_t p;
+        if (TEN_BIT)
+            p = (uint32_t)(((const uint16_t *)src)[(size_t)y * src_stride + x] >> 2);
+        else
+            p = ((const uint8_t *)src)[(size_t)y * src_stride + x];
+        v |= p << (8 * k);
+    }
+    uint32_t *row = (uint32_t *)(dst.base - (size_t)top * dst.stride - left);
+    row[idx]      = v;
+}
+
+// levels 1, 2: 2x2 mean (sum + 2) >> 2 of the previous level's interior, edge replicate
+__global__ void __launch_bounds__(256) k_build_down(DevPlane prev, DevPlane dst, int left, int top, int rows) {
+    const int dw_per_row = dst.stride >> 2;
+    const int idx        = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= dw_per_row * rows)
+        return;
+    const int ry = idx / dw_per_row, rx4 = (idx - ry * dw_per_row) * 4;
+    const int y  = clampi(ry - top, 0, dst.height - 1);
+    const uint8_t *a = prev.base + (size_t)(2 * y) * prev.stride;
+    const uint8_t *b = a + prev.stride;
+    uint32_t v       = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int x    = clampi(rx4 + k - left, 0, dst.width - 1);
+        const uint32_t s = (uint32_t)a[2 * x] + a[2 * x + 1] + b[2 * x] + b[2 * x + 1];
+        v |= ((s + 2) >> 2) << (8 * k);
+    }
+    uint32_t *row = (uint32_t *)(dst.base - (size_t)top * dst.stride - left);
+    row[idx]      = v;
+}
+
+extern "C" hipError_t svtme_launch_build_full(const void *src, uint32_t src_stride, int w, int h, int ten_bit,
+                                              DevPlane dst, int left, int top, int rows, hipStream_t s) {
+    const int n = (dst.stride >> 2) * rows;
+    if (ten_bit)
+        hipLaunchKernelGGL(k_build_full<true>, dim3((n + 255) / 256), dim3(256), 0, s, src, src_stride, w, h, dst,
+                           left, top, rows);
+    else
+        hipLaunchKernelGGL(k_build_full<false>, dim3((n + 255) / 256), dim3(256), 0, s, src, src_stride, w, h, dst,
+                           left, top, rows);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int left, int top, int rows,
+                                              hipStream_t s) {
+    const int n = (dst.stride >> 2) * rows;
+    hipLaunchKernelGGL(k_build_down, dim3((n + 255) / 256), dim3(256), 0, s, prev, dst, left, top, rows);
+    return hipGetLastError();
+}

@@ -6,10 +6,14 @@ Two ways to spread ME over ranks, neither needs a collective on the data path:
   whole pictures of its own; the only exchange is the optional all-gather of
   the per-SB records (the encoder's picture-level consumers, me_process.c:
   274-288, read every SB's results).
-* band-parallel (one picture split in SB-row bands): rank k runs SBs
-  [begin_k, begin_k + count_k) of the same picture (svtme_job.sb_begin /
+* band-parallel (one picture split in SB bands): rank k runs
+  SBs [begin_k, begin_k + count_k) of the same picture (svtme_job.sb_begin /
   sb_count) against the same resident references; the bands concatenate to
-  the whole picture's records, bit-identical to a single-rank run.
+  the whole picture's records, bit-identical to a single-rank run. On GPUs the
+  SB count is padded to equal chunks (sb_chunk) so one all_gather_into_tensor
+  over RCCL moves every rank's record slice straight between device buffers
+  (gather_chunks_device); this is the analogue of the reference's ME segments
+  -> SB ranges (enc_handle.c:393-412, me_process.c:146-157).
 
 `torch.distributed` is plumbing here (RCCL on GPUs, gloo for the CPU tests).
 """
@@ -22,6 +26,39 @@ def sb_band(n_sb: int, rank: int, world: int):
     q, r = divmod(n_sb, world)
     begin = rank * q + min(rank, r)
     return begin, q + (1 if rank < r else 0)
+
+
+def sb_chunk(n_sb: int, rank: int, world: int):
+    """Equal-chunk band of `rank`: chunk = ceil(n_sb / world) SBs, the last
+    rank(s) short (count may be 0). Every rank's slice of the gathered buffer
+    has the same size, so the exchange is a single all-gather."""
+    chunk = -(-n_sb // world)
+    begin = min(rank * chunk, n_sb)
+    return begin, max(0, min(chunk, n_sb - begin))
+
+
+def chunk_slots(n_sb: int, world: int) -> int:
+    """SB slots per rank in the padded all-gather buffer."""
+    return -(-n_sb // world)
+
+
+def gather_chunks_device(d_local, d_out, dist, group=None, stream=None):
+    """All-gather the ranks' record chunks between device buffers.
+
+    d_local: uint8 tensor of chunk_slots x R x record bytes (this rank's
+    records, written by svtme_submit_picture_device; a short last chunk leaves
+    its tail unused); d_out: uint8 tensor world x that size. Row-major SB
+    order of the picture is d_out[:n_sb * R * record bytes]. With RCCL
+    the copy runs on `stream` (the ME library's stream, so it is ordered after
+    the ME kernels without a host sync)."""
+    import torch
+
+    if stream is not None:
+        with torch.cuda.stream(stream):
+            dist.all_gather_into_tensor(d_out, d_local, group=group)
+    else:
+        dist.all_gather_into_tensor(d_out, d_local, group=group)
+    return d_out
 
 
 def gather_band_records(local: np.ndarray, n_sb: int, dist, group=None) -> np.ndarray:
@@ -37,9 +74,11 @@ def gather_band_records(local: np.ndarray, n_sb: int, dist, group=None) -> np.nd
     buf = np.zeros((maxc, R), local.dtype)
     buf[: local.shape[0]] = local
     t = torch.from_numpy(buf.view(np.uint8).reshape(-1).copy())
+    if dist.get_backend(group) == "nccl":  # RCCL moves device tensors only
+        t = t.cuda()
     out = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(out, t, group=group)
-    parts = [o.numpy().view(local.dtype).reshape(maxc, R)[:c] for o, c in zip(out, counts)]
+    parts = [o.cpu().numpy().view(local.dtype).reshape(maxc, R)[:c] for o, c in zip(out, counts)]
     res = np.concatenate(parts, axis=0)
     assert res.shape[0] == n_sb and res.dtype.itemsize == itemsize
     return res

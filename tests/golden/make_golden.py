@@ -17,9 +17,15 @@ stores inputs-as-parameters plus expected outputs:
                      hme_me_level x qp_opt x QP x resolution
   tf_cases.json      temporal-filtering ME cases (me_type ME_MCTF: one list,
                      one reference, HME-only exits) -> me_tf_<name>.npz
+  configs.json       the BASELINE.json configurations at full size
+                     (svt-av1-mirror_amd/workloads.py): record/SB-result checksums
+                     of the whole picture plus every STRIDE-th SB's records in
+                     cfg_<name>.npz; configs[0] (640x360 p12, 30 pictures random
+                     access) as per-picture checksums and full records
 
 Run from the repo root in the build container (needs /root/reference for the
-library build only): python tests/golden/make_golden.py [tf]   (tf: TF fixtures only)
+library build only): python tests/golden/make_golden.py [tf|configs]
+(tf / configs: only those fixtures)
 """
 import hashlib
 import json
@@ -143,6 +149,63 @@ def tf_golden():
         json.dump(meta, fh, indent=1)
 
 
+CFG_STRIDE = 7  # sampled SBs of the full-size configurations (every 7th SB: all rows and columns)
+
+
+def configs_golden():
+    """Full-size BASELINE.json configurations through the reference's own ME
+    (AVX2 kernels, as the encoder runs at --asm avx2; the C kernels must agree
+    on the sampled SBs of every configuration)."""
+    import workloads as W
+
+    ref = S.load_ref()
+    meta = {"stride": CFG_STRIDE, "configs": {}, "ra360_p12": []}
+    for name in ("1080p_sa64", "4k_p8", "4k10_p6", "8k_p8"):
+        wl = W.WORKLOADS[name]
+        frames = W.workload_frames(name)
+        pyr = {t: S.build_host_pyramid(f, "ref") for t, f in frames.items()}
+        refs = {(0, i): pyr[t] for i, t in enumerate(wl["l0"])}
+        refs.update({(1, i): pyr[t] for i, t in enumerate(wl["l1"])})
+        job = W.workload_job(name)
+        ref.svtref_set_simd(1)
+        recs, sbr = S.run_checker(job, pyr[8], refs, "ref", nthreads=8)
+        # C kernels on the sampled SBs (one band job per sample keeps the C run short)
+        ref.svtref_set_simd(0)
+        n = len(recs)
+        for b in range(0, n, CFG_STRIDE * 16):
+            cj = W.workload_job(name, sb_begin=b, sb_count=1)
+            crec, csb = S.run_checker(cj, pyr[8], refs, "ref", nthreads=1)
+            assert not S.compare_records(recs[b:b + 1], crec, sbr[b:b + 1], csb), (name, b)
+        ref.svtref_set_simd(1)
+        np.savez_compressed(os.path.join(HERE, f"cfg_{name}.npz"),
+                            records=np.ascontiguousarray(recs[::CFG_STRIDE]).view(np.uint8).reshape(-1, recs.shape[1] * recs.itemsize),
+                            sb=np.ascontiguousarray(sbr[::CFG_STRIDE]).view(np.uint8).reshape(-1, sbr.itemsize))
+        meta["configs"][name] = {"sbs": n, "refs": int(recs.shape[1]), "checksum": S.records_checksum(recs, sbr),
+                                 "searched": int(recs["searched"].sum()), "desc": wl["desc"],
+                                 "pyramid_sha256": digest(pyr[8].full)}
+        print(name, recs.shape, meta["configs"][name]["checksum"][:16], flush=True)
+    # configs[0]: 640x360 preset 12, 30 pictures random access
+    w, h = 640, 360
+    syn = S.Synth(w, h)
+    frames = {t: syn.frame(t) for t in range(30)}
+    pyr = {t: S.build_host_pyramid(f, "ref") for t, f in frames.items()}
+    all_recs, all_sb = [], []
+    for t, tl, l0, l1 in W.ra_sequence(30):
+        ctrl = S.ref_derive_controls(12, 35, S.input_resolution_of(w, h), tl)
+        job = S.case_job(ctrl, w, h, t, l0, l1, tl)
+        refs = {(0, i): pyr[u] for i, u in enumerate(l0)}
+        refs.update({(1, i): pyr[u] for i, u in enumerate(l1)})
+        recs, sbr = S.run_checker(job, pyr[t], refs, "ref", nthreads=8)
+        meta["ra360_p12"].append({"picture": t, "tl": tl, "l0": list(l0), "l1": list(l1),
+                                  "checksum": S.records_checksum(recs, sbr)})
+        all_recs.append(recs.view(np.uint8).reshape(-1))
+        all_sb.append(sbr.view(np.uint8).reshape(-1))
+    np.savez_compressed(os.path.join(HERE, "cfg_ra360_p12.npz"), records=np.concatenate(all_recs),
+                        sb=np.concatenate(all_sb))
+    with open(os.path.join(HERE, "configs.json"), "w") as fh:
+        json.dump(meta, fh, indent=1)
+
+
 def main():
     ref = S.load_ref()
     rtcd_golden()
@@ -170,6 +233,10 @@ def main():
 
 
 if __name__ == "__main__":
-    if sys.argv[1:] != ["tf"]:
-        main()
-    tf_golden()
+    if sys.argv[1:] == ["configs"]:
+        configs_golden()
+    else:
+        if sys.argv[1:] != ["tf"]:
+            main()
+        tf_golden()
+        configs_golden()

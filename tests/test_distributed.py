@@ -67,3 +67,73 @@ def test_band_parallel_equals_single_rank(svtme, tmp_path):
     ctrl = S.derive_controls(8, 35, S.input_resolution_of(320, 192), 1)
     ref, _ = S.run_case_checker("pan", 320, 192, ctrl, 8, (7, 6), (9, 10), 1, checker="oracle", nthreads=2)
     assert not S.compare_records(ref, full)
+
+
+def _chunk_worker(rank, world, port, out_path, n_pics):
+    """bench.py --mode band's exchange on CPU: every rank searches its equal
+    SB chunk of each of n_pics pictures, writes the records into its slice of
+    a padded byte buffer and one all_gather_into_tensor per picture assembles
+    every picture on every rank (RCCL moves device buffers the same way)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "svt-av1-mirror_amd"))
+    import torch
+    import torch.distributed as dist
+
+    import svtme as S
+    import svtme_dist as D
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w, h = 200, 136  # 4 x 3 = 12 SBs: chunks of 6 at world 2 (5 + pad at world 3 would be short)
+    n_sb = S.sb_total(w, h)
+    slots = D.chunk_slots(n_sb, world)
+    outs = []
+    for p in range(n_pics):
+        ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+        begin, count = D.sb_chunk(n_sb, rank, world)
+        R = 3
+        rec_bytes = S.REF_RECORD_DTYPE.itemsize * R
+        local = torch.zeros(slots * rec_bytes, dtype=torch.uint8)
+        if count:
+            recs, _ = S.run_case_checker("pan", w, h, ctrl, 8 + p, (7 + p, 6 + p), (9 + p,), 1, checker="oracle",
+                                         nthreads=1, sb_begin=begin, sb_count=count)
+            local[: count * rec_bytes] = torch.from_numpy(recs.view(np.uint8).reshape(-1).copy())
+        out = torch.empty(world * slots * rec_bytes, dtype=torch.uint8)
+        D.gather_chunks_device(local, out, dist)
+        outs.append(out[: n_sb * rec_bytes].numpy().copy())
+    if rank == 0:
+        np.save(out_path, np.stack(outs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_chunked_allgather_equals_single_rank(svtme, tmp_path, world):
+    S = svtme
+    out = str(tmp_path / "chunks.npy")
+    mp.spawn(_chunk_worker, args=(world, _free_port(), out, 2), nprocs=world, join=True)
+    got = np.load(out)
+    w, h = 200, 136
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    for p in range(2):
+        ref, _ = S.run_case_checker("pan", w, h, ctrl, 8 + p, (7 + p, 6 + p), (9 + p,), 1, checker="oracle",
+                                    nthreads=2)
+        full = got[p].view(S.REF_RECORD_DTYPE).reshape(ref.shape)
+        assert not S.compare_records(ref, full)
+
+
+def test_sb_chunk_padding():
+    import svtme_dist as D
+
+    for n in (1, 7, 12, 510, 2040, 8160):
+        for world in (1, 2, 3, 4, 8):
+            slots = D.chunk_slots(n, world)
+            cov = []
+            for k in range(world):
+                b, c = D.sb_chunk(n, k, world)
+                assert 0 <= c <= slots and b == min(k * slots, n)
+                cov.extend(range(b, b + c))
+            assert cov == list(range(n))
