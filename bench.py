@@ -1,25 +1,41 @@
 """bench.py — open-loop ME throughput on MI355X (BASELINE.json metric).
 
-One step = one picture-level ME job (svtme_submit_picture_device): every 64x64
-superblock (SB) of a 3840x2160 8-bit picture searched against 4 references
-(L0: distance 1, 2; L1: distance 1, 2) with the preset-8 controls
-(BASELINE.json configs[2], the headline "4K preset-8" configuration). The
-references' and the current picture's padded pyramids are resident in HBM
-before the timed region (the PA stage builds them once per picture).
+Workload (default): BASELINE.json configs[2], the metric's "4K preset-8": every
+64x64 superblock (SB) of a 3840x2160 8-bit picture searched against 4
+references (L0 distance 1, 2; L1 distance 1, 2) with the preset-8 controls of
+svt_aom_sig_deriv_me. Pyramids of the pictures and their references are
+resident in HBM before the timed region (the PA stage builds them once per
+picture). --workload picks another BASELINE config (svt-av1-mirror_amd/workloads.py).
 
---gpus N (launched with torch.distributed.run): one process per GPU; every rank
-runs its own picture job (weak scaling: per-GPU work fixed) and the per-SB
-records of all ranks are then all-gathered over RCCL (the picture-level exchange
-the encoder's cross-SB consumers need, me_process.c:274-288). value = SBs of
-all ranks / max-over-ranks time.
+One step, on N GPUs (one process per GPU, torch.distributed over RCCL): N
+pictures, each split into N equal SB chunks (SBs are
+independent given the picture controls); rank r searches chunk r of every
+picture in ONE batched launch per stage (svtme_submit_batch_device), then the
+ranks all-gather their record chunks over RCCL (one all_gather_into_tensor per
+step, device buffers, on a communication stream overlapped with the next
+step's ME). Per-GPU work is one picture's worth of SBs at every N: "scaling"
+is weak; at N = 1 the step is exactly one picture job. value = SBs of all N
+pictures / max-over-ranks time.
 
-Also reported: the dominant kernel's roofline (k_me_sb: SURVEY.md 8(d)
-algorithmic bytes per SB x SBs per launch / HIP-event kernel time on the
-library's stream), and the reference's own AVX2 ME (oracle/_ref, compiled from
-the reference sources) timed on this host's cores on a bounded sample.
+roofline: the ME pass (the five stage kernels, back to back on the library's
+stream) — algorithmic bytes per pass (bytes/SB x SBs per
+launch) / the pass's average device time, from two HIP events recorded on
+that stream around the timed region. Every stage kernel is listed with its
+own duration (start/stop events attached to its dispatch packets,
+hipExtLaunchKernelGGL, over --kernel-samples further steps; the rocprofv3
+kernel trace under profiles/ agrees) and, at p8, its own byte share;
+`traffic` = HBM bytes per pass from this round's rocprofv3 FETCH_SIZE (x2,
+gfx950) + WRITE_SIZE passes, committed under profiles/ (scripts/gpu_profile.sh).
+
+cpu_baseline: the reference's own ME (motion_estimation.c + its AVX2 kernels,
+compiled from the reference sources into oracle/_ref) on this host's cores
+(every CPU this process may use: affinity and cgroup quota), on a bounded
+sample of whole-picture passes of the same job, rank 0 at N = 1 only.
 """
 import argparse
+import glob
 import json
+import math
 import os
 import sys
 import time
@@ -30,43 +46,51 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
 
 METRIC = "open-loop ME 64x64 superblocks/sec + achieved HBM GB/s, 4K preset-8"
-HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-
-# bytes/SB = src 2688 + R x (ref windows + 680 output), nominal windows
-WINDOW_BYTES = {"p8": 16798, "p6": 38121, "p8_sa64": 28241}
-# the same bytes split over the three stage kernels (p8 stage breakdown of SURVEY.md 8(d):
-# zz 2048 + pre-HME 2645 + 1034 + HME-L0 1081 | HME-L1 5304 | full-pel 4686 + 680 out;
-# source 64x32 + 16x8 in stage A, 32x16 in stage B)
-# (stage D only reads stage A's 448-B result block per SB: no window bytes)
-STAGE_BYTES = {"p8": ((2176, 6808), (0, 0), (512, 5304), (0, 4686 + 680))}
-STAGE_NAMES = ("k_stage_a", "k_stage_d", "k_stage_b", "k_stage_c1+k_stage_e")
-
-WORKLOADS = {
-    "4k_p8": dict(w=3840, h=2160, mode=8, tl=1, l0=(7, 6), l1=(9, 10), windows="p8", ten_bit=False,
-                  desc="3840x2160 8-bit preset 8, 4 refs (L0 d=1,2; L1 d=1,2), open-loop ME"),
-    "1080p_p8": dict(w=1920, h=1080, mode=8, tl=1, l0=(7,), l1=(), windows="p8_sa64", ten_bit=False, sa64=True,
-                     desc="1920x1080 8-bit preset 8, 1 ref (L0 d=1), ME area override 64x64 "
-                          "(8x8-variance resize and sr-adjust off: 4096 positions/SB), open-loop ME"),
-    "4k10_p6": dict(w=3840, h=2160, mode=6, tl=1, l0=(7,), l1=(9,), windows="p6", ten_bit=True,
-                    desc="3840x2160 10-bit preset 6 (8-bit MSB search), 2 refs, open-loop ME"),
-    "8k_p8": dict(w=7680, h=4320, mode=8, tl=1, l0=(7, 6), l1=(9, 10), windows="p8", ten_bit=False,
-                  desc="7680x4320 8-bit preset 8, 4 refs, open-loop ME"),
-}
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
+# v_sad_u8: 4 absdiffs per lane, 64 lanes per CU per clock, 256 CUs, 2.4 GHz
+SAD_PEAK_T = 4 * 64 * 256 * 2.4e9 / 1e12
+STAGES = ("k_stage_a", "k_stage_d", "k_stage_b", "k_stage_c1", "k_stage_e")
+# SURVEY.md 8(d) p8 byte split over the stage kernels: zz 2048 + pre-HME 2645 + 1034 +
+# HME-L0 1081 (+ source 64x32 + 16x8) | HME-L1 5304 (+ source 32x16) | full-pel 4686 + 680 out
+STAGE_BYTES_P8 = {"k_stage_a": (2176, 6808), "k_stage_d": (0, 0), "k_stage_b": (512, 5304),
+                  "k_stage_c1": (0, 4686), "k_stage_e": (0, 680)}
+PICTURE_STRIDE = 32  # picture p of a step pans from t = 8 + 32 p (distinct content per picture)
 
 
-def bytes_per_sb(windows: str, refs: int) -> int:
-    return 2688 + refs * (WINDOW_BYTES[windows] + 680)
+def host_cores():
+    """CPUs this process may run on: affinity, capped by the cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def latest_profile(workload):
+    """pmc_summary.json of the newest profiles/r*_<workload>/ (this round's code)."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}", "pmc_summary.json")))
+    if not paths:
+        return None, None
+    with open(paths[-1]) as fh:
+        return json.load(fh), os.path.relpath(paths[-1], ROOT)
 
 
 def main():
+    import workloads as W
+
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="4k_p8", choices=sorted(WORKLOADS))
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", default="4k_p8", choices=sorted(W.WORKLOADS))
+    ap.add_argument("--pictures", type=int, default=0, help="pictures per step (default: one per GPU)")
+    ap.add_argument("--kernel-samples", type=int, default=20, help="steps timed per kernel after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-seconds of the baseline sample")
-    ap.add_argument("--kernel-samples", type=int, default=10)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="target CPU-seconds of the baseline sample")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -75,111 +99,128 @@ def main():
 
     import torch
 
+    torch.cuda.set_device(local_rank)
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     import svtme as S
+    import svtme_dist as D
 
-    wl = WORKLOADS[args.workload]
-    W, H = wl["w"], wl["h"]
-    syn = S.Synth(W, H)
-    ts = sorted(set((8,) + tuple(wl["l0"]) + tuple(wl["l1"])))
-    frames = {t: (syn.frame10(t) if wl["ten_bit"] else syn.frame(t)) for t in ts}
+    name = args.workload
+    wl = W.WORKLOADS[name]
+    Wd, Ht = wl["w"], wl["h"]
+    P = args.pictures or world
+    n_sb = S.sb_total(Wd, Ht)
+    slots = D.chunk_slots(n_sb, world)
+    begin, count = D.sb_chunk(n_sb, rank, world)
 
     gpu = S.GpuME(local_rank)
-    base = 100 * rank  # each rank owns its own picture (weak scaling)
-    for t, f in frames.items():
-        gpu.upload(base + t, f)
-    res = S.input_resolution_of(W, H)
-    ctrl = S.derive_controls(wl["mode"], 35, res, wl["tl"])
-    if wl.get("sa64"):  # fixed 64x64 full-pel area
-        ctrl.me_sa.sa_min.width = ctrl.me_sa.sa_min.height = 64
-        ctrl.me_sa.sa_max.width = ctrl.me_sa.sa_max.height = 64
-        ctrl.me_8x8_var_enabled = 0
-        ctrl.enable_me_sr_adjustment = 0
-    job = S.make_job(W, H, ctrl, base + 8, [base + t for t in wl["l0"]], [base + t for t in wl["l1"]],
-                     temporal_layer_index=wl["tl"], enable_me_8x8=(res <= S.RES_720P), ref_count_used=(3, 2))
-    R = S.ref_slots(job)
-    n_sb = S.sb_total(job.width, job.height)
-    rec_bytes = n_sb * R * S.REF_RECORD_DTYPE.itemsize
-    sb_bytes = n_sb * S.SB_RESULT_DTYPE.itemsize
+    syn = S.Synth(Wd, Ht)
+    offs = sorted(set((0,) + tuple(t - 8 for t in wl["l0"]) + tuple(t - 8 for t in wl["l1"])))
+    jobs = []
+    for p in range(P):
+        t0 = 8 + PICTURE_STRIDE * p
+        for o in offs:
+            t = t0 + o
+            gpu.upload(t, syn.frame10(t) if wl["ten_bit"] else syn.frame(t))
+        job = W.workload_job(name, base=PICTURE_STRIDE * p, sb_begin=begin, sb_count=count)
+        jobs.append(job)
+    R = S.ref_slots(jobs[0])
+    rec = S.REF_RECORD_DTYPE.itemsize
+    chunk_bytes = slots * R * rec
     dev = torch.device("cuda", local_rank)
-    d_rec = torch.empty(rec_bytes, dtype=torch.uint8, device=dev)
-    d_sb = torch.empty(sb_bytes, dtype=torch.uint8, device=dev)
-    gathered = torch.empty(rec_bytes * world, dtype=torch.uint8, device=dev) if world > 1 else None
+    local = [torch.zeros(P * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+    gathered = [torch.empty(world * P * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)] \
+        if world > 1 else None
     ext = torch.cuda.ExternalStream(gpu.stream(), device=dev)
+    comm = torch.cuda.Stream(device=dev) if world > 1 else None
+    me_done = [torch.cuda.Event() for _ in range(2)]
+    g_done = [torch.cuda.Event() for _ in range(2)]
+    used = [False, False]
 
-    def step():
-        gpu.submit_device(job, d_rec.data_ptr(), d_sb.data_ptr())
+    def step(i):
+        b = i & 1
+        if used[b] and world > 1:
+            ext.wait_event(g_done[b])  # the gather of step i-2 has read local[b]
+        gpu.submit_batch_device(jobs, [local[b].data_ptr() + p * chunk_bytes for p in range(P)])
         if world > 1:
-            with torch.cuda.stream(ext):
-                dist.all_gather_into_tensor(gathered, d_rec)
+            me_done[b].record(ext)
+            comm.wait_event(me_done[b])
+            D.gather_chunks_device(local[b], gathered[b], dist, stream=comm)
+            g_done[b].record(comm)
+        used[b] = True
 
-    for _ in range(args.warmup):
-        step()
-    gpu.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    def fence():
+        gpu.sync()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    fence()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    gpu.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    ev0.record(ext)
+    for i in range(args.steps):
+        step(args.warmup + i)
+    ev1.record(ext)
+    fence()
     elapsed = time.perf_counter() - t0
+    device_ms = ev0.elapsed_time(ev1) / args.steps  # the library stream's time per step (HIP events)
+    # per-kernel durations: start/stop events attached to the stage dispatches
+    # themselves (hipExtLaunchKernelGGL) over a sample of further steps
+    gpu.set_timing(True)
+    for i in range(args.kernel_samples):
+        step(args.warmup + args.steps + i)
+    fence()
+    gpu.set_timing(False)
+    n_timed, stage_ms = gpu.timing_read()
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed / args.steps * 1e3
-    value = n_sb * world * args.steps / elapsed
+    value = n_sb * P * args.steps / elapsed
 
-    # dominant kernel: k_me_sb timed with HIP events on the library's stream
-    gpu.set_timing(True)
-    kms, sms = [], []
-    for _ in range(args.kernel_samples):
-        gpu.submit_device(job, d_rec.data_ptr(), d_sb.data_ptr())
-        kms.append(gpu.kernel_ms())
-        sms.append([gpu.stage_ms(i) for i in range(len(STAGE_NAMES))])
-    gpu.set_timing(False)
-    k_avg_ms = float(np.mean(kms))
-    s_avg_ms = np.mean(np.array(sms), axis=0)
-    bps = bytes_per_sb(wl["windows"], R)
-    achieved = bps * n_sb / (k_avg_ms * 1e-3) / 1e9
+    # roofline of the ME pass on this rank (one batched launch per stage)
+    sbs_launch = count * P
+    bps = W.bytes_per_sb(wl["windows"], R)
+    kern_ms = float(sum(stage_ms))
+    bytes_launch = bps * sbs_launch
+    achieved = bytes_launch / (device_ms * 1e-3) / 1e9
     stages = {}
-    for i, name in enumerate(STAGE_NAMES):
-        if s_avg_ms[i] <= 0:  # concurrent SB-band parts: no per-stage split
+    for k, st in enumerate(STAGES):
+        if stage_ms[k] <= 0:
             continue
-        st = {"avg_ms": round(float(s_avg_ms[i]), 4)}
-        if wl["windows"] in STAGE_BYTES:
-            src_b, per_ref = STAGE_BYTES[wl["windows"]][i]
-            b = (src_b + R * per_ref) * n_sb
-            if b:
-                st["bytes_per_launch"] = b
-                st["achieved_gbps"] = round(b / (float(s_avg_ms[i]) * 1e-3) / 1e9, 1)
-        stages[name] = st
+        e = {"avg_ms": round(stage_ms[k], 4), "share": round(stage_ms[k] / kern_ms, 3)}
+        if wl["windows"] == "p8":
+            src_b, per_ref = STAGE_BYTES_P8[st]
+            sb_b = (src_b + R * per_ref) * sbs_launch
+            if sb_b:
+                e["bytes_per_launch"] = sb_b
+                e["achieved_gbps"] = round(sb_b / (stage_ms[k] * 1e-3) / 1e9, 1)
+                e["frac"] = round(e["achieved_gbps"] / HBM_PEAK_GBPS, 4)
+        stages[st] = e
+    dom = max(stages, key=lambda s: stages[s]["avg_ms"]) if stages else None
+    prof, prof_path = latest_profile(name)
     traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
-    if os.path.exists(pmc_path):
-        with open(pmc_path) as fh:
-            traffic = json.load(fh).get("hbm_bytes_per_launch")
+    if prof and prof.get("hbm_bytes_per_launch") and prof.get("sbs_per_launch") == sbs_launch:
+        traffic = int(prof["hbm_bytes_per_launch"])
+    absdiff = W.ABSDIFF_PER_SB_REF[wl["windows"]] * R * sbs_launch
+    sad_rate = absdiff / (device_ms * 1e-3) / 1e12
 
-    # parity of this run's records against the CPU checker (same picture)
-    recs = np.frombuffer(d_rec.cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n_sb, R)
-    cpu_baseline = None
-    parity = None
+    recs = None
+    if world == 1:
+        gpu.sync()
+        recs = np.frombuffer(local[0][:chunk_bytes].cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n_sb, R)
+    cpu_baseline = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_baseline, parity = cpu_leg(S, wl, job, frames, recs, args.cpu_seconds)
+        cpu_baseline, parity = cpu_leg(S, W, name, recs, args.cpu_seconds)
 
     if rank == 0:
         out = {
@@ -195,15 +236,23 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (integer PCG32 panning texture, SURVEY.md 8(d)); pyramids resident in HBM",
-            "config": {"workload": wl["desc"], "sbs_per_picture": n_sb, "refs": R,
-                       "parallelism": f"one picture job per GPU x {world}, RCCL all-gather of SB records"},
+            "config": {"workload": wl["desc"], "name": name, "sbs_per_picture": n_sb, "refs": R,
+                       "pictures_per_step": P,
+                       "parallelism": f"{world} GPU(s): each picture split in {world} equal SB chunks, "
+                                      f"rank r searches chunk r of all {P} pictures in one batched launch per "
+                                      f"stage" + (", RCCL all-gather of the record chunks" if world > 1 else "")},
             "sb_ref_per_s": round(value * R, 1),
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "ME pass = k_stage_a + k_stage_d + k_stage_b + k_stage_c1 + k_stage_e (one picture job)",
-                         "kernel_avg_ms": round(k_avg_ms, 4), "bytes_per_launch": bps * n_sb,
-                         "stages": stages},
+                         "kernel": "ME pass: k_stage_a -> k_stage_d -> k_stage_b -> k_stage_c1 -> k_stage_e "
+                                   "(one launch each, back to back on the library stream)",
+                         "pass_ms": round(device_ms, 4), "kernel_sum_ms": round(kern_ms, 4),
+                         "kernel_samples": n_timed,
+                         "bytes_per_launch": bytes_launch, "sbs_per_launch": sbs_launch,
+                         "dominant": dom, "stages": stages, "traffic_source": prof_path,
+                         "valu_sad": {"achieved_T_absdiff_s": round(sad_rate, 2), "peak": SAD_PEAK_T,
+                                      "frac": round(sad_rate / SAD_PEAK_T, 4)}},
             "cpu_baseline": cpu_baseline,
             "parity_vs_cpu": parity,
         }
@@ -213,35 +262,32 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_leg(S, wl, job, frames, gpu_recs, cpu_seconds):
+def cpu_leg(S, W, name, gpu_recs, cpu_seconds):
     """The reference's own ME (motion_estimation.c + its AVX2 kernels, compiled
-    from source into oracle/_ref) on this host, AVX2 capped as --asm avx2."""
+    from source into oracle/_ref) on this host, whole-picture passes of the same
+    job; the C restatement (oracle) when oracle/_ref is absent."""
     kind = "reference"
     try:
         S.load_ref().svtref_set_simd(1)
         checker = "ref"
     except Exception:
         kind, checker = "port", "oracle"
-    threads = min(16, os.cpu_count() or 1)
+    wl = W.WORKLOADS[name]
+    threads = host_cores()
+    frames = W.workload_frames(name)
     pyr = {t: S.build_host_pyramid(f, "oracle") for t, f in frames.items()}
-    refs = {}
-    for i, t in enumerate(wl["l0"]):
-        refs[(0, i)] = pyr[t]
-    for i, t in enumerate(wl["l1"]):
-        refs[(1, i)] = pyr[t]
-    cjob = S.make_job(wl["w"], wl["h"], job.ctrl, 8, wl["l0"], wl["l1"], temporal_layer_index=wl["tl"],
-                      enable_me_8x8=bool(job.enable_me_8x8), ref_count_used=(3, 2))
-    n_sb = S.sb_total(cjob.width, cjob.height)
-    # first pass: parity + calibration
+    refs = {(0, i): pyr[t] for i, t in enumerate(wl["l0"])}
+    refs.update({(1, i): pyr[t] for i, t in enumerate(wl["l1"])})
+    job = W.workload_job(name)
+    n_sb = S.sb_total(job.width, job.height)
     t0 = time.perf_counter()
-    recs, _ = S.run_checker(cjob, pyr[8], refs, checker, nthreads=threads, with_sb_results=False)
+    recs, _ = S.run_checker(job, pyr[8], refs, checker, nthreads=threads, with_sb_results=False)
     first = time.perf_counter() - t0
     parity = not S.compare_records(recs, gpu_recs)
-    # bounded sample: repeat whole-picture passes up to ~cpu_seconds of CPU time
-    reps = max(1, int(cpu_seconds / max(first * threads, 1e-3)))
+    reps = max(1, int(cpu_seconds / max(first * threads, 1e-4)))
     t0 = time.perf_counter()
     for _ in range(reps):
-        S.run_checker(cjob, pyr[8], refs, checker, nthreads=threads, with_sb_results=False)
+        S.run_checker(job, pyr[8], refs, checker, nthreads=threads, with_sb_results=False)
     el = time.perf_counter() - t0
     cpu_model = "unknown"
     try:
@@ -253,8 +299,10 @@ def cpu_leg(S, wl, job, frames, gpu_recs, cpu_seconds):
     except OSError:
         pass
     return ({"value": round(n_sb * reps / el, 1), "unit": "SB/s", "cores": threads, "kind": kind,
-             "sample": f"{reps} pass(es) over the full picture ({n_sb} SBs x {S.ref_slots(cjob)} refs), "
-                       f"{threads} threads, {'reference AVX2 kernels' if kind == 'reference' else 'C restatement'}, "
+             "sample": f"{reps} pass(es) over the full picture ({n_sb} SBs x {S.ref_slots(job)} refs), one SB "
+                       f"per task on {threads} threads (all CPUs this process may use: affinity "
+                       f"{len(os.sched_getaffinity(0))}, cgroup quota), "
+                       f"{'reference AVX2 kernels' if kind == 'reference' else 'C restatement'}, "
                        f"{el:.2f} s wall, CPU: {cpu_model}"}, parity)
 
 

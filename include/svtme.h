@@ -238,6 +238,14 @@ svtme_status svtme_picture_upload_10bit(svtme_ctx *ctx, uint64_t picture_number,
 svtme_status svtme_picture_upload_device(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *d_y,
                                          uint32_t stride, uint32_t width, uint32_t height);
 svtme_status svtme_picture_release(svtme_ctx *ctx, uint64_t picture_number);
+/* The resident picture's source planes were replaced (temporal filtering
+ * re-decimates the filtered picture, temporal_filtering.c:3895-3931
+ * pad_and_decimate_filtered_pic): rebuild its pyramid from the new 8-bit
+ * plane. Ordered after every job already submitted on the context (those read
+ * the old planes), before every later one. Fails if the picture is not
+ * resident (a stale pyramid is never silently kept). */
+svtme_status svtme_picture_invalidate(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *y, uint32_t stride,
+                                      uint32_t width, uint32_t height);
 /* Copy a resident pyramid level back to host (level 0 = full, 1 = quarter,
  * 2 = sixteenth), padding included: dst gets (h + 2 pad) rows of `stride` bytes. */
 svtme_status svtme_picture_download(svtme_ctx *ctx, uint64_t picture_number, int level, uint8_t *dst,
@@ -258,14 +266,26 @@ svtme_status svtme_fetch(svtme_ctx *ctx, svtme_ref_record *ref_records, svtme_sb
  * when d_sb_results is not NULL. */
 svtme_status svtme_submit_picture_device(svtme_ctx *ctx, const svtme_job *job, svtme_ref_record *d_ref_records,
                                          svtme_sb_result *d_sb_results);
-/* Time the ME kernels of every job with HIP events on the context's stream
- * (enable = 1); svtme_kernel_ms returns the last job's time over all of its
- * kernels, svtme_stage_ms the part of stage 0 (k_stage_a: zz / pre-HME /
- * HME-L0), 1 (k_stage_d: their decisions), 2 (k_stage_b: HME-L1/L2) or 3
- * (full-pel search + candidates: k_stage_c1 + k_stage_e, or k_stage_c). */
+/* Run ME for a batch of n <= SVTME_MAX_BATCH_JOBS pictures (the ready
+ * pictures of a mini-GOP, or this rank's SB band of n pictures) with ONE launch
+ * of each stage kernel (jobs needing different kernel variants are launched
+ * as separate groups). Job k writes its sb_count x R records to
+ * d_ref_records[k] and, when d_sb_results is not NULL and d_sb_results[k] is
+ * not NULL, its sb_count results to d_sb_results[k] (DEVICE buffers).
+ * Asynchronous on the context's stream; the reference runs these pictures on
+ * its ME threads concurrently (me_process.c:97-104). */
+#define SVTME_MAX_BATCH_JOBS 16
+svtme_status svtme_submit_batch_device(svtme_ctx *ctx, const svtme_job *jobs, uint32_t n,
+                                       svtme_ref_record *const *d_ref_records, svtme_sb_result *const *d_sb_results);
+/* Kernel timing with HIP events on the context's stream, recorded around every
+ * stage launch of every submission while enabled (enable = 1). svtme_timing_read
+ * waits for the recorded submissions and returns, averaged over them, the
+ * milliseconds of stage 0 (k_stage_a: zz / pre-HME / HME-L0), 1 (k_stage_d:
+ * their decisions), 2 (k_stage_b: HME-L1/L2), 3 (k_stage_c1, or the per-SB
+ * k_stage_c) and 4 (k_stage_e) in stage_ms[0..4]; returns the number of
+ * submissions averaged and clears them. */
 svtme_status svtme_set_timing(svtme_ctx *ctx, int enable);
-float svtme_kernel_ms(svtme_ctx *ctx);
-float svtme_stage_ms(svtme_ctx *ctx, int stage);
+uint32_t svtme_timing_read(svtme_ctx *ctx, float stage_ms[5]);
 /* Device pointer of the last job's record buffer (for RCCL all-gather). */
 void *svtme_device_records(svtme_ctx *ctx, uint64_t *bytes);
 /* The HIP stream (hipStream_t) the context launches on, for event timing. */
@@ -293,6 +313,13 @@ void svtme_derive_controls_tf(int hme_me_level, int qp_opt, int qp, int input_re
  * Per-kernel rtcd variants. Signatures identical to the pointers declared in
  * the reference's Source/Lib/Codec/aom_dsp_rtcd.h (line cited per entry).
  * ------------------------------------------------------------------------- */
+/* The variants are reentrant (per-thread HIP stream and scratch). They never
+ * return an error: on a HIP failure they leave their outputs untouched, set
+ * svtme_last_error() and raise the calling thread's failure flag, which
+ * svtme_rtcd_failed() returns (1) and clears, so the caller can re-run the call
+ * on the variant it replaced (integration/svtme_svt_glue.c). */
+int svtme_rtcd_failed(void);
+
 /* aom_dsp_rtcd.h:779 svt_sad_loop_kernel */
 void svt_sad_loop_kernel_hip(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
                              uint32_t block_height, uint32_t block_width, uint64_t *best_sad,

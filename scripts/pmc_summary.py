@@ -1,4 +1,4 @@
-"""Average rocprofv3 PMC counters per k_me_sb launch from gpurun_out/pmc_*/ CSVs.
+"""Average rocprofv3 PMC counters per ME-pass launch from <out>/pmc_*/ CSVs.
 
 FETCH_SIZE / WRITE_SIZE are KB; FETCH_SIZE is doubled for gfx950
 (MI355X_MICROARCH.md, HBM section: FETCH_SIZE reports half the bytes of wide
@@ -21,7 +21,7 @@ def main(out):
         by_dispatch = defaultdict(dict)
         names = {}
         for r in rows:
-            if not any(k in r["Kernel_Name"] for k in ("k_me_sb", "k_stage")):
+            if "k_stage" not in r["Kernel_Name"]:
                 continue
             by_dispatch[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0]
@@ -35,6 +35,16 @@ def main(out):
         for k, v in d.items():
             avg[k] += v
     res = {"counters_avg_per_launch": dict(avg), "per_kernel": kern}
+    for k, d in kern.items():
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_bytes"] = d["FETCH_SIZE"] * 1024 * 2 + d["WRITE_SIZE"] * 1024
+    try:  # the launch size the counters belong to (bench.json of the same profile)
+        with open(os.path.join(out, "bench.json")) as fh:
+            b = json.loads(fh.read().strip().splitlines()[-1])
+        res["sbs_per_launch"] = b["roofline"]["sbs_per_launch"]
+        res["workload"] = b["config"].get("name")
+    except (OSError, ValueError, KeyError, IndexError):
+        pass
     if "FETCH_SIZE" in avg:
         res["fetch_bytes_corrected"] = avg["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in avg:

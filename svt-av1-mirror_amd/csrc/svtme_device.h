@@ -74,7 +74,6 @@ struct DevJob {
     svtme_sb_result *out_sb;       // [sb_count] or nullptr
     uint32_t R;
     uint32_t pic_w_b64;
-    unsigned long long *stamps;    // diagnostic builds only: [sb_count][16] s_memtime
     ARes *ares;                    // [sb_count][SVTME_A_N] stage-A results
     BState *bst;                   // [sb_count] stage-B state
     uint32_t ta_count;             // stage-A searches per SB
@@ -84,6 +83,19 @@ struct DevJob {
     unsigned long long *keys;      // [sb_count][R][85] full-pel argmin keys (sad << 32 | order)
     CSlot *cslot;                  // [sb_count][R]
     uint32_t parts;                // search-row bands per (SB, reference) in k_stage_c1; 0 = per-SB k_stage_c
+};
+
+// A launch over a batch of picture jobs (svtme_submit_batch_device). The jobs
+// live in device memory; start[k] is the first work unit (wave or workgroup,
+// per stage) of job k in this launch, start[n..] = UINT32_MAX. Unit u belongs
+// to the job with the largest start[k] <= u (constant-index compares: the
+// kernel argument is never indexed dynamically).
+#define SVTME_MAX_BATCH 16
+struct DevBatch {
+    const DevJob *jobs;
+    uint32_t n;
+    uint32_t total; // units of this launch
+    uint32_t start[SVTME_MAX_BATCH];
 };
 
 static inline uint32_t svtme_round_up(uint32_t v, uint32_t a) { return (v + a - 1) / a * a; }

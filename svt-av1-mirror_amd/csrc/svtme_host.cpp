@@ -28,7 +28,9 @@ extern "C" hipError_t svtme_launch_build_full(const void *src, uint32_t src_stri
                                               DevPlane dst, int left, int top, int rows, hipStream_t s);
 extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int left, int top, int rows,
                                               hipStream_t s);
-extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid);
+extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
+                                          hipEvent_t *ev, uint32_t *mask);
+extern "C" uint32_t svtme_launch_key(const DevJob *dj);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" uint32_t svtme_fp_parts(const svtme_controls *c);
@@ -87,9 +89,23 @@ struct svtme_ctx {
     size_t sb_cap               = 0;
     uint32_t last_count = 0, last_R = 0;
     bool last_has_sb    = false;
-    bool timing         = false;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    hipEvent_t ev_mid[3] = {nullptr, nullptr, nullptr}; // after stages A, D, B
+    // job tables: a ring of device slots of SVTME_MAX_BATCH DevJobs, copied from
+    // pinned host memory on the job stream (in order: a slot is only rewritten
+    // after every kernel queued before has read it); a table identical to the
+    // last one published is reused without a copy
+    static constexpr int kRing = 16;
+    DevJob *d_table = nullptr, *h_table = nullptr;
+    hipEvent_t ring_copied[kRing] = {}; // the copy out of the pinned slot has run
+    bool ring_used[kRing] = {};
+    uint32_t ring_n[kRing] = {};
+    int ring_next = 0;
+    // timing: start/stop events of every stage launch of every launch group
+    // while enabled (attached to the dispatch packets: hipExtLaunchKernelGGL)
+    static constexpr int kTimeSets = 256;
+    bool timing = false;
+    hipEvent_t tev[kTimeSets][10] = {};
+    uint32_t tmask[kTimeSets] = {};
+    int t_pending = 0;
     ARes *d_ares    = nullptr; // stage-A results [count][SVTME_A_N]
     size_t ares_cap = 0;
     BState *d_bst   = nullptr; // stage-B state [count]
@@ -99,12 +115,6 @@ struct svtme_ctx {
     bool keys_rest             = false; // every key is ~0 (banded jobs accumulate with atomic min)
     CSlot *d_cslot             = nullptr; // [count][R]
     size_t cslot_cap           = 0;
-#ifdef SVTME_STAMPS
-    unsigned long long *d_stamps = nullptr;
-    size_t stamps_cap            = 0;
-    double stamp_sum[16]         = {0};
-    uint64_t stamp_n             = 0;
-#endif
     std::mutex mu;
 };
 
@@ -147,25 +157,17 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         (void)hipFree(c->d_records);
     if (c->d_sb)
         (void)hipFree(c->d_sb);
-    if (c->ev0)
-        (void)hipEventDestroy(c->ev0);
-    if (c->ev1)
-        (void)hipEventDestroy(c->ev1);
-    for (auto &e : c->ev_mid)
-        if (e)
-            (void)hipEventDestroy(e);
-#ifdef SVTME_STAMPS
-    if (c->stamp_n) {
-        fprintf(stderr, "[svtme stamps] %llu SBs, mean cycles per phase (from previous stamp):",
-                (unsigned long long)c->stamp_n);
-        for (int k = 1; k < 16; k++)
-            if (c->stamp_sum[k] > 0)
-                fprintf(stderr, " p%d=%.0f", k, c->stamp_sum[k] / c->stamp_n);
-        fprintf(stderr, "\n");
-    }
-    if (c->d_stamps)
-        (void)hipFree(c->d_stamps);
-#endif
+    for (auto &set : c->tev)
+        for (auto &e : set)
+            if (e)
+                (void)hipEventDestroy(e);
+    for (int k = 0; k < svtme_ctx::kRing; k++)
+        if (c->ring_copied[k])
+            (void)hipEventDestroy(c->ring_copied[k]);
+    if (c->d_table)
+        (void)hipFree(c->d_table);
+    if (c->h_table)
+        (void)hipHostFree(c->h_table);
     if (c->d_ares)
         (void)hipFree(c->d_ares);
     if (c->d_bst)
@@ -289,6 +291,24 @@ extern "C" svtme_status svtme_picture_upload_device(svtme_ctx *c, uint64_t pn, c
     return SVTME_OK;
 }
 
+extern "C" svtme_status svtme_picture_invalidate(svtme_ctx *c, uint64_t pn, const uint8_t *y, uint32_t stride,
+                                                 uint32_t w, uint32_t h) {
+    if (!c)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_invalidate: null ctx");
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        auto it = c->pics.find(pn);
+        if (it == c->pics.end())
+            return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_invalidate: picture %llu not resident",
+                        (unsigned long long)pn);
+        if (it->second.W != svtme_align8_u(w) || it->second.H != svtme_align8_u(h))
+            return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_invalidate: picture %llu is %ux%u, new planes %ux%u",
+                        (unsigned long long)pn, it->second.W, it->second.H, w, h);
+    }
+    // same stream as the jobs: the rebuild runs after every job already queued
+    return upload_host(c, pn, y, stride, w, h, 0);
+}
+
 extern "C" svtme_status svtme_picture_release(svtme_ctx *c, uint64_t pn) {
     if (!c)
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_release: null ctx");
@@ -389,88 +409,151 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
     return SVTME_OK;
 }
 
-static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_sb, svtme_ref_record *d_out,
-                                  svtme_sb_result *d_out_sb) {
+static svtme_status ensure_ring(svtme_ctx *c) {
+    if (c->d_table)
+        return SVTME_OK;
+    const size_t bytes = sizeof(DevJob) * SVTME_MAX_BATCH * svtme_ctx::kRing;
+    HIP_TRY(hipMalloc((void **)&c->d_table, bytes));
+    HIP_TRY(hipHostMalloc((void **)&c->h_table, bytes, hipHostMallocDefault));
+    for (int k = 0; k < svtme_ctx::kRing; k++)
+        HIP_TRY(hipEventCreateWithFlags(&c->ring_copied[k], hipEventDisableTiming));
+    return SVTME_OK;
+}
+
+// Validate, lay out and launch n jobs. out[k] / out_sb[k]: device outputs of
+// job k; null out => the context's own record buffer (single job only).
+static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uint32_t n,
+                                        svtme_ref_record *const *out, svtme_sb_result *const *out_sb,
+                                        bool with_sb) {
     HIP_TRY(hipSetDevice(c->device));
-    DevJob dj;
-    uint32_t count;
-    svtme_status st = validate_job(c, job, &dj, &count);
-    if (st)
-        return st;
-    if (d_out) {
-        dj.out_records = d_out;
-        dj.out_sb      = d_out_sb;
-    } else {
-        if ((st = ensure_buf((void **)&c->d_records, &c->records_cap,
-                             (size_t)count * dj.R * sizeof(svtme_ref_record))))
+    if (n == 0 || n > SVTME_MAX_BATCH)
+        return fail(SVTME_ERR_BAD_PARAMETER, "batch of %u jobs (1..%d)", n, SVTME_MAX_BATCH);
+    DevJob hj[SVTME_MAX_BATCH];
+    uint32_t count[SVTME_MAX_BATCH];
+    size_t sbs = 0, slots = 0;
+    svtme_status st;
+    for (uint32_t k = 0; k < n; k++) {
+        if ((st = validate_job(c, &jobs[k], &hj[k], &count[k])))
             return st;
-        dj.out_records = c->d_records;
+        sbs += count[k];
+        slots += (size_t)count[k] * hj[k].R;
+    }
+    if (!out && n != 1)
+        return fail(SVTME_ERR_BAD_PARAMETER, "context-owned outputs hold one job");
+    if (out) {
+        for (uint32_t k = 0; k < n; k++) {
+            if (!out[k])
+                return fail(SVTME_ERR_BAD_PARAMETER, "null record buffer for job %u", k);
+            hj[k].out_records = out[k];
+            hj[k].out_sb      = out_sb ? out_sb[k] : nullptr;
+        }
+    } else {
+        if ((st = ensure_buf((void **)&c->d_records, &c->records_cap, slots * sizeof(svtme_ref_record))))
+            return st;
+        hj[0].out_records = c->d_records;
         if (with_sb) {
-            if ((st = ensure_buf((void **)&c->d_sb, &c->sb_cap, (size_t)count * sizeof(svtme_sb_result))))
+            if ((st = ensure_buf((void **)&c->d_sb, &c->sb_cap, sbs * sizeof(svtme_sb_result))))
                 return st;
-            dj.out_sb = c->d_sb;
+            hj[0].out_sb = c->d_sb;
         }
     }
-#ifdef SVTME_STAMPS
-    if ((st = ensure_buf((void **)&c->d_stamps, &c->stamps_cap, (size_t)count * 16 * 8)))
+    // inter-stage scratch of the whole batch, per-job offsets
+    if ((st = ensure_buf((void **)&c->d_ares, &c->ares_cap, sbs * SVTME_A_N * sizeof(ARes))))
         return st;
-    HIP_TRY(hipMemsetAsync(c->d_stamps, 0, (size_t)count * 16 * 8, c->stream));
-    dj.stamps = c->d_stamps;
-#endif
-    if (c->timing)
-        HIP_TRY(hipEventRecord(c->ev0, c->stream));
-    if ((st = ensure_buf((void **)&c->d_ares, &c->ares_cap, (size_t)count * SVTME_A_N * sizeof(ARes))))
+    if ((st = ensure_buf((void **)&c->d_bst, &c->bst_cap, sbs * sizeof(BState))))
         return st;
-    if ((st = ensure_buf((void **)&c->d_bst, &c->bst_cap, (size_t)count * sizeof(BState))))
-        return st;
-    dj.ares = c->d_ares;
-    dj.bst  = c->d_bst;
-    dj.parts = svtme_fp_parts(&dj.job.ctrl);
-    if (dj.parts) { // wide full-pel stage (k_stage_c1 + k_stage_e)
-        const size_t kb = (size_t)count * dj.R * SVTME_PU_COUNT * sizeof(unsigned long long);
+    bool any_banded = false, any_single = false, any_wide = false;
+    for (uint32_t k = 0; k < n; k++) {
+        hj[k].parts = svtme_fp_parts(&hj[k].job.ctrl);
+        any_wide |= hj[k].parts != 0;
+        any_banded |= hj[k].parts > 1;
+        any_single |= hj[k].parts == 1;
+    }
+    if (any_wide) { // wide full-pel stage (k_stage_c1 + k_stage_e)
+        const size_t kb = slots * SVTME_PU_COUNT * sizeof(unsigned long long);
         if (c->keys_cap < kb) {
             if ((st = ensure_buf((void **)&c->d_keys, &c->keys_cap, kb)))
                 return st;
             c->keys_rest = false;
         }
-        if ((st = ensure_buf((void **)&c->d_cslot, &c->cslot_cap, (size_t)count * dj.R * sizeof(CSlot))))
+        if ((st = ensure_buf((void **)&c->d_cslot, &c->cslot_cap, slots * sizeof(CSlot))))
             return st;
-        if (dj.parts > 1 && !c->keys_rest) {
+        // banded jobs merge with atomic min into keys that must all be ~0; k_stage_e
+        // resets what it consumed, plain-store (single band) jobs leave keys behind
+        if (any_banded && !c->keys_rest)
             HIP_TRY(hipMemsetAsync(c->d_keys, 0xFF, c->keys_cap, c->stream));
-            c->keys_rest = true;
-        }
-        if (dj.parts == 1)
-            c->keys_rest = false; // plain stores leave keys behind
-        dj.keys  = c->d_keys;
-        dj.cslot = c->d_cslot;
+        c->keys_rest = !any_single;
     }
-    svtme_stage_a_list(&dj.job, dj.ta_list, &dj.ta_count);
-    svtme_stage_b_list(&dj.job, dj.tb_list, &dj.tb_count);
-    HIP_TRY(svtme_launch_stages(&dj, count, c->stream, c->timing ? c->ev_mid : nullptr));
-#ifdef SVTME_STAMPS
-    {
-        std::vector<unsigned long long> h((size_t)count * 16);
-        HIP_TRY(hipMemcpyAsync(h.data(), c->d_stamps, h.size() * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        for (uint32_t b = 0; b < count; b++) {
-            unsigned long long prev = h[b * 16];
-            for (int k = 1; k < 16; k++) {
-                const unsigned long long v = h[b * 16 + k];
-                if (v) {
-                    c->stamp_sum[k] += (double)(v - prev);
-                    prev = v;
-                }
+    size_t sb_off = 0, slot_off = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        hj[k].ares  = c->d_ares + sb_off * SVTME_A_N;
+        hj[k].bst   = c->d_bst + sb_off;
+        hj[k].keys  = hj[k].parts ? c->d_keys + slot_off * SVTME_PU_COUNT : nullptr;
+        hj[k].cslot = hj[k].parts ? c->d_cslot + slot_off : nullptr;
+        svtme_stage_a_list(&hj[k].job, hj[k].ta_list, &hj[k].ta_count);
+        svtme_stage_b_list(&hj[k].job, hj[k].tb_list, &hj[k].tb_count);
+        sb_off += count[k];
+        slot_off += (size_t)count[k] * hj[k].R;
+    }
+    // group by kernel variant (stable), publish the table, launch each group
+    DevJob ordered[SVTME_MAX_BATCH];
+    uint32_t keys[SVTME_MAX_BATCH], m = 0;
+    for (uint32_t k = 0; k < n; k++) keys[k] = svtme_launch_key(&hj[k]);
+    bool taken[SVTME_MAX_BATCH] = {};
+    uint32_t group_start[SVTME_MAX_BATCH + 1], groups = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        if (taken[k])
+            continue;
+        group_start[groups++] = m;
+        for (uint32_t q = k; q < n; q++)
+            if (!taken[q] && keys[q] == keys[k]) {
+                ordered[m++] = hj[q];
+                taken[q]     = true;
             }
-        }
-        c->stamp_n += count;
     }
-#endif
-    if (c->timing)
-        HIP_TRY(hipEventRecord(c->ev1, c->stream));
-    c->last_count  = count;
-    c->last_R      = dj.R;
-    c->last_has_sb = with_sb && !d_out;
+    group_start[groups] = m;
+    if ((st = ensure_ring(c)))
+        return st;
+    int slot = -1;
+    for (int k = 0; k < svtme_ctx::kRing && slot < 0; k++)
+        if (c->ring_used[k] && c->ring_n[k] == n &&
+            memcmp(c->h_table + (size_t)k * SVTME_MAX_BATCH, ordered, sizeof(DevJob) * n) == 0)
+            slot = k; // already resident (device copy of this exact table)
+    if (slot < 0) {
+        slot         = c->ring_next;
+        c->ring_next = (slot + 1) % svtme_ctx::kRing;
+        DevJob *h    = c->h_table + (size_t)slot * SVTME_MAX_BATCH;
+        if (c->ring_used[slot])
+            HIP_TRY(hipEventSynchronize(c->ring_copied[slot])); // pinned slot no longer being read
+        memcpy(h, ordered, sizeof(DevJob) * n);
+        HIP_TRY(hipMemcpyAsync(c->d_table + (size_t)slot * SVTME_MAX_BATCH, h, sizeof(DevJob) * n,
+                               hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipEventRecord(c->ring_copied[slot], c->stream));
+        c->ring_used[slot] = true;
+        c->ring_n[slot]    = n;
+    }
+    DevJob *d = c->d_table + (size_t)slot * SVTME_MAX_BATCH;
+    for (uint32_t g = 0; g < groups; g++) {
+        hipEvent_t *ev = nullptr;
+        uint32_t *mask = nullptr;
+        if (c->timing && c->t_pending < svtme_ctx::kTimeSets) {
+            ev   = c->tev[c->t_pending];
+            mask = &c->tmask[c->t_pending++];
+        }
+        HIP_TRY(svtme_launch_stages(d + group_start[g], ordered + group_start[g], group_start[g + 1] - group_start[g],
+                                    c->stream, ev, mask));
+    }
+    c->last_count      = (uint32_t)sbs;
+    c->last_R          = n == 1 ? hj[0].R : 0;
+    c->last_has_sb     = with_sb && !out;
     return SVTME_OK;
+}
+
+static svtme_status submit_locked(svtme_ctx *c, const svtme_job *job, bool with_sb, svtme_ref_record *d_out,
+                                  svtme_sb_result *d_out_sb) {
+    if (d_out)
+        return submit_batch_locked(c, job, 1, &d_out, &d_out_sb, d_out_sb != nullptr);
+    return submit_batch_locked(c, job, 1, nullptr, nullptr, with_sb);
 }
 
 extern "C" svtme_status svtme_submit_picture_device(svtme_ctx *c, const svtme_job *job, svtme_ref_record *d_recs,
@@ -481,39 +564,45 @@ extern "C" svtme_status svtme_submit_picture_device(svtme_ctx *c, const svtme_jo
     return submit_locked(c, job, d_sb != nullptr, d_recs, d_sb);
 }
 
+extern "C" svtme_status svtme_submit_batch_device(svtme_ctx *c, const svtme_job *jobs, uint32_t n,
+                                                  svtme_ref_record *const *d_recs, svtme_sb_result *const *d_sb) {
+    if (!c || !jobs || !d_recs)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_batch_device: null ctx, jobs or outputs");
+    std::lock_guard<std::mutex> lk(c->mu);
+    return submit_batch_locked(c, jobs, n, d_recs, d_sb, d_sb != nullptr);
+}
+
 extern "C" svtme_status svtme_set_timing(svtme_ctx *c, int enable) {
     if (!c)
         return fail(SVTME_ERR_BAD_PARAMETER, "null ctx");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    if (enable && !c->ev0) {
-        HIP_TRY(hipEventCreate(&c->ev0));
-        HIP_TRY(hipEventCreate(&c->ev1));
-        for (auto &e : c->ev_mid)
-            HIP_TRY(hipEventCreate(&e));
-    }
+    if (enable && !c->tev[0][0])
+        for (auto &set : c->tev)
+            for (auto &e : set) HIP_TRY(hipEventCreate(&e));
     c->timing = enable != 0;
     return SVTME_OK;
 }
 
-extern "C" float svtme_kernel_ms(svtme_ctx *c) {
-    if (!c || !c->timing)
-        return -1.0f;
-    float ms = -1.0f;
-    if (hipEventSynchronize(c->ev1) != hipSuccess || hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess)
-        return -1.0f;
-    return ms;
-}
-
-extern "C" float svtme_stage_ms(svtme_ctx *c, int stage) {
-    if (!c || !c->timing || stage < 0 || stage > 3 || !c->ev_mid[0])
-        return -1.0f;
-    hipEvent_t a = stage == 0 ? c->ev0 : c->ev_mid[stage - 1];
-    hipEvent_t b = stage == 3 ? c->ev1 : c->ev_mid[stage];
-    float ms = -1.0f;
-    if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess)
-        return -1.0f;
-    return ms;
+extern "C" uint32_t svtme_timing_read(svtme_ctx *c, float stage_ms[5]) {
+    if (!c || !stage_ms)
+        return 0;
+    std::lock_guard<std::mutex> lk(c->mu);
+    double sum[5] = {0, 0, 0, 0, 0};
+    const int n = c->t_pending;
+    for (int i = 0; i < n; i++)
+        for (int k = 0; k < 5; k++) {
+            if (!((c->tmask[i] >> k) & 1u))
+                continue;
+            float ms = 0.0f;
+            if (hipEventSynchronize(c->tev[i][2 * k + 1]) != hipSuccess ||
+                hipEventElapsedTime(&ms, c->tev[i][2 * k], c->tev[i][2 * k + 1]) != hipSuccess)
+                return 0;
+            sum[k] += ms;
+        }
+    for (int k = 0; k < 5; k++) stage_ms[k] = n ? (float)(sum[k] / n) : 0.0f;
+    c->t_pending = 0;
+    return (uint32_t)n;
 }
 
 extern "C" svtme_status svtme_submit_picture_async(svtme_ctx *c, const svtme_job *job) {

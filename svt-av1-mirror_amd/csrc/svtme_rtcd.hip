@@ -7,15 +7,19 @@
 // semantics can be checked in isolation. One call is microseconds of CPU work,
 // far below a launch: the performance boundary is the picture job API.
 //
-// Each call: copy the bytes the kernel reads into a per-process device
-// scratch, run one kernel, copy the outputs back. On any HIP error the call
-// reports through svtme_last_error() and stderr and leaves outputs untouched;
-// there is no CPU fallback.
+// Each call: copy the bytes the kernel reads into the calling thread's device
+// scratch, run one kernel on the calling thread's stream, copy the outputs
+// back. Reentrant: the reference calls these from up to 25 ME threads at once
+// (enc_handle.c:731-773), so every thread owns its stream and scratch and no
+// lock is taken. On any HIP error the call reports through svtme_last_error()
+// and stderr, leaves outputs untouched and raises the thread's failure flag
+// (svtme_rtcd_failed()); the library has no CPU path of its own -- the
+// encoder glue (integration/svtme_svt_glue.c) re-runs the call on the C
+// variant it replaced, so the encoder never consumes stale outputs.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstring>
-#include <mutex>
 #include <string>
 
 #include "svtme_device.h"
@@ -25,17 +29,24 @@ extern "C" void svtme_set_error_internal(const char *msg);
 namespace {
 
 struct Scratch {
-    std::mutex mu;
     hipStream_t stream = nullptr;
     uint8_t *d         = nullptr;
     size_t cap         = 0;
     bool init          = false;
+    bool failed        = false;
+    ~Scratch() {
+        if (d)
+            (void)hipFree(d);
+        if (stream)
+            (void)hipStreamDestroy(stream);
+    }
 };
-Scratch g_rt;
+thread_local Scratch g_rt;
 
 bool report(hipError_t e, const char *what) {
     if (e == hipSuccess)
         return true;
+    g_rt.failed = true;
     char buf[256];
     snprintf(buf, sizeof(buf), "%s: %s", what, hipGetErrorString(e));
     svtme_set_error_internal(buf);
@@ -254,6 +265,13 @@ __global__ void k_downsample(const uint8_t *in, uint32_t in_stride, uint32_t w, 
 // --------------------------------------------------------------------------
 // host wrappers
 // --------------------------------------------------------------------------
+// 1 if an rtcd call of this thread failed since the last query (then cleared)
+extern "C" int svtme_rtcd_failed(void) {
+    const int f = g_rt.failed ? 1 : 0;
+    g_rt.failed = false;
+    return f;
+}
+
 #define RT_CHECK(expr, what)                                                                                        \
     do {                                                                                                            \
         if (!report((expr), what))                                                                                  \
@@ -272,7 +290,6 @@ extern "C" void svt_sad_loop_kernel_hip(uint8_t *src, uint32_t src_stride, uint8
                                         int16_t *x_search_center, int16_t *y_search_center, uint32_t src_stride_raw,
                                         uint8_t skip_search_line, int16_t search_area_width,
                                         int16_t search_area_height) {
-    std::lock_guard<std::mutex> lk(g_rt.mu);
     *best_sad = 0xffffff;
     if (search_area_width <= 0 || search_area_height <= 0 || block_height == 0 || block_width == 0)
         return;
@@ -303,7 +320,6 @@ extern "C" void svt_sad_loop_kernel_hip(uint8_t *src, uint32_t src_stride, uint8
 
 template <typename T>
 static uint32_t nxm_hip(const T *src, uint32_t src_stride, const T *ref, uint32_t ref_stride, uint32_t h, uint32_t w) {
-    std::lock_guard<std::mutex> lk(g_rt.mu);
     if (h == 0 || w == 0)
         return 0;
     const size_t ss = span(h, src_stride, w) * sizeof(T), rs = span(h, ref_stride, w) * sizeof(T);
@@ -337,7 +353,6 @@ extern "C" void svt_ext_sad_calculation_8x8_16x16_hip(uint8_t *src, uint32_t src
                                                       uint32_t *p_best_sad_16x16, uint32_t *p_best_mv8x8,
                                                       uint32_t *p_best_mv16x16, uint32_t mv, uint32_t *p_sad16x16,
                                                       uint32_t *p_sad8x8, bool sub_sad) {
-    std::lock_guard<std::mutex> lk(g_rt.mu);
     const size_t ss = span(16, src_stride, 16), rs = span(16, ref_stride, 16);
     uint8_t *d = scratch(ss + rs + 64 + 16 * 4);
     if (!d)
@@ -365,7 +380,6 @@ extern "C" void svt_ext_sad_calculation_8x8_16x16_hip(uint8_t *src, uint32_t src
 extern "C" void svt_ext_sad_calculation_32x32_64x64_hip(uint32_t *p_sad16x16, uint32_t *p_best_sad_32x32,
                                                         uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
                                                         uint32_t *p_best_mv64x64, uint32_t mv, uint32_t *p_sad32x32) {
-    std::lock_guard<std::mutex> lk(g_rt.mu);
     uint32_t *io = (uint32_t *)scratch(30 * 4);
     if (!io)
         return;
@@ -390,7 +404,6 @@ extern "C" void svt_ext_all_sad_calculation_8x8_16x16_hip(uint8_t *src, uint32_t
                                                           uint32_t *p_best_mv16x16, uint32_t p_eight_sad16x16[16][8],
                                                           uint32_t p_eight_sad8x8[64][8], bool sub_sad) {
     (void)p_eight_sad8x8; // not written by the C reference either (motion_estimation.c:218)
-    std::lock_guard<std::mutex> lk(g_rt.mu);
     const size_t ss = span(64, src_stride, 64), rs = span(64, ref_stride, 64 + 7);
     uint8_t *d = scratch(ss + rs + 64 + 288 * 4);
     if (!d)
@@ -422,7 +435,6 @@ extern "C" void svt_ext_eight_sad_calculation_32x32_64x64_hip(uint32_t p_sad16x1
                                                               uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
                                                               uint32_t *p_best_mv64x64, uint32_t mv,
                                                               uint32_t p_sad32x32[4][8]) {
-    std::lock_guard<std::mutex> lk(g_rt.mu);
     uint32_t *io = (uint32_t *)scratch(170 * 4);
     if (!io)
         return;
@@ -444,7 +456,6 @@ extern "C" void svt_ext_eight_sad_calculation_32x32_64x64_hip(uint32_t p_sad16x1
 
 extern "C" void svt_initialize_buffer_32bits_hip(uint32_t *pointer, uint32_t count128, uint32_t count32,
                                                  uint32_t value) {
-    std::lock_guard<std::mutex> lk(g_rt.mu);
     const uint32_t n = count128 * 4 + count32;
     if (!n)
         return;
@@ -460,7 +471,6 @@ extern "C" void svt_initialize_buffer_32bits_hip(uint32_t *pointer, uint32_t cou
 extern "C" void svt_aom_downsample_2d_hip(uint8_t *input_samples, uint32_t input_stride, uint32_t input_area_width,
                                           uint32_t input_area_height, uint8_t *decim_samples, uint32_t decim_stride,
                                           uint32_t decim_step) {
-    std::lock_guard<std::mutex> lk(g_rt.mu);
     const uint32_t half = decim_step >> 1;
     if (decim_step < 2 || input_area_width <= half || input_area_height <= half)
         return;

@@ -28,21 +28,13 @@
 // (sad << 32 | y << 16 | x, or sad << 32 | raster order) so the reference's
 // strict-< first-minimum scan order (compute_sad_c.c:90,
 // motion_estimation.c:137-425) falls out of an integer min.
+#include <hip/hip_ext.h>
 #include <type_traits>
 
 #include "svtme_me_common.h"
 
 namespace svtme {
 
-#ifdef SVTME_STAMPS
-#define STAMP(k)                                                                                                    \
-    do {                                                                                                            \
-        if (threadIdx.x == 0 && dj.stamps)                                                                          \
-            dj.stamps[(size_t)sb_local * 16 + (k)] = __builtin_amdgcn_s_memtime();                                 \
-    } while (0)
-#else
-#define STAMP(k) do { } while (0)
-#endif
 
 #define STAGE_A_BUF_DW 1024 // per-wave window buffers (dwords)
 #define STAGE_B_BUF_DW 640
@@ -389,6 +381,25 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
     return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
 }
 
+// the job of work unit u of a batch launch, and u's index inside that job. The
+// job table is read through the constant address space: it is written before
+// the launch and never during it, so the compiler may keep its fields in SGPRs
+// (scalar loads, hoisted and CSE'd across the kernel's own stores) exactly as
+// it does for a by-value kernel argument.
+typedef __attribute__((address_space(4))) const DevJob cjob_t;
+__device__ __forceinline__ const DevJob &batch_job(const DevBatch &B, uint32_t u, uint32_t *local) {
+    uint32_t j = 0, s0 = 0;
+#pragma unroll
+    for (int k = 1; k < SVTME_MAX_BATCH; k++)
+        if (u >= B.start[k]) {
+            j  = (uint32_t)k;
+            s0 = B.start[k];
+        }
+    *local = u - s0;
+    cjob_t *t = (cjob_t *)(uintptr_t)B.jobs;
+    return *(const DevJob *)(t + UNI(j));
+}
+
 // per-slot reference planes into LDS with constant-index argument reads
 template <int NLV>
 __device__ __forceinline__ void copy_planes(const DevJob &dj, DevPlane (*pl)[NLV], uint16_t *dist) {
@@ -427,16 +438,17 @@ __device__ __forceinline__ uint32_t zz_finish(const ZzLoads &z) {
 #define TA_HME 0 // zz SAD + the four HME-L0 quadrants of one slot
 #define TA_PH 1  // the two pre-HME regions of one slot
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_stage_a(const DevJob dj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_stage_a(const DevBatch B) {
     __shared__ __attribute__((aligned(16))) uint8_t srcb[4][256];
     __shared__ uint32_t wbuf[4][STAGE_A_BUF_DW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total)
+        return;
+    uint32_t gw;
+    const DevJob &dj        = batch_job(B, u, &gw);
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t total = job.sb_count * dj.ta_count;
-    const uint32_t gw    = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
-    if (gw >= total)
-        return;
     const uint32_t sb_local = UNI(gw / dj.ta_count);
     const int entry         = UNI(dj.ta_list[gw - sb_local * dj.ta_count]);
     const int kind = entry >> 3, s = entry & 7, l = s >> 2, r = s & 3;
@@ -596,14 +608,16 @@ struct Dec {
     uint64_t lsad[8][4];
 };
 
-__global__ void __launch_bounds__(256) k_stage_d(const DevJob dj) {
+__global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
     __shared__ Dec dec[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total)
+        return;
+    uint32_t sb_local;
+    const DevJob &dj        = batch_job(B, u, &sb_local);
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t sb_local = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
-    if (sb_local >= job.sb_count)
-        return;
     Dec &d               = dec[wid];
     const SbGeo G        = sb_geo(dj, sb_local);
     const int nl         = job.num_lists;
@@ -806,16 +820,17 @@ __device__ __forceinline__ void hme_refine(int level, const DevPlane &P, int16_t
 }
 
 template <bool L2>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L2 ? 4 : 6, 8))) k_stage_b(const DevJob dj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L2 ? 4 : 6, 8))) k_stage_b(const DevBatch B) {
     __shared__ __attribute__((aligned(16))) uint8_t srcb[4][L2 ? 64 * 64 : 32 * 32];
     __shared__ uint32_t wbuf[4][STAGE_B_BUF_DW];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total)
+        return;
+    uint32_t gw;
+    const DevJob &dj        = batch_job(B, u, &gw);
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t total = job.sb_count * dj.tb_count;
-    const uint32_t gw    = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
-    if (gw >= total)
-        return;
     const uint32_t sb_local = UNI(gw / dj.tb_count);
     const int e             = UNI(dj.tb_list[gw - sb_local * dj.tb_count]);
     const int s = e >> 2, q = e & 3, l = s >> 2, r = s & 3;
@@ -886,7 +901,7 @@ struct SlotCentre {
     uint8_t do_ref;
 };
 
-__device__ SlotCentre final_centre(const DevJob &dj, uint32_t sb_local, uint32_t vmask) {
+__device__ __forceinline__ SlotCentre final_centre(const DevJob &dj, uint32_t sb_local, uint32_t vmask) {
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
     const int s             = threadIdx.x & 63;
@@ -1194,7 +1209,7 @@ __device__ void fullpel(StC &st, const DevPlane &C, uint32_t ox, uint32_t oy) {
 
 // Candidate arrays + distortions + GM detection for one SB, all threads
 // (motion_estimation.c:2532-3007). Thread n builds Z-order PU n.
-__device__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
+__device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
     const svtme_job &job = dj.job;
     const int tid = threadIdx.x;
     const int nl = job.num_lists, nr0 = job.num_refs[0], nr1 = nl == 2 ? job.num_refs[1] : 0;
@@ -1422,7 +1437,7 @@ __device__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t
 // me_prune_ref, the per-reference records and the candidate arrays /
 // distortions / GM detection of one SB from its searched best SADs and MVs
 // (motion_estimation.c:1522-1565, 2520-3007); all threads of the workgroup
-__device__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh, uint32_t vmask) {
+__device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh, uint32_t vmask) {
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -1452,7 +1467,6 @@ __device__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t sb_local, uint3
         }
     }
     __syncthreads();
-    STAMP(14);
 
     // ---- records (sb_count x R, slots in list-0-then-list-1 order)
     {
@@ -1490,19 +1504,19 @@ __device__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t sb_local, uint3
 }
 
 template <bool SUB_ME>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_c(const DevJob dj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_c(const DevBatch B) {
     __shared__ StC st;
+    uint32_t sb_local;
+    const DevJob &dj        = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const bool w0           = wid == 0;
-    const uint32_t sb_local = xcd_remap(blockIdx.x, gridDim.x);
     const SbGeo G           = sb_geo(dj, sb_local);
     const uint32_t ox = G.ox, oy = G.oy, bw = G.bw, bh = G.bh;
     const uint32_t vmask = valid_mask(job);
 
     const DevPlane &C = dj.cur.lv[0]; // source block read in place (me_process.c:183-214)
-    STAMP(8);
     if (tid == 0) {
 #pragma unroll
         for (int s = 0; s < 8; s++) {
@@ -1529,7 +1543,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
     for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) (&st.best_mv[0][0])[e] = 0;
     __syncthreads();
-    STAMP(9);
 
     // ---- integer_search_b64 (motion_estimation.c:1249-1516); lane s of wave 0 owns slot s.
     // Two rounds when enable_me_sr_adjustment == 2: the other slots read slot 0's 64x64 SAD.
@@ -1591,7 +1604,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 st.nreq = tot;
         }
         __syncthreads();
-        STAMP(10);
         if (st.nreq) {
             for (int q = wid; q < 2 * st.nreq; q += 4) {
                 const uint32_t v = wave_nxm(st.req[q], st.req_stride[q], C.base + (ptrdiff_t)oy * C.stride + ox,
@@ -1645,7 +1657,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 st.k32 = 1; // a single position
         }
         __syncthreads();
-        STAMP(11);
         for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) {
             const int s = e / SVTME_PU_COUNT;
             if (st.in_round[s])
@@ -1653,7 +1664,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
         if (st.nfp) {
             fullpel<SUB_ME>(st, C, ox, oy); // centre probe (motion_estimation.c:1414-1417)
-            STAMP(12);
             // 8x8-variance resize (motion_estimation.c:1418-1438)
             if (w0 && lane < 8 && st.in_round[lane] && c.me_8x8_var_enabled && (st.is_w[lane] * st.is_h[lane] > 24)) {
                 const int s = lane;
@@ -1713,13 +1723,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 st.k32 = k32;
         }
         __syncthreads();
-        STAMP(13);
         if (st.nfp)
             fullpel<SUB_ME>(st, C, ox, oy);
     }
 
     stage_c_tail(st, dj, sb_local, bw, bh, vmask);
-    STAMP(15);
 }
 
 // ----------------------------------------------------------------------------
@@ -1828,15 +1836,17 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
 
 // K32: every order fits 12 bits (the host bounds the area, svtme_fp_k32)
 template <bool SUB, bool K32>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 5 : 4, 8))) k_stage_c1(const DevJob dj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 5 : 4, 8))) k_stage_c1(const DevBatch B) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total)
+        return;
+    uint32_t gw;
+    const DevJob &dj        = batch_job(B, u, &gw);
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t parts  = dj.parts;
     const uint32_t per_sb = dj.R * parts;
-    const uint32_t gw     = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
-    if (gw >= job.sb_count * per_sb)
-        return;
     const uint32_t sb_local = UNI(gw / per_sb);
     const uint32_t rem      = gw - sb_local * per_sb;
     const int k             = UNI(rem / parts);
@@ -1993,12 +2003,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
 
 // Per SB: decode the argmin keys into best SAD / MV per PU (strict-< first
 // minimum in search order), then stage_c_tail
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_e(const DevJob dj) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_e(const DevBatch B) {
     __shared__ StC st;
     __shared__ CSlot csl[8];
+    uint32_t sb_local;
+    const DevJob &dj        = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
     const svtme_job &job    = dj.job;
     const int tid           = threadIdx.x;
-    const uint32_t sb_local = xcd_remap(blockIdx.x, gridDim.x);
     const SbGeo G           = sb_geo(dj, sb_local);
     const uint32_t vmask    = valid_mask(job);
     const int R             = (int)dj.R;
@@ -2140,43 +2151,80 @@ extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {
     return parts < 1 ? 1 : (parts > 16 ? 16 : parts);
 }
 
-// mid (optional): three events recorded after stages A, D and B
-extern "C" hipError_t svtme_launch_stages(const DevJob *dj, uint32_t sb_count, hipStream_t s, hipEvent_t *mid) {
-    if (dj->ta_count) {
-        const uint32_t waves = sb_count * dj->ta_count;
-        hipLaunchKernelGGL(svtme::k_stage_a, dim3((waves + 3) / 4), dim3(256), 0, s, *dj);
-    }
-    if (mid)
-        (void)hipEventRecord(mid[0], s);
-    hipLaunchKernelGGL(svtme::k_stage_d, dim3((sb_count + 3) / 4), dim3(256), 0, s, *dj);
-    if (mid)
-        (void)hipEventRecord(mid[1], s);
-    if (dj->tb_count) {
-        const uint32_t waves = sb_count * dj->tb_count;
-        if (dj->job.ctrl.enable_hme_level2_flag)
-            hipLaunchKernelGGL(svtme::k_stage_b<true>, dim3((waves + 3) / 4), dim3(256), 0, s, *dj);
-        else
-            hipLaunchKernelGGL(svtme::k_stage_b<false>, dim3((waves + 3) / 4), dim3(256), 0, s, *dj);
-    }
-    if (mid)
-        (void)hipEventRecord(mid[2], s);
+// Batch launch key: jobs launched together must agree on it (svtme_host.cpp
+// splits a batch into groups by it).
+extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
     const bool full = dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
-    if (dj->parts) { // wide full-pel stage + per-SB decode
-        const uint32_t waves = sb_count * dj->R * dj->parts;
-        const dim3 grid((waves + 3) / 4);
-        const bool k32 = svtme_fp_k32(&dj->job.ctrl);
-        if (full && k32)
-            hipLaunchKernelGGL((svtme::k_stage_c1<false, true>), grid, dim3(256), 0, s, *dj);
-        else if (full)
-            hipLaunchKernelGGL((svtme::k_stage_c1<false, false>), grid, dim3(256), 0, s, *dj);
-        else if (k32)
-            hipLaunchKernelGGL((svtme::k_stage_c1<true, true>), grid, dim3(256), 0, s, *dj);
+    return (uint32_t)full | (uint32_t)(dj->parts != 0) << 1 | (uint32_t)svtme_fp_k32(&dj->job.ctrl) << 2 |
+           (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3;
+}
+
+static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
+    DevBatch b;
+    b.jobs     = d_jobs;
+    b.n        = n;
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < SVTME_MAX_BATCH; k++) {
+        b.start[k] = k < n ? t : 0xFFFFFFFFu;
+        if (k < n)
+            t += units(h[k]);
+    }
+    b.total = t;
+    return b;
+}
+
+// One launch of every stage over a batch of n jobs sharing svtme_launch_key.
+// d_jobs: the jobs in device memory; h_jobs: the same jobs on the host (unit
+// counts). ev (optional, timing): ten events, start / stop of stage k in
+// ev[2k], ev[2k+1] (k = A, D, B, C1|C, E), attached to the dispatch packets
+// themselves (hipExtLaunchKernelGGL: no extra packets, no gaps); *mask gets
+// bit k for every stage launched.
+#define SVTME_LAUNCH(K, grid, k, ...)                                                                               \
+    do {                                                                                                           \
+        if (ev) {                                                                                                  \
+            hipExtLaunchKernelGGL(K, grid, dim3(256), 0, s, ev[2 * (k)], ev[2 * (k) + 1], 0, __VA_ARGS__);           \
+            *mask |= 1u << (k);                                                                                    \
+        } else                                                                                                     \
+            hipLaunchKernelGGL(K, grid, dim3(256), 0, s, __VA_ARGS__);                                             \
+    } while (0)
+
+extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
+                                          hipEvent_t *ev, uint32_t *mask) {
+    if (n == 0 || n > SVTME_MAX_BATCH)
+        return hipErrorInvalidValue;
+    const DevJob &h0 = h_jobs[0];
+    if (mask)
+        *mask = 0;
+    const DevBatch ba = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta_count; });
+    if (ba.total)
+        SVTME_LAUNCH(svtme::k_stage_a, dim3((ba.total + 3) / 4), 0, ba);
+    const DevBatch bd = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
+    SVTME_LAUNCH(svtme::k_stage_d, dim3((bd.total + 3) / 4), 1, bd);
+    const DevBatch bb = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.tb_count; });
+    if (bb.total) {
+        if (h0.job.ctrl.enable_hme_level2_flag)
+            SVTME_LAUNCH(svtme::k_stage_b<true>, dim3((bb.total + 3) / 4), 2, bb);
         else
-            hipLaunchKernelGGL((svtme::k_stage_c1<true, false>), grid, dim3(256), 0, s, *dj);
-        hipLaunchKernelGGL(svtme::k_stage_e, dim3(sb_count), dim3(256), 0, s, *dj);
+            SVTME_LAUNCH(svtme::k_stage_b<false>, dim3((bb.total + 3) / 4), 2, bb);
+    }
+    const bool full = h0.job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
+    const DevBatch be = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
+    if (h0.parts) { // wide full-pel stage + per-SB decode
+        const DevBatch bc = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.R * j.parts; });
+        const dim3 grid((bc.total + 3) / 4);
+        const bool k32 = svtme_fp_k32(&h0.job.ctrl);
+        if (full && k32)
+            SVTME_LAUNCH((svtme::k_stage_c1<false, true>), grid, 3, bc);
+        else if (full)
+            SVTME_LAUNCH((svtme::k_stage_c1<false, false>), grid, 3, bc);
+        else if (k32)
+            SVTME_LAUNCH((svtme::k_stage_c1<true, true>), grid, 3, bc);
+        else
+            SVTME_LAUNCH((svtme::k_stage_c1<true, false>), grid, 3, bc);
+        SVTME_LAUNCH(svtme::k_stage_e, dim3(be.total), 4, be);
     } else if (full)
-        hipLaunchKernelGGL(svtme::k_stage_c<false>, dim3(sb_count), dim3(256), 0, s, *dj);
+        SVTME_LAUNCH(svtme::k_stage_c<false>, dim3(be.total), 3, be);
     else
-        hipLaunchKernelGGL(svtme::k_stage_c<true>, dim3(sb_count), dim3(256), 0, s, *dj);
+        SVTME_LAUNCH(svtme::k_stage_c<true>, dim3(be.total), 3, be);
     return hipGetLastError();
 }

@@ -486,8 +486,7 @@ def make_job(width: int, height: int, ctrl: Controls, picture_number: int, refs_
 # Product library (HIP): loaded lazily; raises if absent
 # ----------------------------------------------------------------------------
 def product_lib_path() -> str:
-    # SVTME_LIB selects a diagnostic build (e.g. libsvtme_stamps.so); default is the product
-    return os.path.join(PKG_DIR, os.environ.get("SVTME_LIB", "libsvtme.so"))
+    return os.path.join(PKG_DIR, "libsvtme.so")
 
 
 def load_product():
@@ -504,6 +503,8 @@ def load_product():
         lib.svtme_picture_upload_10bit.restype = C.c_int32
         lib.svtme_picture_upload_device.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
         lib.svtme_picture_upload_device.restype = C.c_int32
+        lib.svtme_picture_invalidate.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
+        lib.svtme_picture_invalidate.restype = C.c_int32
         lib.svtme_picture_release.argtypes = [vp, C.c_uint64]
         lib.svtme_picture_release.restype = C.c_int32
         lib.svtme_picture_download.argtypes = [vp, C.c_uint64, C.c_int, vp, C.POINTER(C.c_uint32),
@@ -521,14 +522,16 @@ def load_product():
         lib.svtme_submit_picture_device.restype = C.c_int32
         lib.svtme_set_timing.argtypes = [vp, C.c_int]
         lib.svtme_set_timing.restype = C.c_int32
-        lib.svtme_kernel_ms.argtypes = [vp]
-        lib.svtme_kernel_ms.restype = C.c_float
-        lib.svtme_stage_ms.argtypes = [vp, C.c_int]
-        lib.svtme_stage_ms.restype = C.c_float
+        lib.svtme_timing_read.argtypes = [vp, C.POINTER(C.c_float)]
+        lib.svtme_timing_read.restype = C.c_uint32
+        lib.svtme_submit_batch_device.argtypes = [vp, C.POINTER(Job), C.c_uint32, C.POINTER(vp), C.POINTER(vp)]
+        lib.svtme_submit_batch_device.restype = C.c_int32
         lib.svtme_device_records.argtypes = [vp, C.POINTER(C.c_uint64)]
         lib.svtme_device_records.restype = vp
         lib.svtme_stream.argtypes = [vp]
         lib.svtme_stream.restype = vp
+        lib.svtme_rtcd_failed.argtypes = []
+        lib.svtme_rtcd_failed.restype = C.c_int
         lib.svtme_last_error.argtypes = []
         lib.svtme_last_error.restype = C.c_char_p
         lib.svtme_derive_controls.argtypes = [C.c_int] * 6 + [C.POINTER(Controls)]
@@ -579,6 +582,13 @@ class GpuME:
         self._check(self.lib.svtme_picture_upload_device(self.ctx, picture_number, dev_ptr, stride, w, h),
                     "svtme_picture_upload_device")
 
+    def invalidate(self, picture_number: int, y: np.ndarray):
+        """The resident picture's planes were replaced (TF re-decimation): rebuild."""
+        y = np.ascontiguousarray(y)
+        h, w = y.shape
+        self._check(self.lib.svtme_picture_invalidate(self.ctx, picture_number, y.ctypes.data, w, w, h),
+                    "svtme_picture_invalidate")
+
     def release(self, picture_number: int):
         self._check(self.lib.svtme_picture_release(self.ctx, picture_number), "svtme_picture_release")
 
@@ -612,12 +622,42 @@ class GpuME:
     def set_timing(self, enable: bool = True):
         self._check(self.lib.svtme_set_timing(self.ctx, 1 if enable else 0), "svtme_set_timing")
 
-    def kernel_ms(self) -> float:
-        return float(self.lib.svtme_kernel_ms(self.ctx))
+    def timing_read(self):
+        """(submissions averaged, [ms of k_stage_a, k_stage_d, k_stage_b, k_stage_c1|c, k_stage_e])
+        over the launches recorded since timing was enabled or last read."""
+        ms = (C.c_float * 5)()
+        n = self.lib.svtme_timing_read(self.ctx, ms)
+        return int(n), [float(v) for v in ms]
 
-    def stage_ms(self, stage: int) -> float:
-        """Last job's time in stage 0 (k_stage_a), 1 (k_stage_d), 2 (k_stage_b) or 3 (k_stage_c)."""
-        return float(self.lib.svtme_stage_ms(self.ctx, stage))
+    def submit_batch_device(self, jobs, d_records, d_sb=None):
+        """One launch per stage over several jobs (device outputs, asynchronous)."""
+        n = len(jobs)
+        arr = (Job * n)(*jobs)
+        recs = (C.c_void_p * n)(*d_records)
+        sbs = (C.c_void_p * n)(*d_sb) if d_sb is not None else None
+        self._check(self.lib.svtme_submit_batch_device(self.ctx, arr, n, recs, sbs), "svtme_submit_batch_device")
+
+    def submit_batch(self, jobs, with_sb_results: bool = True):
+        """Batch submission with host outputs (tests): device buffers via torch."""
+        import torch
+
+        outs, d_recs, d_sb = [], [], []
+        for job in jobs:
+            total = sb_total(job.width, job.height)
+            count = job.sb_count if job.sb_count else total - job.sb_begin
+            r = torch.empty(count * ref_slots(job) * REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+            sb = torch.empty(count * SB_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+            outs.append((r, sb, count, ref_slots(job)))
+            d_recs.append(r.data_ptr())
+            d_sb.append(sb.data_ptr())
+        self.submit_batch_device(jobs, d_recs, d_sb if with_sb_results else None)
+        self.sync()
+        res = []
+        for r, sb, count, R in outs:
+            recs = np.frombuffer(r.cpu().numpy().tobytes(), REF_RECORD_DTYPE).reshape(count, R)
+            sbr = np.frombuffer(sb.cpu().numpy().tobytes(), SB_RESULT_DTYPE).reshape(count) if with_sb_results else None
+            res.append((recs, sbr))
+        return res
 
     def sync(self):
         self._check(self.lib.svtme_sync(self.ctx), "svtme_sync")

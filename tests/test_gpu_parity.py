@@ -180,3 +180,34 @@ def test_banded_fullpel_parity(svtme, gpu):
     assert not _controls_case(S, gpu, S.derive_controls(8, 35, S.input_resolution_of(640, 360), 1), 640, 360,
                               (7, 6), (9, 10))
     assert not _controls_case(S, gpu, ctrl, 640, 360, (7,), ())
+
+
+def test_picture_invalidate(svtme, gpu):
+    """svtme_picture_invalidate (TF re-decimation, temporal_filtering.c:3895-3931):
+    the resident pyramid is rebuilt from the new planes, jobs queued before it
+    read the old planes, jobs after it the new ones; a non-resident picture is
+    refused."""
+    S = svtme
+    w, h = 320, 192
+    syn = S.Synth(w, h)
+    old, new = syn.frame(7), syn.frame(11)
+    cur, ref9 = syn.frame(8), syn.frame(9)
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    for pn, f in ((3008, cur), (3007, old), (3009, ref9)):
+        gpu.upload(pn, f)
+    job = S.make_job(w, h, ctrl, 3008, (3007,), (3009,), temporal_layer_index=1, ref_count_used=(1, 1))
+    before = gpu.submit(job)
+    gpu.invalidate(3007, new)
+    after = gpu.submit(job)
+    p_new = S.build_host_pyramid(new, "oracle")
+    for lv, name in enumerate(("full", "quarter", "sixteenth")):
+        assert np.array_equal(gpu.download(3007, lv), getattr(p_new, name)), name
+    pyr = {8: S.build_host_pyramid(cur, "oracle"), 9: S.build_host_pyramid(ref9, "oracle")}
+    for ref7, got in ((S.build_host_pyramid(old, "oracle"), before), (p_new, after)):
+        orecs, osbr = S.run_checker(job, pyr[8], {(0, 0): ref7, (1, 0): pyr[9]}, "oracle", nthreads=8)
+        assert not S.compare_records(orecs, got[0], osbr, got[1])
+    assert not S.compare_records(before[0], after[0]) == []  # the new planes changed the result
+    with pytest.raises(RuntimeError):
+        gpu.invalidate(123456, new)
+    for pn in (3007, 3008, 3009):
+        gpu.release(pn)
