@@ -70,13 +70,27 @@ def host_cores():
     return n
 
 
+def kernel_code_sha():
+    """sha256 of the device sources of the ME pass (stage kernels + shared headers)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in ("svtme_stages.hip", "svtme_me_common.h", "svtme_device.h"):
+        with open(os.path.join(ROOT, "svt-av1-mirror_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def latest_profile(workload):
-    """pmc_summary.json of the newest profiles/r*_<workload>/ (this round's code)."""
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}", "pmc_summary.json")))
-    if not paths:
-        return None, None
-    with open(paths[-1]) as fh:
-        return json.load(fh), os.path.relpath(paths[-1], ROOT)
+    """pmc_summary.json under profiles/*_<workload>/ taken on THIS build's stage
+    kernels (same code_sha), or (None, None)."""
+    sha = kernel_code_sha()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{workload}", "pmc_summary.json"))):
+        with open(path) as fh:
+            prof = json.load(fh)
+        if prof.get("code_sha") == sha:
+            return prof, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():

@@ -11,6 +11,9 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import kernel_code_sha  # noqa: E402
+
 
 def main(out):
     per = defaultdict(list)
@@ -45,6 +48,7 @@ def main(out):
         res["workload"] = b["config"].get("name")
     except (OSError, ValueError, KeyError, IndexError):
         pass
+    res["code_sha"] = kernel_code_sha()  # the stage sources these counters were taken on
     if "FETCH_SIZE" in avg:
         res["fetch_bytes_corrected"] = avg["FETCH_SIZE"] * 1024 * 2
     if "WRITE_SIZE" in avg:
