@@ -50,10 +50,11 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level paramete
 # v_sad_u8: 4 absdiffs per lane, 64 lanes per CU per clock, 256 CUs, 2.4 GHz
 SAD_PEAK_T = 4 * 64 * 256 * 2.4e9 / 1e12
 STAGES = ("k_stage_a", "k_stage_d", "k_stage_b", "k_stage_c1", "k_stage_e")
+STAGES_FUSED = ("k_hme", "-", "-", "k_stage_c1", "k_stage_e")  # k_hme = stages A + D + B in one launch
 # SURVEY.md 8(d) p8 byte split over the stage kernels: zz 2048 + pre-HME 2645 + 1034 +
 # HME-L0 1081 (+ source 64x32 + 16x8) | HME-L1 5304 (+ source 32x16) | full-pel 4686 + 680 out
 STAGE_BYTES_P8 = {"k_stage_a": (2176, 6808), "k_stage_d": (0, 0), "k_stage_b": (512, 5304),
-                  "k_stage_c1": (0, 4686), "k_stage_e": (0, 680)}
+                  "k_stage_c1": (0, 4686), "k_stage_e": (0, 680), "k_hme": (2688, 12112)}
 PICTURE_STRIDE = 32  # picture p of a step pans from t = 8 + 32 p (distinct content per picture)
 
 
@@ -208,7 +209,9 @@ def main():
     bytes_launch = bps * sbs_launch
     achieved = bytes_launch / (device_ms * 1e-3) / 1e9
     stages = {}
-    for k, st in enumerate(STAGES):
+    fused = stage_ms[0] > 0 and stage_ms[1] <= 0 and stage_ms[2] <= 0
+    names = STAGES_FUSED if fused else STAGES
+    for k, st in enumerate(names):
         if stage_ms[k] <= 0:
             continue
         e = {"avg_ms": round(stage_ms[k], 4), "share": round(stage_ms[k] / kern_ms, 3)}
@@ -259,8 +262,8 @@ def main():
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "ME pass: k_stage_a -> k_stage_d -> k_stage_b -> k_stage_c1 -> k_stage_e "
-                                   "(one launch each, back to back on the library stream)",
+                         "kernel": "ME pass: " + " -> ".join(n for n in names if n != "-") +
+                                   " (one launch each, back to back on the library stream)",
                          "pass_ms": round(device_ms, 4), "kernel_sum_ms": round(kern_ms, 4),
                          "kernel_samples": n_timed,
                          "bytes_per_launch": bytes_launch, "sbs_per_launch": sbs_launch,

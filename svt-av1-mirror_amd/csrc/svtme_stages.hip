@@ -29,6 +29,7 @@
 // strict-< first-minimum scan order (compute_sad_c.c:90,
 // motion_estimation.c:137-425) falls out of an integer min.
 #include <hip/hip_ext.h>
+#include <cstdlib>
 #include <type_traits>
 
 #include "svtme_me_common.h"
@@ -608,23 +609,10 @@ struct Dec {
     uint64_t lsad[8][4];
 };
 
-__global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
-    __shared__ Dec dec[4];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
-    if (u >= B.total)
-        return;
-    uint32_t sb_local;
-    const DevJob &dj        = batch_job(B, u, &sb_local);
-    const svtme_job &job    = dj.job;
-    const svtme_controls &c = job.ctrl;
-    Dec &d               = dec[wid];
-    const SbGeo G        = sb_geo(dj, sb_local);
-    const int nl         = job.num_lists;
-    const uint32_t vmask = valid_mask(job);
-    if (lane < SVTME_A_N)
-        d.a[lane] = dj.ares[(size_t)sb_local * SVTME_A_N + lane];
-    if (lane < 8) { // init_me_hme_data (motion_estimation.c:3010-3070)
+// init_me_hme_data (motion_estimation.c:3010-3070) of the decision state
+__device__ __forceinline__ void dec_init(Dec &d) {
+    const int lane = threadIdx.x & 63;
+    if (lane < 8) {
         d.do_ref[lane] = 1;
         d.zz[lane]     = U32MAX;
         for (int k = 0; k < 2; k++) {
@@ -640,8 +628,13 @@ __global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
         (&d.lsad[0][0])[lane] = 0;
     }
     wave_lds_fence();
+}
 
-    // ---- init_zz_sad decisions (motion_estimation.c:2382-2437)
+// init_zz_sad decisions (motion_estimation.c:2382-2437), one wavefront
+__device__ __forceinline__ void dec_zz(Dec &d, const svtme_job &job, const SbGeo &G, uint32_t vmask) {
+    const svtme_controls &c = job.ctrl;
+    const int lane          = threadIdx.x & 63;
+    const int nl            = job.num_lists;
     if (c.me_early_exit_th || c.me_safe_limit_zz_th) {
         const int s = lane;
         uint32_t zz = U32MAX;
@@ -665,7 +658,13 @@ __global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
         }
         wave_lds_fence();
     }
-    // ---- pre-HME decisions (motion_estimation.c:1693-1796), list 0 then list 1
+}
+
+// pre-HME decisions (motion_estimation.c:1693-1796), list 0 then list 1, one wavefront
+__device__ __forceinline__ void dec_prehme(Dec &d, const svtme_job &job, uint32_t vmask) {
+    const svtme_controls &c = job.ctrl;
+    const int lane          = threadIdx.x & 63;
+    const int nl            = job.num_lists;
     if (c.prehme_enable) {
         for (int l = 0; l < nl; l++) {
             const int r = lane >> 1, sr = lane & 1, s = l * 4 + r;
@@ -723,7 +722,12 @@ __global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
             d.do_ref[s] = 0;
         wave_lds_fence();
     }
-    // ---- HME level 0 decisions (motion_estimation.c:1906-2036)
+}
+
+// HME level 0 decisions (motion_estimation.c:1906-2036), one wavefront
+__device__ __forceinline__ void dec_l0(Dec &d, const svtme_job &job, uint32_t vmask) {
+    const svtme_controls &c = job.ctrl;
+    const int lane          = threadIdx.x & 63;
     if (c.enable_hme_flag && c.enable_hme_level0_flag) {
         const int s = lane >> 2, q = lane & 3;
         bool searched = false;
@@ -779,6 +783,26 @@ __global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
         }
         wave_lds_fence();
     }
+}
+
+__global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
+    __shared__ Dec dec[4];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total)
+        return;
+    uint32_t sb_local;
+    const DevJob &dj     = batch_job(B, u, &sb_local);
+    const svtme_job &job = dj.job;
+    Dec &d               = dec[wid];
+    const SbGeo G        = sb_geo(dj, sb_local);
+    const uint32_t vmask = valid_mask(job);
+    if (lane < SVTME_A_N)
+        d.a[lane] = dj.ares[(size_t)sb_local * SVTME_A_N + lane];
+    dec_init(d);
+    dec_zz(d, job, G, vmask);
+    dec_prehme(d, job, vmask);
+    dec_l0(d, job, vmask);
     BState *b = dj.bst + sb_local;
     if (lane < 32) {
         (&b->lx[0][0])[lane]   = (&d.lx[0][0])[lane];
@@ -985,6 +1009,488 @@ __device__ __forceinline__ SlotCentre final_centre(const DevJob &dj, uint32_t sb
     o.sc_y       = valid ? my_scy : 0;
     o.do_ref     = dref;
     return o;
+}
+
+// ----------------------------------------------------------------------------
+// k_hme: stages A, D and B of one SB fused in one workgroup (4 wavefronts).
+// Used when every SB of the job is 64 wide, the HME searches sub-sample rows
+// (hme_search_method SUB_SAD) and level 2 is off (svtme_hme_fused); other jobs
+// run k_stage_a -> k_stage_d -> k_stage_b. Both write the same BState.
+//
+//   A0  zz SADs of every slot (init_zz_sad), then the zz decisions, so that
+//       pre-HME / level-0 searches the reference provably skips (zz early exit,
+//       zz pruning) are never run;
+//   A1  the pre-HME regions and HME-L0 quadrants, as register tiles: a lane
+//       owns HQ aligned position quads x HT position rows 2 plane rows apart
+//       (the sub-sampled block's rows), so each loaded reference row feeds up
+//       to 8 block rows x 12 positions; the 16x16 (sub: 16x8) source block
+//       sits in SGPRs. Tile minima merge with ds_min_u64 per search;
+//   D   the pre-HME and level-0 decisions (dec_prehme, dec_l0);
+//   B   HME-L1: a lane owns HQ quads of one position row of one (slot,
+//       quadrant) search, the 32x16 (sub) source block in LDS.
+// Keys inside a tile are 32-bit (sad << 16 | x, one v_lshl_or / v_and_or and
+// a v_min3 per position pair); the row, then the lane's best widen to the
+// 64-bit sad << 32 | y << 16 | x order of the reference's scan.
+// ----------------------------------------------------------------------------
+#define HT 4 // position rows per 1/16 tile
+#define HQ 3 // position quads per tile
+
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+// 16 bytes at a dword-aligned global address (the planes are global memory)
+__device__ __forceinline__ u32x4a4 ldg4(const uint32_t *p) {
+    typedef __attribute__((address_space(1))) const u32x4a4 gu4;
+    return *(gu4 *)(uintptr_t)p;
+}
+// 16 uniform bytes through the scalar cache (p wave-uniform, 4-byte aligned)
+__device__ __forceinline__ uint4 sld4(const uint8_t *p) {
+    typedef __attribute__((address_space(4))) const uint32_t cu32;
+    cu32 *q = (cu32 *)(uintptr_t)p;
+    return make_uint4(q[0], q[1], q[2], q[3]);
+}
+__device__ __forceinline__ unsigned long long qsad64(unsigned long long ref, uint32_t s, unsigned long long a) {
+    return __builtin_amdgcn_qsad_pk_u16_u8(ref, s, a);
+}
+__device__ __forceinline__ unsigned long long pair(uint32_t lo, uint32_t hi) {
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+struct HSrch {             // one 1/16-resolution search (pre-HME region or HME-L0 quadrant)
+    const uint8_t *a0;     // dword-aligned plane address of window dword 0, position row 0
+    int32_t item0;         // first tile of this search in the SB's tile list
+    int16_t sa_w, ncols;   // positions per row; tile columns
+    int16_t cnt0, cnt1;    // position rows of each tile-row parity (skip: cnt0 = rows, cnt1 = 0)
+    int16_t ylast;         // last plane-row offset a tile of this search may read
+    uint8_t sh, skip, id;  // byte offset of position 0; odd rows only; ARes index
+};
+struct HSrch1 {            // one HME-L1 refinement search
+    const uint8_t *a0;
+    int32_t item0;
+    int16_t sa_w, ncols;
+    uint8_t sh, id;        // id = slot * 4 + quadrant
+};
+
+struct HmeSh {
+    Dec d;
+    unsigned long long key[SVTME_A_N]; // search minima by ARes index
+    int16_t kxo[SVTME_A_N], kyo[SVTME_A_N];
+    uint32_t zzacc[8];
+    uint8_t ph_need[8], l0_need[8];
+    HSrch srch[48];
+    int32_t nsrch, nitems;
+    unsigned long long key1[32];
+    int16_t x1o[32], y1o[32];
+    HSrch1 s1[32];
+    int32_t nsrch1, nitems1;
+    int16_t hx[32], hy[32];
+    uint64_t hsad[32];
+    __attribute__((aligned(16))) uint8_t src4[16][32]; // quarter-resolution source, sub rows
+};
+
+// SADs of the 16 x kh (sub) source block sr at an HT x HQ tile of positions of
+// a 1/16 window: quads q0.. of row a0 (sh = byte offset of position 0),
+// position rows yf + 2t (t < tv); plane rows are clamped to ylast. Returns
+// the tile's minimum key (sad << 32 | y << 16 | x), ~0 if no position is valid.
+__device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
+                                                         int yf, int tv, int ylast, int kh,
+                                                         const uint32_t (&sr)[8][4]) {
+    unsigned long long acc[HT][HQ];
+#pragma unroll
+    for (int t = 0; t < HT; t++)
+#pragma unroll
+        for (int qq = 0; qq < HQ; qq++) acc[t][qq] = 0;
+#pragma unroll
+    for (int m = 0; m < HT + 7; m++) {
+        const int ro       = min(yf + 2 * m, ylast);
+        const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)ro * stride) + q0;
+        const u32x4a4 lo = ldg4(rp), hi = ldg4(rp + 4);
+        const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        unsigned long long P[HQ + 3];
+#pragma unroll
+        for (int j = 0; j < HQ + 3; j++) P[j] = pair(d[j], d[j + 1]);
+#pragma unroll
+        for (int t = 0; t < HT; t++) {
+            const int k = m - t;
+            if (k < 0 || k >= 8)
+                continue;
+            if (k >= kh) // wave-uniform (partial-height SB)
+                continue;
+#pragma unroll
+            for (int qq = 0; qq < HQ; qq++)
+#pragma unroll
+                for (int j = 0; j < 4; j++) acc[t][qq] = qsad64(P[qq + j], sr[k][j], acc[t][qq]);
+        }
+    }
+    uint32_t xo[HQ][4];
+#pragma unroll
+    for (int qq = 0; qq < HQ; qq++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int x = 4 * (q0 + qq) - sh + e;
+            xo[qq][e]   = (x >= 0 && x < sa_w) ? (uint32_t)x : U32MAX;
+        }
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (int t = 0; t < HT; t++) {
+        uint32_t mt = U32MAX;
+#pragma unroll
+        for (int qq = 0; qq < HQ; qq++) {
+            const uint32_t lo = (uint32_t)acc[t][qq], hi = (uint32_t)(acc[t][qq] >> 32);
+            const uint32_t k0 = (lo << 16) | xo[qq][0], k1 = (lo & 0xFFFF0000u) | xo[qq][1];
+            const uint32_t k2 = (hi << 16) | xo[qq][2], k3 = (hi & 0xFFFF0000u) | xo[qq][3];
+            mt = min_u32(mt, min_u32(min_u32(k0, k1), min_u32(k2, k3)));
+        }
+        if (t < tv && mt != U32MAX) {
+            const unsigned long long kk = ((unsigned long long)(mt >> 16) << 32) |
+                                          ((unsigned long long)(uint32_t)(yf + 2 * t) << 16) | (mt & 0xFFFFu);
+            best = kk < best ? kk : best;
+        }
+    }
+    return best;
+}
+
+// SADs of the 32 x kh1 (sub) quarter-resolution source block (LDS, rows 32
+// bytes apart) at HQ quads of position row y of a 1/4 window. u16 lanes hold
+// 8 block rows (8 x 8 x 1020 < 2^16), then widen.
+__device__ __forceinline__ unsigned long long hme_tile32(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
+                                                         int y, int kh1, const uint8_t (*src)[32]) {
+    uint32_t a32[HQ][4];
+#pragma unroll
+    for (int qq = 0; qq < HQ; qq++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) a32[qq][e] = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        unsigned long long acc[HQ] = {0, 0, 0};
+#pragma unroll
+        for (int kk = 0; kk < 8; kk++) {
+            const int k = h * 8 + kk;
+            if (k >= kh1) // wave-uniform
+                break;
+            const uint4 s0 = ((const uint4 *)src[k])[0], s1 = ((const uint4 *)src[k])[1];
+            const uint32_t sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+            const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)(y + 2 * k) * stride) + q0;
+            const u32x4a4 l0 = ldg4(rp), l1 = ldg4(rp + 4), l2 = ldg4(rp + 8);
+            const uint32_t d[12] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w, l2.x, l2.y, l2.z, l2.w};
+#pragma unroll
+            for (int qq = 0; qq < HQ; qq++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) acc[qq] = qsad64(pair(d[qq + j], d[qq + j + 1]), sv[j], acc[qq]);
+        }
+#pragma unroll
+        for (int qq = 0; qq < HQ; qq++) qsad_unpack(acc[qq], a32[qq]);
+    }
+    uint32_t mt = U32MAX; // sad (< 2^17) << 15 | x (< 2^15)
+#pragma unroll
+    for (int qq = 0; qq < HQ; qq++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int x = 4 * (q0 + qq) - sh + e;
+            if (x >= 0 && x < sa_w)
+                mt = min_u32(mt, (a32[qq][e] << 15) | (uint32_t)x);
+        }
+    if (mt == U32MAX)
+        return ~0ull;
+    return ((unsigned long long)(mt >> 15) << 32) | ((unsigned long long)(uint32_t)y << 16) | (mt & 0x7FFFu);
+}
+
+// flat tile index -> search (binary search over item0, n > 0 searches)
+template <typename S>
+__device__ __forceinline__ int find_search(const S *t, int n, int it) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (t[mid].item0 <= it)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
+    __shared__ HmeSh sh;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint32_t sb_local;
+    const DevJob &dj        = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const SbGeo G           = sb_geo(dj, sb_local);
+    const uint32_t vmask    = valid_mask(job);
+    Dec &d                  = sh.d;
+    const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
+    const int kh  = (int)(G.bh >> 2) >> 1; // 1/16 block rows (sub)
+    const int kh1 = (int)(G.bh >> 2);      // 1/4 block rows (sub): (bh / 2) / 2
+
+    // ---- A0: zz SADs (init_zz_sad, motion_estimation.c:2382-2437): thread = slot x sub row
+    const bool zz_on = c.me_early_exit_th || c.me_safe_limit_zz_th;
+    if (tid < 8)
+        sh.zzacc[tid] = 0;
+    if (wid == 0) {
+        dec_init(d);
+    }
+    __syncthreads();
+    if (zz_on) {
+        const int s = tid >> 5, r = tid & 31;
+        if (slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && r < (int)(G.bh >> 1)) {
+            const DevPlane &F = dj.ref[s >> 2][s & 3].lv[0];
+            const DevPlane &C = dj.cur.lv[0];
+            const uint32_t *rr = (const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * r) * F.stride + G.ox);
+            const uint32_t *cr = (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox);
+            uint32_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < 16; j += 4) {
+                const uint4 a = *(const uint4 *)(rr + j), b = *(const uint4 *)(cr + j);
+                acc = __builtin_amdgcn_sad_u8(a.x, b.x, acc);
+                acc = __builtin_amdgcn_sad_u8(a.y, b.y, acc);
+                acc = __builtin_amdgcn_sad_u8(a.z, b.z, acc);
+                acc = __builtin_amdgcn_sad_u8(a.w, b.w, acc);
+            }
+            atomicAdd(&sh.zzacc[s], acc);
+        }
+    }
+    __syncthreads();
+    // ---- zz decisions, then the A1 search table (wave 0)
+    if (wid == 0) {
+        if (lane < 8)
+            d.a[SVTME_A_ZZ + lane] = ARes{sh.zzacc[lane], 0, 0};
+        wave_lds_fence();
+        dec_zz(d, job, G, vmask);
+        if (lane < 8) {
+            const int s    = lane;
+            const bool act = slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && d.do_ref[s];
+            sh.ph_need[s]  = act && c.prehme_enable && !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th);
+            sh.l0_need[s]  = act && c.enable_hme_flag && c.enable_hme_level0_flag &&
+                            !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2));
+        }
+        if (lane < SVTME_A_N)
+            sh.key[lane] = ~0ull;
+        wave_lds_fence();
+        // lane = slot * 6 + k: k < 2 pre-HME region k, else HME-L0 quadrant k - 2
+        const int s = lane / 6, k = lane - 6 * (lane / 6), l = s >> 2, r = s & 3;
+        bool mk = false;
+        HSrch e;
+        int items = 0;
+        if (lane < 48 && ((k < 2) ? sh.ph_need[s] : sh.l0_need[s])) {
+            const DevPlane &P   = dj.ref[l][r].lv[2];
+            const uint16_t dist = ref_dist_const(job, l, r);
+            int16_t xo, yo, sw, shh;
+            bool skip;
+            if (k < 2) { // prehme_core (motion_estimation.c:1568-1636)
+                const uint32_t f    = scaled_dist(dist);
+                const uint16_t sa_w = (uint16_t)min((uint32_t)c.prehme_sa_cfg[k].sa_min.width * f,
+                                                    (uint32_t)c.prehme_sa_cfg[k].sa_max.width);
+                const uint16_t sa_h = (uint16_t)min((uint32_t)c.prehme_sa_cfg[k].sa_min.height * f,
+                                                    (uint32_t)c.prehme_sa_cfg[k].sa_max.height);
+                prehme_area(P, sox, soy, (int16_t)sa_w, (int16_t)sa_h, &xo, &yo, &sw, &shh);
+                skip = c.prehme_skip_search_line != 0; // compute_sad_c.c:74 (16-wide, <= 16 rows)
+                e.id = (uint8_t)(SVTME_A_PH + s * 2 + k);
+            } else { // hme_level_0 (motion_estimation.c:835-889)
+                int16_t saw, sah;
+                hme_l0_area(c, l, r, dist, 0, 0, &saw, &sah);
+                hme_l0_rect(c, P, sox, soy, saw, sah, (k - 2) >> 1, (k - 2) & 1, &xo, &yo, &sw, &shh);
+                skip = false;
+                e.id = (uint8_t)(SVTME_A_L0 + s * 4 + (k - 2));
+            }
+            sh.kxo[e.id] = xo;
+            sh.kyo[e.id] = yo;
+            const int nrows = (sw > 0 && shh > 0) ? (skip ? shh / 2 : shh) : 0;
+            if (nrows > 0) {
+                const uint8_t *w0 = P.base + (ptrdiff_t)(soy + yo) * P.stride + (sox + xo);
+                e.sh              = (uint8_t)((uintptr_t)w0 & 3);
+                e.a0              = w0 - e.sh;
+                e.sa_w            = sw;
+                e.skip            = skip;
+                const int nq      = (e.sh + sw + 3) >> 2;
+                e.ncols           = (int16_t)((nq + HQ - 1) / HQ);
+                if (skip) {
+                    e.cnt0  = (int16_t)nrows;
+                    e.cnt1  = 0;
+                    e.ylast = (int16_t)(2 * nrows - 1 + 2 * (kh - 1));
+                    items   = e.ncols * ((nrows + HT - 1) / HT);
+                } else {
+                    e.cnt0  = (int16_t)((nrows + 1) >> 1);
+                    e.cnt1  = (int16_t)(nrows >> 1);
+                    e.ylast = (int16_t)(nrows - 1 + 2 * (kh - 1));
+                    items   = e.ncols * 2 * ((e.cnt0 + HT - 1) / HT);
+                }
+                mk = true;
+            }
+        }
+        int tot;
+        const int kpos  = wave_compact(mk, &tot);
+        const int incl  = wave_incl_scan(items);
+        if (mk) {
+            e.item0         = incl - items;
+            sh.srch[kpos]   = e;
+        }
+        if (lane == 63)
+            sh.nitems = incl;
+        if (lane == 0)
+            sh.nsrch = tot;
+    }
+    // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs
+    uint32_t sr[8][4];
+    {
+        const DevPlane &S = dj.cur.lv[2];
+        const uint8_t *sp = uni_ptr(S.base + (ptrdiff_t)soy * S.stride + sox);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * S.stride);
+            sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
+        }
+    }
+    // quarter-resolution source block (32 x 32, even rows) into LDS for HME-L1
+    if (c.enable_hme_level1_flag && tid < 32) {
+        const DevPlane &Q = dj.cur.lv[1];
+        const int row = tid >> 1, half = tid & 1;
+        ((uint4 *)sh.src4[row])[half] =
+            *(const uint4 *)(Q.base + (ptrdiff_t)((G.oy >> 1) + 2 * row) * Q.stride + (G.ox >> 1) + 16 * half);
+    }
+    __syncthreads();
+    // ---- A1: pre-HME regions and HME-L0 quadrants, one HT x HQ tile per thread
+    {
+        const int nitems = sh.nitems, nsrch = sh.nsrch;
+        const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
+        for (int it = tid; it < nitems; it += 256) {
+            const HSrch &e  = sh.srch[find_search(sh.srch, nsrch, it)];
+            const int local = it - e.item0;
+            const int rt = local / e.ncols, col = local - rt * e.ncols;
+            int yf, tv;
+            if (e.skip) {
+                yf = 8 * rt + 1;
+                tv = min(HT, e.cnt0 - HT * rt);
+            } else {
+                const int p = rt & 1, i = rt >> 1;
+                yf = 8 * i + p;
+                tv = min(HT, (p ? e.cnt1 : e.cnt0) - HT * i);
+            }
+            if (tv <= 0)
+                continue;
+            const unsigned long long kk =
+                hme_tile16(e.a0, pstride, HQ * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
+            if (kk != ~0ull)
+                atomicMin(&sh.key[e.id], kk);
+        }
+    }
+    __syncthreads();
+    // ---- D: pre-HME and level-0 decisions, then the HME-L1 table (wave 0)
+    const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH; // true on this path
+    if (wid == 0) {
+        if (lane < SVTME_A_N && lane >= SVTME_A_PH) {
+            uint32_t best;
+            int x, y;
+            key_result(sh.key[lane], &best, &x, &y);
+            d.a[lane] = ARes{hsub ? best * 2 : best, i16((x + sh.kxo[lane]) * 4), i16((y + sh.kyo[lane]) * 4)};
+        }
+        wave_lds_fence();
+        dec_prehme(d, job, vmask);
+        dec_l0(d, job, vmask);
+        // HME-L1 per (slot, quadrant), lane = slot * 4 + q (hme_level1_b64, :2041-2122)
+        const int s = lane >> 2, q = lane & 3, l = s >> 2, r = s & 3;
+        bool mk   = false;
+        int items = 0;
+        HSrch1 e;
+        if (lane < 32) {
+            int16_t X = 0, Y = 0;
+            uint64_t SD = 0;
+            sh.key1[lane] = ~0ull;
+            const bool listed = c.enable_hme_flag && c.enable_hme_level1_flag && slot_valid(vmask, s) &&
+                                tl_or_l0(job, l);
+            if (listed) {
+                const int16_t X0 = d.lx[s][q], Y0 = d.ly[s][q];
+                const uint64_t S0 = d.lsad[s][q];
+                bool done = false;
+                if (c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2)) {
+                    X = Y = 0;
+                    SD   = 0;
+                    done = true;
+                }
+                if (!done && !d.do_ref[s]) {
+                    X = Y = 0;
+                    SD   = U32MAX;
+                    done = true;
+                }
+                if (!done && c.prev_me_stage_based_exit_th && S0 < (c.prev_me_stage_based_exit_th >> 5)) {
+                    X = X0, Y = Y0, SD = S0;
+                    done = true;
+                }
+                if (!done) { // hme_level_1 (motion_estimation.c:923-1022)
+                    const DevPlane &P = dj.ref[l][r].lv[1];
+                    const int16_t qx = i16(((int16_t)G.ox) >> 1), qy = i16(((int16_t)G.oy) >> 1);
+                    int16_t xo, yo, sw, shh;
+                    hme_refine_rect(1, P, qx, qy, (int16_t)c.hme_l1_sa.width, (int16_t)c.hme_l1_sa.height,
+                                    i16(X0 >> 1), i16(Y0 >> 1), &xo, &yo, &sw, &shh);
+                    sh.x1o[lane] = xo;
+                    sh.y1o[lane] = yo;
+                    SD           = ~0ull; // searched: resolved from key1 below
+                    if (sw > 0 && shh > 0 && kh1 > 0) {
+                        const uint8_t *w0 = P.base + (ptrdiff_t)(qy + yo) * P.stride + (qx + xo);
+                        e.sh              = (uint8_t)((uintptr_t)w0 & 3);
+                        e.a0              = w0 - e.sh;
+                        e.sa_w            = sw;
+                        e.ncols           = (int16_t)((((e.sh + sw + 3) >> 2) + HQ - 1) / HQ);
+                        e.id              = (uint8_t)lane;
+                        items             = e.ncols * shh;
+                        mk                = true;
+                    }
+                }
+            }
+            sh.hx[lane]   = X;
+            sh.hy[lane]   = Y;
+            sh.hsad[lane] = SD;
+        }
+        int tot;
+        const int kpos = wave_compact(mk, &tot);
+        const int incl = wave_incl_scan(items);
+        if (mk) {
+            e.item0        = incl - items;
+            sh.s1[kpos]    = e;
+        }
+        if (lane == 63)
+            sh.nitems1 = incl;
+        if (lane == 0)
+            sh.nsrch1 = tot;
+    }
+    __syncthreads();
+    // ---- B: HME-L1 tiles
+    {
+        const int nitems = sh.nitems1, nsrch = sh.nsrch1;
+        const int pstride = dj.cur.lv[1].stride;
+        for (int it = tid; it < nitems; it += 256) {
+            const HSrch1 &e = sh.s1[find_search(sh.s1, nsrch, it)];
+            const int local = it - e.item0;
+            const int y = local / e.ncols, col = local - y * e.ncols;
+            const unsigned long long kk = hme_tile32(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh1, sh.src4);
+            if (kk != ~0ull)
+                atomicMin(&sh.key1[e.id], kk);
+        }
+    }
+    __syncthreads();
+    if (wid == 0) {
+        BState *b = dj.bst + sb_local;
+        if (lane < 32) {
+            int16_t X = sh.hx[lane], Y = sh.hy[lane];
+            uint64_t SD = sh.hsad[lane];
+            if (SD == ~0ull) { // searched (hme_level_1 result, full-pel x 2)
+                uint32_t best;
+                int x, y;
+                key_result(sh.key1[lane], &best, &x, &y);
+                SD = hsub ? (uint64_t)best * 2 : best;
+                X  = i16((x + sh.x1o[lane]) * 2);
+                Y  = i16((y + sh.y1o[lane]) * 2);
+            }
+            b->hx[0][lane]            = X;
+            b->hy[0][lane]            = Y;
+            b->hsad[0][lane]          = SD;
+            (&b->lx[0][0])[lane]   = (&d.lx[0][0])[lane];
+            (&b->ly[0][0])[lane]   = (&d.ly[0][0])[lane];
+            (&b->lsad[0][0])[lane] = (&d.lsad[0][0])[lane];
+        }
+        if (lane < 8) {
+            b->zz[lane]     = d.zz[lane];
+            b->do_ref[lane] = d.do_ref[lane];
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -2136,6 +2642,13 @@ static void fp_area_bound(const svtme_controls *c, uint32_t *w, uint32_t *h) {
     *h = mh;
 }
 
+// k_hme applies: every SB 64 wide, sub-sampled HME rows, level 2 off
+extern "C" bool svtme_hme_fused(const svtme_job *job) {
+    const svtme_controls &c = job->ctrl;
+    return (job->width % 64) == 0 && c.hme_search_method != SVTME_FULL_SAD_SEARCH && !c.enable_hme_level2_flag &&
+           getenv("SVTME_NO_FUSED_HME") == nullptr;
+}
+
 extern "C" bool svtme_fp_k32(const svtme_controls *c) {
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
@@ -2156,7 +2669,7 @@ extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {
 extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
     const bool full = dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     return (uint32_t)full | (uint32_t)(dj->parts != 0) << 1 | (uint32_t)svtme_fp_k32(&dj->job.ctrl) << 2 |
-           (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3;
+           (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4;
 }
 
 static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
@@ -2195,10 +2708,13 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     const DevJob &h0 = h_jobs[0];
     if (mask)
         *mask = 0;
+    const DevBatch bd = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
+    if (svtme_hme_fused(&h0.job)) {
+        SVTME_LAUNCH(svtme::k_hme, dim3(bd.total), 0, bd);
+    } else {
     const DevBatch ba = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta_count; });
     if (ba.total)
         SVTME_LAUNCH(svtme::k_stage_a, dim3((ba.total + 3) / 4), 0, ba);
-    const DevBatch bd = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
     SVTME_LAUNCH(svtme::k_stage_d, dim3((bd.total + 3) / 4), 1, bd);
     const DevBatch bb = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.tb_count; });
     if (bb.total) {
@@ -2206,6 +2722,7 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
             SVTME_LAUNCH(svtme::k_stage_b<true>, dim3((bb.total + 3) / 4), 2, bb);
         else
             SVTME_LAUNCH(svtme::k_stage_b<false>, dim3((bb.total + 3) / 4), 2, bb);
+    }
     }
     const bool full = h0.job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     const DevBatch be = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
