@@ -1,0 +1,68 @@
+"""Per-phase timing of k_hme from a diagnostic build (-DSVTME_STAMPS).
+
+Build (container):  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DSVTME_STAMPS \
+    -o svt-av1-mirror_amd/libsvtme_stamp.so svt-av1-mirror_amd/csrc/*.hip svt-av1-mirror_amd/csrc/svtme_host.cpp
+Run (GPU box):      python3 scripts/hme_stamps.py [workload] [pictures]
+
+Thread 0 of every k_hme workgroup stamps the shader clock at 7 points: start,
+after A0 (zz), after the A1 table, after A1 tiles, after D + L1 table, after
+the L1 tiles, end. Prints per-phase cycle statistics and the launch span.
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ.setdefault("SVTME_LIB", os.path.join(ROOT, "svt-av1-mirror_amd", "libsvtme_stamp.so"))
+sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
+
+import svtme as S  # noqa: E402
+import workloads as W  # noqa: E402
+
+PHASES = ["A0 zz", "A1 table", "A1 tiles", "D + L1 table", "L1 tiles", "store"]
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "4k_p8"
+    P = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    wl = W.WORKLOADS[name]
+    import torch
+
+    torch.cuda.set_device(0)  # torch first (as bench.py), then the library's context
+    gpu = S.GpuME(0)
+    syn = S.Synth(wl["w"], wl["h"])
+    jobs = []
+    for p in range(P):
+        for t in sorted(set((8,) + tuple(wl["l0"]) + tuple(wl["l1"]))):
+            gpu.upload(t + 32 * p, syn.frame(t))
+        jobs.append(W.workload_job(name, base=32 * p))
+    n_sb = S.sb_total(wl["w"], wl["h"])
+
+    R = S.ref_slots(jobs[0])
+    bufs = [torch.zeros(n_sb * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for _ in jobs]
+    for _ in range(5):
+        gpu.submit_batch_device(jobs, [b.data_ptr() for b in bufs])
+    gpu.sync()
+    lib = S.load_product()
+    nb = n_sb * P
+    st = np.zeros((nb, 8), np.uint64)
+    fn = lib.svtme_debug_hme_stamps
+    fn.argtypes = [C.c_void_p, C.c_uint32]
+    fn.restype = C.c_int
+    assert fn(st.ctypes.data, nb) == 0
+    st = st[:, :7].astype(np.int64)
+    d = np.diff(st, axis=1)
+    print(f"{name} x{P}: {nb} workgroups, launch span {st[:, 6].max() - st[:, 0].min()} cycles "
+          f"(first start -> last end), per-WG total mean {np.mean(st[:, 6] - st[:, 0]):.0f}")
+    for k, ph in enumerate(PHASES):
+        v = d[:, k]
+        print(f"  {ph:14s} mean {v.mean():8.0f}  p50 {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}  max {v.max():8.0f}")
+    starts = np.sort(st[:, 0] - st[:, 0].min())
+    print("  WG start spread (cycles) p10/p50/p90/max:", [int(np.percentile(starts, q)) for q in (10, 50, 90, 100)])
+    gpu.close()
+
+
+if __name__ == "__main__":
+    main()

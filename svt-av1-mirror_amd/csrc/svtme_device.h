@@ -83,6 +83,10 @@ struct DevJob {
     unsigned long long *keys;      // [sb_count][R][85] full-pel argmin keys (sad << 32 | order)
     CSlot *cslot;                  // [sb_count][R]
     uint32_t parts;                // search-row bands per (SB, reference) in k_stage_c1; 0 = per-SB k_stage_c
+    // per-slot search parameters independent of the SB (svtme_hme_prepare, host)
+    uint16_t sdist[8];             // |picture distance| of slot s (ref_dist_const)
+    int16_t l0_sa[8][2];           // HME-L0 area (get_hme_l0_search_area)
+    int16_t ph_sa[8][2][2];        // pre-HME region areas (prehme_core)
 };
 
 // A launch over a batch of picture jobs (svtme_submit_batch_device). The jobs

@@ -34,6 +34,7 @@ extern "C" uint32_t svtme_launch_key(const DevJob *dj);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" uint32_t svtme_fp_parts(const svtme_controls *c);
+extern "C" void svtme_hme_prepare(DevJob *dj);
 
 // ----------------------------------------------------------------------------
 // errors
@@ -492,6 +493,7 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
         hj[k].cslot = hj[k].parts ? c->d_cslot + slot_off : nullptr;
         svtme_stage_a_list(&hj[k].job, hj[k].ta_list, &hj[k].ta_count);
         svtme_stage_b_list(&hj[k].job, hj[k].tb_list, &hj[k].tb_count);
+        svtme_hme_prepare(&hj[k]);
         sb_off += count[k];
         slot_off += (size_t)count[k] * hj[k].R;
     }

@@ -11,17 +11,19 @@
 
 namespace svtme {
 
-__device__ __forceinline__ int16_t i16(int v) { return (int16_t)v; }
-__device__ __forceinline__ int absi(int v) { return v < 0 ? -v : v; }
-__device__ __forceinline__ uint32_t min_u32(uint32_t a, uint32_t b) { return a < b ? a : b; }
-__device__ __forceinline__ uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
+#define SVTME_HD __host__ __device__ __forceinline__
+SVTME_HD int16_t i16(int v) { return (int16_t)v; }
+SVTME_HD int absi(int v) { return v < 0 ? -v : v; }
+SVTME_HD int imin(int a, int b) { return a < b ? a : b; }
+SVTME_HD uint32_t min_u32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+SVTME_HD uint64_t min_u64(uint64_t a, uint64_t b) { return a < b ? a : b; }
 
 // motion_estimation.c:1239-1243
-__device__ __forceinline__ uint16_t scaled_dist(uint16_t dist) {
+SVTME_HD uint16_t scaled_dist(uint16_t dist) {
     uint8_t round_up = ((dist % 8) == 0) ? 0 : 1;
     return (uint16_t)(((dist * 5) / 8) + round_up);
 }
-__device__ __forceinline__ uint16_t ref_dist_const(const svtme_job &j, int l, int r) {
+SVTME_HD uint16_t ref_dist_const(const svtme_job &j, int l, int r) {
     int64_t d = (int64_t)j.picture_number - (int64_t)j.ref_picture_number[l][r];
     return (uint16_t)(int16_t)(d < 0 ? -d : d);
 }
@@ -190,8 +192,8 @@ __device__ void hme_refine_rect(int level, const DevPlane &p, int16_t org_x, int
 
 // get_hme_l0_search_area (motion_estimation.c:1800-1867); the per-ref
 // mutate/restore of hme_l0_sa makes it a function of (list, ref, dist)
-__device__ void hme_l0_area(const svtme_controls &c, int l, int r, uint16_t dist, int16_t l00x, int16_t l00y,
-                            int16_t *sa_w, int16_t *sa_h) {
+SVTME_HD void hme_l0_area(const svtme_controls &c, int l, int r, uint16_t dist, int16_t l00x, int16_t l00y,
+                          int16_t *sa_w, int16_t *sa_h) {
     uint32_t mnw = c.hme_l0_sa.sa_min.width, mnh = c.hme_l0_sa.sa_min.height;
     uint32_t mxw = c.hme_l0_sa.sa_max.width, mxh = c.hme_l0_sa.sa_max.height;
     if (c.enable_me_sr_adjustment && c.distance_based_hme_resizing) {
@@ -216,9 +218,9 @@ __device__ void hme_l0_area(const svtme_controls &c, int l, int r, uint16_t dist
     }
     const int32_t f = scaled_dist(dist);
     int16_t w       = i16(mnw / c.num_hme_sa_w);
-    w               = i16(min((((w * f) + 15) & ~0x0F), (int)(((mxw / c.num_hme_sa_w) + 15) & ~0x0F)));
+    w               = i16(imin((((w * f) + 15) & ~0x0F), (int)(((mxw / c.num_hme_sa_w) + 15) & ~0x0F)));
     int16_t h       = i16(mnh / c.num_hme_sa_h);
-    h               = i16(min((h * f), (int)(mxh / c.num_hme_sa_h)));
+    h               = i16(imin((h * f), (int)(mxh / c.num_hme_sa_h)));
     *sa_w = w, *sa_h = h;
 }
 

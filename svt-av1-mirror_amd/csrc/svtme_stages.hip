@@ -1032,8 +1032,21 @@ __device__ __forceinline__ SlotCentre final_centre(const DevJob &dj, uint32_t sb
 // a v_min3 per position pair); the row, then the lane's best widen to the
 // 64-bit sad << 32 | y << 16 | x order of the reference's scan.
 // ----------------------------------------------------------------------------
-#define HT 4 // position rows per 1/16 tile
-#define HQ 3 // position quads per tile
+// Diagnostic build (-DSVTME_STAMPS, scripts/hme_stamps.py): thread 0 of every
+// k_hme workgroup records the shader clock at each phase boundary.
+#ifdef SVTME_STAMPS
+__device__ unsigned long long g_hme_stamps[1 << 17][8];
+#define HME_STAMP(k)                                                                                                   \
+    do {                                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < (1u << 17))                                                               \
+            g_hme_stamps[blockIdx.x][k] = __builtin_readcyclecounter();                                                \
+    } while (0)
+#else
+#define HME_STAMP(k)
+#endif
+
+#define HQ 3  // position quads per HME-L1 tile (8-wide areas at any alignment: 2 or 3 quads)
+#define HQ16 2 // position quads per 1/16 tile (interior windows are dword aligned: 8/16/32 wide = 2/4/8 quads)
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 // 16 bytes at a dword-aligned global address (the planes are global memory)
@@ -1061,6 +1074,7 @@ struct HSrch {             // one 1/16-resolution search (pre-HME region or HME-
     int16_t cnt0, cnt1;    // position rows of each tile-row parity (skip: cnt0 = rows, cnt1 = 0)
     int16_t ylast;         // last plane-row offset a tile of this search may read
     uint8_t sh, skip, id;  // byte offset of position 0; odd rows only; ARes index
+    uint8_t need;          // bit of HmeSh::need (slot * 2 + (L0 ? 1 : 0))
 };
 struct HSrch1 {            // one HME-L1 refinement search
     const uint8_t *a0;
@@ -1070,11 +1084,12 @@ struct HSrch1 {            // one HME-L1 refinement search
 };
 
 struct HmeSh {
+    DevJob dj; // the job, copied once: every later job / control read is an LDS read
     Dec d;
     unsigned long long key[SVTME_A_N]; // search minima by ARes index
     int16_t kxo[SVTME_A_N], kyo[SVTME_A_N];
     uint32_t zzacc[8];
-    uint8_t ph_need[8], l0_need[8];
+    uint32_t need;                     // bit slot * 2: pre-HME searched, slot * 2 + 1: HME-L0 searched
     HSrch srch[48];
     int32_t nsrch, nitems;
     unsigned long long key1[32];
@@ -1086,43 +1101,58 @@ struct HmeSh {
     __attribute__((aligned(16))) uint8_t src4[16][32]; // quarter-resolution source, sub rows
 };
 
-// SADs of the 16 x kh (sub) source block sr at an HT x HQ tile of positions of
+// rows of one 1/16 tile row: 8 dwords from quad q0 (two dword-aligned 16-byte loads)
+struct Row8 {
+    u32x4a4 lo, hi;
+};
+__device__ __forceinline__ Row8 row8(const uint8_t *a0, int stride, int ro, int q0) {
+    const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)ro * stride) + q0;
+    return Row8{ldg4(rp), ldg4(rp + 4)};
+}
+
+// SADs of the 16 x kh (sub) source block sr at a T x HQ tile of positions of
 // a 1/16 window: quads q0.. of row a0 (sh = byte offset of position 0),
-// position rows yf + 2t (t < tv); plane rows are clamped to ylast. Returns
-// the tile's minimum key (sad << 32 | y << 16 | x), ~0 if no position is valid.
+// position rows yf + 2t (t < tv); plane rows are clamped to ylast. Rows are
+// loaded two ahead of their use. Returns the tile's minimum key
+// (sad << 32 | y << 16 | x), ~0 if no position is valid.
+template <int T>
 __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                          int yf, int tv, int ylast, int kh,
                                                          const uint32_t (&sr)[8][4]) {
-    unsigned long long acc[HT][HQ];
+    constexpr int NR = T + 7;
+    unsigned long long acc[T][HQ16];
 #pragma unroll
-    for (int t = 0; t < HT; t++)
+    for (int t = 0; t < T; t++)
 #pragma unroll
-        for (int qq = 0; qq < HQ; qq++) acc[t][qq] = 0;
+        for (int qq = 0; qq < HQ16; qq++) acc[t][qq] = 0;
+    Row8 buf[3];
+    buf[0] = row8(a0, stride, min(yf, ylast), q0);
+    buf[1] = row8(a0, stride, min(yf + 2, ylast), q0);
 #pragma unroll
-    for (int m = 0; m < HT + 7; m++) {
-        const int ro       = min(yf + 2 * m, ylast);
-        const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)ro * stride) + q0;
-        const u32x4a4 lo = ldg4(rp), hi = ldg4(rp + 4);
-        const uint32_t d[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        unsigned long long P[HQ + 3];
+    for (int m = 0; m < NR; m++) {
+        if (m + 2 < NR)
+            buf[(m + 2) % 3] = row8(a0, stride, min(yf + 2 * (m + 2), ylast), q0);
+        const Row8 &R = buf[m % 3];
+        const uint32_t d[8] = {R.lo.x, R.lo.y, R.lo.z, R.lo.w, R.hi.x, R.hi.y, R.hi.z, R.hi.w};
+        unsigned long long P[HQ16 + 3];
 #pragma unroll
-        for (int j = 0; j < HQ + 3; j++) P[j] = pair(d[j], d[j + 1]);
+        for (int j = 0; j < HQ16 + 3; j++) P[j] = pair(d[j], d[j + 1]);
 #pragma unroll
-        for (int t = 0; t < HT; t++) {
+        for (int t = 0; t < T; t++) {
             const int k = m - t;
             if (k < 0 || k >= 8)
                 continue;
             if (k >= kh) // wave-uniform (partial-height SB)
                 continue;
 #pragma unroll
-            for (int qq = 0; qq < HQ; qq++)
+            for (int qq = 0; qq < HQ16; qq++)
 #pragma unroll
                 for (int j = 0; j < 4; j++) acc[t][qq] = qsad64(P[qq + j], sr[k][j], acc[t][qq]);
         }
     }
-    uint32_t xo[HQ][4];
+    uint32_t xo[HQ16][4];
 #pragma unroll
-    for (int qq = 0; qq < HQ; qq++)
+    for (int qq = 0; qq < HQ16; qq++)
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             const int x = 4 * (q0 + qq) - sh + e;
@@ -1130,10 +1160,10 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
         }
     unsigned long long best = ~0ull;
 #pragma unroll
-    for (int t = 0; t < HT; t++) {
+    for (int t = 0; t < T; t++) {
         uint32_t mt = U32MAX;
 #pragma unroll
-        for (int qq = 0; qq < HQ; qq++) {
+        for (int qq = 0; qq < HQ16; qq++) {
             const uint32_t lo = (uint32_t)acc[t][qq], hi = (uint32_t)(acc[t][qq] >> 32);
             const uint32_t k0 = (lo << 16) | xo[qq][0], k1 = (lo & 0xFFFF0000u) | xo[qq][1];
             const uint32_t k2 = (hi << 16) | xo[qq][2], k3 = (hi & 0xFFFF0000u) | xo[qq][3];
@@ -1148,46 +1178,52 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
     return best;
 }
 
-// SADs of the 32 x kh1 (sub) quarter-resolution source block (LDS, rows 32
-// bytes apart) at HQ quads of position row y of a 1/4 window. u16 lanes hold
-// 8 block rows (8 x 8 x 1020 < 2^16), then widen.
-__device__ __forceinline__ unsigned long long hme_tile32(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
-                                                         int y, int kh1, const uint8_t (*src)[32]) {
-    uint32_t a32[HQ][4];
+// One quarter of the SADs of the 32 x kh1 (sub) quarter-resolution source
+// block (LDS, rows 32 bytes apart) at HQ quads of position row y of a 1/4
+// window: block rows [4g, 4g + 4) of lane g = lane & 3, all loads issued up
+// front; the 4 lanes of a quad then sum their partial SADs (DPP) and every
+// lane returns the row's minimum key.
+__device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
+                                                          int y, int kh1, const uint8_t (*src)[32]) {
+    const int g = threadIdx.x & 3;
+    auto ld = [&](int kk, u32x4a4 (&L)[3]) {
+        const int k        = min(4 * g + kk, 15);
+        const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)(y + 2 * k) * stride) + q0;
+        L[0] = ldg4(rp), L[1] = ldg4(rp + 4), L[2] = ldg4(rp + 8);
+    };
+    u32x4a4 L[2][3];
+    ld(0, L[0]);
+    unsigned long long acc[HQ] = {0, 0, 0};
 #pragma unroll
-    for (int qq = 0; qq < HQ; qq++)
-#pragma unroll
-        for (int e = 0; e < 4; e++) a32[qq][e] = 0;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        unsigned long long acc[HQ] = {0, 0, 0};
-#pragma unroll
-        for (int kk = 0; kk < 8; kk++) {
-            const int k = h * 8 + kk;
-            if (k >= kh1) // wave-uniform
-                break;
+    for (int kk = 0; kk < 4; kk++) {
+        if (kk + 1 < 4)
+            ld(kk + 1, L[(kk + 1) & 1]);
+        const int k = 4 * g + kk;
+        if (k < kh1) {
+            const u32x4a4 *R = L[kk & 1];
             const uint4 s0 = ((const uint4 *)src[k])[0], s1 = ((const uint4 *)src[k])[1];
             const uint32_t sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-            const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)(y + 2 * k) * stride) + q0;
-            const u32x4a4 l0 = ldg4(rp), l1 = ldg4(rp + 4), l2 = ldg4(rp + 8);
-            const uint32_t d[12] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w, l2.x, l2.y, l2.z, l2.w};
+            const uint32_t d[12] = {R[0].x, R[0].y, R[0].z, R[0].w, R[1].x, R[1].y,
+                                    R[1].z, R[1].w, R[2].x, R[2].y, R[2].z, R[2].w};
 #pragma unroll
             for (int qq = 0; qq < HQ; qq++)
 #pragma unroll
                 for (int j = 0; j < 8; j++) acc[qq] = qsad64(pair(d[qq + j], d[qq + j + 1]), sv[j], acc[qq]);
         }
-#pragma unroll
-        for (int qq = 0; qq < HQ; qq++) qsad_unpack(acc[qq], a32[qq]);
     }
     uint32_t mt = U32MAX; // sad (< 2^17) << 15 | x (< 2^15)
 #pragma unroll
-    for (int qq = 0; qq < HQ; qq++)
+    for (int qq = 0; qq < HQ; qq++) {
+        uint32_t a[4] = {0, 0, 0, 0};
+        qsad_unpack(acc[qq], a);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-            const int x = 4 * (q0 + qq) - sh + e;
+            const uint32_t v = dpp_add<0x4E>(dpp_add<0xB1>(a[e])); // the quad's 4 row groups
+            const int x      = 4 * (q0 + qq) - sh + e;
             if (x >= 0 && x < sa_w)
-                mt = min_u32(mt, (a32[qq][e] << 15) | (uint32_t)x);
+                mt = min_u32(mt, (v << 15) | (uint32_t)x);
         }
+    }
     if (mt == U32MAX)
         return ~0ull;
     return ((unsigned long long)(mt >> 15) << 32) | ((unsigned long long)(uint32_t)y << 16) | (mt & 0x7FFFu);
@@ -1207,11 +1243,22 @@ __device__ __forceinline__ int find_search(const S *t, int n, int it) {
     return lo;
 }
 
-__global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
+#define HT16 2 // position rows per 1/16 tile
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_hme(const DevBatch B) {
     __shared__ HmeSh sh;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = UNI(tid >> 6);
     uint32_t sb_local;
-    const DevJob &dj        = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
+    {
+        const DevJob &gj = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
+        const uint32_t *js = (const uint32_t *)&gj;
+        uint32_t *jd       = (uint32_t *)&sh.dj;
+        for (int i = tid; i < (int)(sizeof(DevJob) / 4); i += 256) jd[i] = js[i];
+        if (tid < 8)
+            sh.zzacc[tid] = 0;
+    }
+    __syncthreads();
+    const DevJob &dj        = sh.dj;
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
     const SbGeo G           = sb_geo(dj, sb_local);
@@ -1220,79 +1267,54 @@ __global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
     const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
     const int kh  = (int)(G.bh >> 2) >> 1; // 1/16 block rows (sub)
     const int kh1 = (int)(G.bh >> 2);      // 1/4 block rows (sub): (bh / 2) / 2
-
-    // ---- A0: zz SADs (init_zz_sad, motion_estimation.c:2382-2437): thread = slot x sub row
     const bool zz_on = c.me_early_exit_th || c.me_safe_limit_zz_th;
-    if (tid < 8)
-        sh.zzacc[tid] = 0;
+    HME_STAMP(0);
+
+    // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs
+    uint32_t sr[8][4];
+    {
+        const uint8_t *sp = uni_ptr(dj.cur.lv[2].base + (ptrdiff_t)soy * dj.cur.lv[2].stride + sox);
+        const int sst     = UNI(dj.cur.lv[2].stride);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * sst);
+            sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
+        }
+    }
+    // ---- phase 0 (independent work of all waves):
+    //   wave 0: A1 search table of every search the slots may need (geometry only)
+    //   waves 1-3: zz SADs (init_zz_sad, motion_estimation.c:2382-2437), one slot per
+    //              wave at a time (lane = sub row x half row); the quarter-resolution source
     if (wid == 0) {
         dec_init(d);
-    }
-    __syncthreads();
-    if (zz_on) {
-        const int s = tid >> 5, r = tid & 31;
-        if (slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && r < (int)(G.bh >> 1)) {
-            const DevPlane &F = dj.ref[s >> 2][s & 3].lv[0];
-            const DevPlane &C = dj.cur.lv[0];
-            const uint32_t *rr = (const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * r) * F.stride + G.ox);
-            const uint32_t *cr = (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox);
-            uint32_t acc = 0;
-#pragma unroll
-            for (int j = 0; j < 16; j += 4) {
-                const uint4 a = *(const uint4 *)(rr + j), b = *(const uint4 *)(cr + j);
-                acc = __builtin_amdgcn_sad_u8(a.x, b.x, acc);
-                acc = __builtin_amdgcn_sad_u8(a.y, b.y, acc);
-                acc = __builtin_amdgcn_sad_u8(a.z, b.z, acc);
-                acc = __builtin_amdgcn_sad_u8(a.w, b.w, acc);
-            }
-            atomicAdd(&sh.zzacc[s], acc);
-        }
-    }
-    __syncthreads();
-    // ---- zz decisions, then the A1 search table (wave 0)
-    if (wid == 0) {
-        if (lane < 8)
-            d.a[SVTME_A_ZZ + lane] = ARes{sh.zzacc[lane], 0, 0};
-        wave_lds_fence();
-        dec_zz(d, job, G, vmask);
-        if (lane < 8) {
-            const int s    = lane;
-            const bool act = slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && d.do_ref[s];
-            sh.ph_need[s]  = act && c.prehme_enable && !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th);
-            sh.l0_need[s]  = act && c.enable_hme_flag && c.enable_hme_level0_flag &&
-                            !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2));
-        }
         if (lane < SVTME_A_N)
             sh.key[lane] = ~0ull;
-        wave_lds_fence();
         // lane = slot * 6 + k: k < 2 pre-HME region k, else HME-L0 quadrant k - 2
-        const int s = lane / 6, k = lane - 6 * (lane / 6), l = s >> 2, r = s & 3;
-        bool mk = false;
-        HSrch e;
+        const int s = lane / 6, k = lane - 6 * (lane / 6), l = s >> 2;
+        const bool on = lane < 48 && slot_valid(vmask, s) && tl_or_l0(job, l) &&
+                        (k < 2 ? c.prehme_enable != 0 : (c.enable_hme_flag && c.enable_hme_level0_flag));
+        bool mk   = false;
         int items = 0;
-        if (lane < 48 && ((k < 2) ? sh.ph_need[s] : sh.l0_need[s])) {
-            const DevPlane &P   = dj.ref[l][r].lv[2];
-            const uint16_t dist = ref_dist_const(job, l, r);
+        HSrch e;
+        if (on) {
+            const DevPlane &P = dj.ref[l][s & 3].lv[2];
+            const int16_t aw  = k < 2 ? dj.ph_sa[s][k][0] : dj.l0_sa[s][0];
+            const int16_t ah  = k < 2 ? dj.ph_sa[s][k][1] : dj.l0_sa[s][1];
             int16_t xo, yo, sw, shh;
             bool skip;
             if (k < 2) { // prehme_core (motion_estimation.c:1568-1636)
-                const uint32_t f    = scaled_dist(dist);
-                const uint16_t sa_w = (uint16_t)min((uint32_t)c.prehme_sa_cfg[k].sa_min.width * f,
-                                                    (uint32_t)c.prehme_sa_cfg[k].sa_max.width);
-                const uint16_t sa_h = (uint16_t)min((uint32_t)c.prehme_sa_cfg[k].sa_min.height * f,
-                                                    (uint32_t)c.prehme_sa_cfg[k].sa_max.height);
-                prehme_area(P, sox, soy, (int16_t)sa_w, (int16_t)sa_h, &xo, &yo, &sw, &shh);
-                skip = c.prehme_skip_search_line != 0; // compute_sad_c.c:74 (16-wide, <= 16 rows)
-                e.id = (uint8_t)(SVTME_A_PH + s * 2 + k);
+                prehme_area(P, sox, soy, aw, ah, &xo, &yo, &sw, &shh);
+                skip   = c.prehme_skip_search_line != 0; // compute_sad_c.c:74 (16 wide, <= 16 rows)
+                e.id   = (uint8_t)(SVTME_A_PH + s * 2 + k);
+                e.need = (uint8_t)(s * 2);
             } else { // hme_level_0 (motion_estimation.c:835-889)
-                int16_t saw, sah;
-                hme_l0_area(c, l, r, dist, 0, 0, &saw, &sah);
-                hme_l0_rect(c, P, sox, soy, saw, sah, (k - 2) >> 1, (k - 2) & 1, &xo, &yo, &sw, &shh);
-                skip = false;
-                e.id = (uint8_t)(SVTME_A_L0 + s * 4 + (k - 2));
+                hme_l0_rect(c, P, sox, soy, aw, ah, (k - 2) >> 1, (k - 2) & 1, &xo, &yo, &sw, &shh);
+                skip   = false;
+                e.id   = (uint8_t)(SVTME_A_L0 + s * 4 + (k - 2));
+                e.need = (uint8_t)(s * 2 + 1);
             }
-            sh.kxo[e.id] = xo;
-            sh.kyo[e.id] = yo;
+            sh.kxo[e.id]    = xo;
+            sh.kyo[e.id]    = yo;
             const int nrows = (sw > 0 && shh > 0) ? (skip ? shh / 2 : shh) : 0;
             if (nrows > 0) {
                 const uint8_t *w0 = P.base + (ptrdiff_t)(soy + yo) * P.stride + (sox + xo);
@@ -1301,78 +1323,119 @@ __global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
                 e.sa_w            = sw;
                 e.skip            = skip;
                 const int nq      = (e.sh + sw + 3) >> 2;
-                e.ncols           = (int16_t)((nq + HQ - 1) / HQ);
+                e.ncols           = (int16_t)((nq + HQ16 - 1) / HQ16);
                 if (skip) {
                     e.cnt0  = (int16_t)nrows;
                     e.cnt1  = 0;
                     e.ylast = (int16_t)(2 * nrows - 1 + 2 * (kh - 1));
-                    items   = e.ncols * ((nrows + HT - 1) / HT);
+                    items   = e.ncols * ((nrows + HT16 - 1) / HT16);
                 } else {
                     e.cnt0  = (int16_t)((nrows + 1) >> 1);
                     e.cnt1  = (int16_t)(nrows >> 1);
                     e.ylast = (int16_t)(nrows - 1 + 2 * (kh - 1));
-                    items   = e.ncols * 2 * ((e.cnt0 + HT - 1) / HT);
+                    items   = e.ncols * 2 * ((e.cnt0 + HT16 - 1) / HT16);
                 }
                 mk = true;
             }
         }
         int tot;
-        const int kpos  = wave_compact(mk, &tot);
-        const int incl  = wave_incl_scan(items);
+        const int kpos = wave_compact(mk, &tot);
+        const int incl = wave_incl_scan(items);
         if (mk) {
-            e.item0         = incl - items;
-            sh.srch[kpos]   = e;
+            e.item0       = incl - items;
+            sh.srch[kpos] = e;
         }
         if (lane == 63)
             sh.nitems = incl;
         if (lane == 0)
             sh.nsrch = tot;
-    }
-    // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs
-    uint32_t sr[8][4];
-    {
-        const DevPlane &S = dj.cur.lv[2];
-        const uint8_t *sp = uni_ptr(S.base + (ptrdiff_t)soy * S.stride + sox);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * S.stride);
-            sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
+    } else {
+        if (zz_on) {
+            const int r = lane >> 1, h = lane & 1; // sub row r, half row h
+            for (int s = wid - 1; s < 8; s += 3) { // wave-uniform slot
+                if (!(slot_valid(vmask, s) && tl_or_l0(job, s >> 2)))
+                    continue;
+                const DevPlane &F = dj.ref[s >> 2][s & 3].lv[0];
+                const DevPlane &C = dj.cur.lv[0];
+                uint32_t acc      = 0;
+                if (r < (int)(G.bh >> 1)) {
+                    const uint32_t *rr =
+                        (const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * r) * F.stride + G.ox) + 8 * h;
+                    const uint32_t *cr =
+                        (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox) + 8 * h;
+                    const u32x4a4 a0 = ldg4(rr), a1 = ldg4(rr + 4);
+                    const u32x4a4 b0 = ldg4(cr), b1 = ldg4(cr + 4);
+                    acc = __builtin_amdgcn_sad_u8(a0.x, b0.x, acc);
+                    acc = __builtin_amdgcn_sad_u8(a0.y, b0.y, acc);
+                    acc = __builtin_amdgcn_sad_u8(a0.z, b0.z, acc);
+                    acc = __builtin_amdgcn_sad_u8(a0.w, b0.w, acc);
+                    acc = __builtin_amdgcn_sad_u8(a1.x, b1.x, acc);
+                    acc = __builtin_amdgcn_sad_u8(a1.y, b1.y, acc);
+                    acc = __builtin_amdgcn_sad_u8(a1.z, b1.z, acc);
+                    acc = __builtin_amdgcn_sad_u8(a1.w, b1.w, acc);
+                }
+                acc = wave_sum_u32(acc);
+                if (lane == 0)
+                    sh.zzacc[s] = acc;
+            }
+        }
+        // quarter-resolution source block (32 x 32, even rows) for HME-L1
+        if (c.enable_hme_level1_flag && tid >= 224) {
+            const DevPlane &Q = dj.cur.lv[1];
+            const int row = (tid - 224) >> 1, half = tid & 1;
+            const u32x4a4 v = ldg4((const uint32_t *)(Q.base + (ptrdiff_t)((G.oy >> 1) + 2 * row) * Q.stride +
+                                                      (G.ox >> 1) + 16 * half));
+            ((uint4 *)sh.src4[row])[half] = make_uint4(v.x, v.y, v.z, v.w);
         }
     }
-    // quarter-resolution source block (32 x 32, even rows) into LDS for HME-L1
-    if (c.enable_hme_level1_flag && tid < 32) {
-        const DevPlane &Q = dj.cur.lv[1];
-        const int row = tid >> 1, half = tid & 1;
-        ((uint4 *)sh.src4[row])[half] =
-            *(const uint4 *)(Q.base + (ptrdiff_t)((G.oy >> 1) + 2 * row) * Q.stride + (G.ox >> 1) + 16 * half);
+    __syncthreads();
+    HME_STAMP(1);
+    // ---- zz decisions; which searches the reference performs (wave 0)
+    if (wid == 0) {
+        if (lane < 8)
+            d.a[SVTME_A_ZZ + lane] = ARes{sh.zzacc[lane], 0, 0};
+        wave_lds_fence();
+        dec_zz(d, job, G, vmask);
+        const int s    = lane >> 1;
+        const bool act = lane < 16 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && d.do_ref[s];
+        const bool nd  = act && ((lane & 1) ? !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2))
+                                            : !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th));
+        const unsigned long long m = __ballot(nd);
+        if (lane == 0)
+            sh.need = (uint32_t)m;
     }
     __syncthreads();
-    // ---- A1: pre-HME regions and HME-L0 quadrants, one HT x HQ tile per thread
+    HME_STAMP(2);
+    // ---- A1: pre-HME regions and HME-L0 quadrants, one HT16 x HQ tile per thread
     {
         const int nitems = sh.nitems, nsrch = sh.nsrch;
+        const uint32_t need = sh.need;
         const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
         for (int it = tid; it < nitems; it += 256) {
-            const HSrch &e  = sh.srch[find_search(sh.srch, nsrch, it)];
+            const HSrch &e = sh.srch[find_search(sh.srch, nsrch, it)];
+            if (!((need >> e.need) & 1u))
+                continue;
             const int local = it - e.item0;
             const int rt = local / e.ncols, col = local - rt * e.ncols;
             int yf, tv;
             if (e.skip) {
-                yf = 8 * rt + 1;
-                tv = min(HT, e.cnt0 - HT * rt);
+                yf = 2 * HT16 * rt + 1;
+                tv = min(HT16, e.cnt0 - HT16 * rt);
             } else {
                 const int p = rt & 1, i = rt >> 1;
-                yf = 8 * i + p;
-                tv = min(HT, (p ? e.cnt1 : e.cnt0) - HT * i);
+                yf = 2 * HT16 * i + p;
+                tv = min(HT16, (p ? e.cnt1 : e.cnt0) - HT16 * i);
             }
             if (tv <= 0)
                 continue;
             const unsigned long long kk =
-                hme_tile16(e.a0, pstride, HQ * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
+                hme_tile16<HT16>(e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
             if (kk != ~0ull)
                 atomicMin(&sh.key[e.id], kk);
         }
     }
     __syncthreads();
+    HME_STAMP(3);
     // ---- D: pre-HME and level-0 decisions, then the HME-L1 table (wave 0)
     const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH; // true on this path
     if (wid == 0) {
@@ -1386,7 +1449,7 @@ __global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
         dec_prehme(d, job, vmask);
         dec_l0(d, job, vmask);
         // HME-L1 per (slot, quadrant), lane = slot * 4 + q (hme_level1_b64, :2041-2122)
-        const int s = lane >> 2, q = lane & 3, l = s >> 2, r = s & 3;
+        const int s = lane >> 2, q = lane & 3, l = s >> 2;
         bool mk   = false;
         int items = 0;
         HSrch1 e;
@@ -1415,7 +1478,7 @@ __global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
                     done = true;
                 }
                 if (!done) { // hme_level_1 (motion_estimation.c:923-1022)
-                    const DevPlane &P = dj.ref[l][r].lv[1];
+                    const DevPlane &P = dj.ref[l][s & 3].lv[1];
                     const int16_t qx = i16(((int16_t)G.ox) >> 1), qy = i16(((int16_t)G.oy) >> 1);
                     int16_t xo, yo, sw, shh;
                     hme_refine_rect(1, P, qx, qy, (int16_t)c.hme_l1_sa.width, (int16_t)c.hme_l1_sa.height,
@@ -1443,8 +1506,8 @@ __global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
         const int kpos = wave_compact(mk, &tot);
         const int incl = wave_incl_scan(items);
         if (mk) {
-            e.item0        = incl - items;
-            sh.s1[kpos]    = e;
+            e.item0     = incl - items;
+            sh.s1[kpos] = e;
         }
         if (lane == 63)
             sh.nitems1 = incl;
@@ -1452,20 +1515,23 @@ __global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
             sh.nsrch1 = tot;
     }
     __syncthreads();
-    // ---- B: HME-L1 tiles
+    HME_STAMP(4);
+    // ---- B: HME-L1 tiles, 4 lanes (block-row quarters) per tile
     {
-        const int nitems = sh.nitems1, nsrch = sh.nsrch1;
+        const int nlanes = 4 * sh.nitems1, nsrch = sh.nsrch1;
         const int pstride = dj.cur.lv[1].stride;
-        for (int it = tid; it < nitems; it += 256) {
+        for (int it4 = tid; it4 < nlanes; it4 += 256) {
+            const int it    = it4 >> 2;
             const HSrch1 &e = sh.s1[find_search(sh.s1, nsrch, it)];
             const int local = it - e.item0;
             const int y = local / e.ncols, col = local - y * e.ncols;
-            const unsigned long long kk = hme_tile32(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh1, sh.src4);
-            if (kk != ~0ull)
+            const unsigned long long kk = hme_tile32q(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh1, sh.src4);
+            if ((it4 & 3) == 0 && kk != ~0ull)
                 atomicMin(&sh.key1[e.id], kk);
         }
     }
     __syncthreads();
+    HME_STAMP(5);
     if (wid == 0) {
         BState *b = dj.bst + sb_local;
         if (lane < 32) {
@@ -1479,9 +1545,9 @@ __global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
                 X  = i16((x + sh.x1o[lane]) * 2);
                 Y  = i16((y + sh.y1o[lane]) * 2);
             }
-            b->hx[0][lane]            = X;
-            b->hy[0][lane]            = Y;
-            b->hsad[0][lane]          = SD;
+            b->hx[0][lane]         = X;
+            b->hy[0][lane]         = Y;
+            b->hsad[0][lane]       = SD;
             (&b->lx[0][0])[lane]   = (&d.lx[0][0])[lane];
             (&b->ly[0][0])[lane]   = (&d.ly[0][0])[lane];
             (&b->lsad[0][0])[lane] = (&d.lsad[0][0])[lane];
@@ -1491,7 +1557,16 @@ __global__ void __launch_bounds__(256) k_hme(const DevBatch B) {
             b->do_ref[lane] = d.do_ref[lane];
         }
     }
+    HME_STAMP(6);
 }
+
+#ifdef SVTME_STAMPS
+extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks) {
+    if (nblocks > (1u << 17))
+        nblocks = 1u << 17;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long));
+}
+#endif
 
 // ----------------------------------------------------------------------------
 // Stage C: integer full-pel search with the 85-PU argmin, ME pruning, records,
@@ -2275,6 +2350,60 @@ struct PuMin {
         b32 = k32 < b32 ? k32 : b32;
         b64 = k64 < b64 ? k64 : b64;
     }
+    // K32: the 4 positions x0 + e (orders o0 + e) of an aligned quad, SADs packed
+    // as u16 pairs (lo: e = 0, 1; hi: e = 2, 3; already doubled for SUB). The
+    // 8x8 minima take all 4 positions per lane; the 16x16 / 32x32 / 64x64
+    // minima are lane-specialised: lane g = lane & 3 of each 4-lane group
+    // keeps position g only (16x16 sums on the packed pairs, <= 65280), so b16 /
+    // b32 / b64 hold minima over positions = g (mod 4) until finalize().
+    __device__ __forceinline__ void add_quad(uint32_t lo, uint32_t hi, uint32_t o0, int x0, int w) {
+        const int g = threadIdx.x & 3;
+        if (x0 >= 0 && x0 + 3 < w) { // wave-uniform: whole quad inside the area
+            const uint32_t k0 = ((lo & 0xFFFFu) << 12) | o0, k1 = ((lo >> 16) << 12) | (o0 + 1);
+            const uint32_t k2 = ((hi & 0xFFFFu) << 12) | (o0 + 2), k3 = ((hi >> 16) << 12) | (o0 + 3);
+            b8 = min_u32(min_u32((uint32_t)b8, min_u32(k0, k1)), min_u32(k2, k3));
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int x = x0 + e;
+                if (x < 0 || x >= w)
+                    continue; // wave-uniform
+                const uint32_t v = e < 2 ? lo : hi;
+                const uint32_t sd = (e & 1) ? (v >> 16) : (v & 0xFFFFu);
+                b8 = min_u32((uint32_t)b8, (sd << 12) | (o0 + e));
+            }
+        }
+        const uint32_t L = dpp_add<0x4E>(dpp_add<0xB1>(lo)), H = dpp_add<0x4E>(dpp_add<0xB1>(hi));
+        const uint32_t v = (g & 2) ? H : L;
+        const uint32_t s16 = (g & 1) ? (v >> 16) : (v & 0xFFFFu);
+        const uint32_t s32 = dpp_add<0x128>(dpp_add<0x124>(s16)); // row_ror 4, 8: same g
+        // 64x64: the 4 rows' s32 of the same g (row_bcast would mix the classes):
+        // permlane16_swap / permlane32_swap of a register with itself leave the two
+        // rows (halves) being summed in the pair of outputs of every lane
+        const auto p16     = __builtin_amdgcn_permlane16_swap(s32, s32, false, false);
+        const uint32_t t   = p16[0] + p16[1];
+        const auto p32     = __builtin_amdgcn_permlane32_swap(t, t, false, false);
+        const uint32_t s64 = p32[0] + p32[1];
+        const int x = x0 + g;
+        if (x >= 0 && x < w) {
+            const uint32_t og = o0 + (uint32_t)g;
+            b16 = min_u32((uint32_t)b16, (s16 << 12) | og);
+            b32 = min_u32((uint32_t)b32, (s32 << 12) | og);
+            b64 = min_u32((uint32_t)b64, (s64 << 12) | og);
+        }
+    }
+    // K32 after add_quad: min of b16 / b32 / b64 over the 4 lanes of each group
+    __device__ __forceinline__ void finalize() {
+        if (K32) {
+            b16 = quad_min((uint32_t)b16);
+            b32 = quad_min((uint32_t)b32);
+            b64 = quad_min((uint32_t)b64);
+        }
+    }
+    __device__ __forceinline__ static uint32_t quad_min(uint32_t v) {
+        v = min_u32(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
+        return min_u32(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false));
+    }
 };
 
 // Full-pel SADs of this lane's 8x8 block (source rows src) at search rows
@@ -2318,14 +2447,24 @@ __device__ __forceinline__ void fp_rows(PuMin<K32> &M, const uint32_t *a, int sd
                         acc = qsad(T[iy + rr * RSTEP][iq], T[iy + rr * RSTEP][iq + 1], src[rr][0], acc);
                         acc = qsad(T[iy + rr * RSTEP][iq + 1], T[iy + rr * RSTEP][iq + 2], src[rr][1], acc);
                     }
-                    uint32_t s4[4] = {0, 0, 0, 0};
-                    qsad_unpack(acc, s4);
                     const int y = ty + iy;
+                    if (K32) {
+                        const int x0   = 4 * (tq + iq) - sh;
+                        uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
+                        if (SUB) { // raw 8x4 SADs <= 8160: doubling stays inside each u16
+                            lo <<= 1;
+                            hi <<= 1;
+                        }
+                        M.add_quad(lo, hi, obase + (uint32_t)(y * w + x0), x0, w);
+                    } else {
+                        uint32_t s4[4] = {0, 0, 0, 0};
+                        qsad_unpack(acc, s4);
 #pragma unroll
-                    for (int k = 0; k < 4; k++) {
-                        const int x = 4 * (tq + iq) - sh + k;
-                        if (x >= 0 && x < w) // wave-uniform
-                            M.add(SUB ? s4[k] << 1 : s4[k], obase + (uint32_t)(y * w + x));
+                        for (int k = 0; k < 4; k++) {
+                            const int x = 4 * (tq + iq) - sh + k;
+                            if (x >= 0 && x < w) // wave-uniform
+                                M.add(SUB ? s4[k] << 1 : s4[k], obase + (uint32_t)(y * w + x));
+                        }
                     }
                 }
             }
@@ -2443,6 +2582,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
         const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc);
         const int sh     = (int)((uintptr_t)g & 3);
         fp_rows<SUB, K32, 1>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
+        M.finalize();
         const uint32_t p8   = (uint32_t)(PuMin<K32>::wide(M.b8) >> 32);
         const uint32_t p64  = rl32((uint32_t)(PuMin<K32>::wide(M.b64) >> 32), 63);
         const uint32_t mean = p64 / 64;
@@ -2483,6 +2623,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
     const int y0 = (int)(((uint32_t)h * part) / parts), y1 = (int)(((uint32_t)h * (part + 1)) / parts);
     const uint32_t obase = probe ? 1u : 0u; // the centre probe wins ties: order 0
     fp_rows<SUB, K32, SUB ? FP_TQ : 2>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
+    M.finalize();
     const unsigned long long k8 = PuMin<K32>::wide(M.b8), k16 = PuMin<K32>::wide(M.b16);
     const unsigned long long k32 = PuMin<K32>::wide(M.b32), k64 = PuMin<K32>::wide(M.b64);
     unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
@@ -2632,14 +2773,41 @@ static void fp_area_bound(const svtme_controls *c, uint32_t *w, uint32_t *h) {
         mw *= c->mv_sa_adj_sa_multiplier;
         mh *= c->mv_sa_adj_sa_multiplier;
     }
-    mw += 7;
+    mw = (mw + 7) & ~7u;
     mh = mh < 3 ? 3 : mh;
     if (c->me_8x8_var_enabled && c->me_sr_mult2_th != 0xFFFFFFFFu) {
-        mw = mw * 3 / 2 + 7;
+        mw = ((mw * 3 / 2) + 7) & ~7u;
         mh = mh * 3 / 2;
     }
     *w = mw;
     *h = mh;
+}
+
+// Per-slot search parameters of k_hme that do not depend on the SB: the
+// distance, get_hme_l0_search_area (motion_estimation.c:1800-1867, here with
+// l00 = (0, 0): the real-time reduction it would read is rejected by the job
+// validator) and the pre-HME areas (prehme_core :1580-1587).
+extern "C" void svtme_hme_prepare(DevJob *dj) {
+    const svtme_job &job    = dj->job;
+    const svtme_controls &c = job.ctrl;
+    for (int s = 0; s < 8; s++) {
+        const int l = s >> 2, r = s & 3;
+        const bool valid = l < job.num_lists && r < job.num_refs[l];
+        const uint16_t dist = valid ? svtme::ref_dist_const(job, l, r) : 1;
+        dj->sdist[s] = dist;
+        int16_t w = 0, h = 0;
+        if (valid)
+            svtme::hme_l0_area(c, l, r, dist, 0, 0, &w, &h);
+        dj->l0_sa[s][0] = w;
+        dj->l0_sa[s][1] = h;
+        const uint32_t f = svtme::scaled_dist(dist);
+        for (int k = 0; k < 2; k++) {
+            const uint32_t mw = (uint32_t)c.prehme_sa_cfg[k].sa_min.width * f, xw = c.prehme_sa_cfg[k].sa_max.width;
+            const uint32_t mh = (uint32_t)c.prehme_sa_cfg[k].sa_min.height * f, xh = c.prehme_sa_cfg[k].sa_max.height;
+            dj->ph_sa[s][k][0] = (int16_t)(uint16_t)(mw < xw ? mw : xw);
+            dj->ph_sa[s][k][1] = (int16_t)(uint16_t)(mh < xh ? mh : xh);
+        }
+    }
 }
 
 // k_hme applies: every SB 64 wide, sub-sampled HME rows, level 2 off
@@ -2652,7 +2820,7 @@ extern "C" bool svtme_hme_fused(const svtme_job *job) {
 extern "C" bool svtme_fp_k32(const svtme_controls *c) {
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
-    return 1u + w * h <= 4096u;
+    return (c->me_8x8_var_enabled ? 1u : 0u) + w * h <= 4096u; // order 0 is the variance probe
 }
 
 extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {

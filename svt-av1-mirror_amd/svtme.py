@@ -486,7 +486,8 @@ def make_job(width: int, height: int, ctrl: Controls, picture_number: int, refs_
 # Product library (HIP): loaded lazily; raises if absent
 # ----------------------------------------------------------------------------
 def product_lib_path() -> str:
-    return os.path.join(PKG_DIR, "libsvtme.so")
+    # SVTME_LIB: a diagnostic build of the same sources (e.g. scripts/hme_stamps.py)
+    return os.environ.get("SVTME_LIB") or os.path.join(PKG_DIR, "libsvtme.so")
 
 
 def load_product():
