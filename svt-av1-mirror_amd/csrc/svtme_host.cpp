@@ -211,6 +211,7 @@ static svtme_status alloc_pic(svtme_ctx *c, uint64_t pn, uint32_t W, uint32_t H,
         total += (size_t)stride[lv] * rows[lv];
         total = (total + 255) & ~(size_t)255;
     }
+    total += 1024; // slack: search-window loads may read a few dwords past the last row
     if (it == c->pics.end()) {
         PicBuf pb;
         HIP_TRY(hipMalloc((void **)&pb.mem, total));

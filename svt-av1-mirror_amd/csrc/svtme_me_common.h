@@ -38,23 +38,51 @@ __device__ __forceinline__ uint32_t valid_mask(const svtme_job &job) {
     return m;
 }
 
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        unsigned long long t = __shfl_xor(v, o, 64);
-        v                    = t < v ? t : v;
-    }
+// Wavefront reductions and scans with DPP (row_shr 1/2/4/8 inside each row of
+// 16 lanes, then row_bcast 15/31 across rows): a handful of VALU ops instead of
+// ds_bpermute round trips. Every lane of the wavefront must be active.
+#define DPP_ROW_SHR(n) (0x110 + (n))
+#define DPP_ROW_BCAST15 0x142
+#define DPP_ROW_BCAST31 0x143
+
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ uint32_t dpp_or(uint32_t v, uint32_t id) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, CTRL, RM, 0xF, false);
+}
+// inclusive prefix along lanes with op f and identity id; lane 63 ends with the total
+template <typename F>
+__device__ __forceinline__ uint32_t wave_scan32(uint32_t v, uint32_t id, F f) {
+    v = f(v, dpp_or<DPP_ROW_SHR(1)>(v, id));
+    v = f(v, dpp_or<DPP_ROW_SHR(2)>(v, id));
+    v = f(v, dpp_or<DPP_ROW_SHR(4)>(v, id));
+    v = f(v, dpp_or<DPP_ROW_SHR(8)>(v, id));
+    v = f(v, dpp_or<DPP_ROW_BCAST15, 0xA>(v, id));
+    v = f(v, dpp_or<DPP_ROW_BCAST31, 0xC>(v, id));
     return v;
+}
+__device__ __forceinline__ uint32_t lane63(uint32_t v) { return (uint32_t)__builtin_amdgcn_readlane((int)v, 63); }
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+    auto step = [&](uint32_t tl, uint32_t th) {
+        const unsigned long long t = ((unsigned long long)th << 32) | tl;
+        v                          = t < v ? t : v;
+    };
+#define WMIN64(CTRL, RM)                                                                                              \
+    step(dpp_or<CTRL, RM>((uint32_t)v, U32MAX), dpp_or<CTRL, RM>((uint32_t)(v >> 32), U32MAX))
+    WMIN64(DPP_ROW_SHR(1), 0xF);
+    WMIN64(DPP_ROW_SHR(2), 0xF);
+    WMIN64(DPP_ROW_SHR(4), 0xF);
+    WMIN64(DPP_ROW_SHR(8), 0xF);
+    WMIN64(DPP_ROW_BCAST15, 0xA);
+    WMIN64(DPP_ROW_BCAST31, 0xC);
+#undef WMIN64
+    return ((unsigned long long)lane63((uint32_t)(v >> 32)) << 32) | lane63((uint32_t)v);
 }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min_u32(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
+    return lane63(wave_scan32(v, U32MAX, [](uint32_t a, uint32_t b) { return a < b ? a : b; }));
 }
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+    return lane63(wave_scan32(v, 0u, [](uint32_t a, uint32_t b) { return a + b; }));
 }
 // rank of this lane among lanes with pred set (exclusive prefix count) and the total
 __device__ __forceinline__ int wave_compact(bool pred, int *total) {
@@ -67,14 +95,7 @@ __device__ __forceinline__ int wave_compact(bool pred, int *total) {
 
 // wave-inclusive prefix sum over lanes (lane order)
 __device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int t = __shfl_up(v, o, 64);
-        if (lane >= o)
-            v += t;
-    }
-    return v;
+    return (int)wave_scan32((uint32_t)v, 0u, [](uint32_t a, uint32_t b) { return a + b; });
 }
 
 // exact n / d for n * d < 2^32 with m = magic_u32(d); d == 1 wraps m to 0
@@ -82,6 +103,10 @@ __device__ __forceinline__ uint32_t magic_u32(uint32_t d) { return 0xFFFFFFFFu /
 __device__ __forceinline__ int mdiv(int n, uint32_t m) { return m ? (int)__umulhi((uint32_t)n, m) : n; }
 
 #define UNI(x) __builtin_amdgcn_readfirstlane((int)(x))
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+}
 
 // a pointer known to be wave-uniform, moved to SGPRs (enables base + 32-bit offset addressing)
 template <typename T>

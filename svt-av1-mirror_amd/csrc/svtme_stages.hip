@@ -925,11 +925,9 @@ struct SlotCentre {
     uint8_t do_ref;
 };
 
-__device__ __forceinline__ SlotCentre final_centre(const DevJob &dj, uint32_t sb_local, uint32_t vmask) {
-    const svtme_job &job    = dj.job;
+__device__ __forceinline__ SlotCentre final_centre(const svtme_job &job, const BState *b, uint32_t vmask) {
     const svtme_controls &c = job.ctrl;
     const int s             = threadIdx.x & 63;
-    const BState *b         = dj.bst + sb_local;
     const bool valid        = slot_valid(vmask, s);
     int lvl                 = -1;
     if (c.enable_hme_level0_flag && !c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
@@ -960,11 +958,11 @@ __device__ __forceinline__ SlotCentre final_centre(const DevJob &dj, uint32_t sb
     for (int k = 0; k < 8; k++) {
         if (!((vmask >> k) & 1u))
             continue;
-        const bool ok = __shfl((int)own, k, 64) != 0;
-        const bool hk = __shfl((int)hme_slot, k, 64) != 0;
+        const bool ok = rl32((uint32_t)own, k) != 0;
+        const bool hk = rl32((uint32_t)hme_slot, k) != 0;
         const bool tk = tl_or_l0(job, k >> 2);
-        const int16_t kx = (int16_t)__shfl((int)hx, k, 64), ky = (int16_t)__shfl((int)hy, k, 64);
-        const uint64_t ks = __shfl(hs, k, 64);
+        const int16_t kx = (int16_t)rl32((uint32_t)(int32_t)hx, k), ky = (int16_t)rl32((uint32_t)(int32_t)hy, k);
+        const uint64_t ks = rl64(hs, k);
         if (ok) {
             cx = kx, cy = ky, cs = ks;
         }
@@ -1083,23 +1081,6 @@ struct HSrch1 {            // one HME-L1 refinement search
     uint8_t sh, id;        // id = slot * 4 + quadrant
 };
 
-struct HmeSh {
-    DevJob dj; // the job, copied once: every later job / control read is an LDS read
-    Dec d;
-    unsigned long long key[SVTME_A_N]; // search minima by ARes index
-    int16_t kxo[SVTME_A_N], kyo[SVTME_A_N];
-    uint32_t zzacc[8];
-    uint32_t need;                     // bit slot * 2: pre-HME searched, slot * 2 + 1: HME-L0 searched
-    HSrch srch[48];
-    int32_t nsrch, nitems;
-    unsigned long long key1[32];
-    int16_t x1o[32], y1o[32];
-    HSrch1 s1[32];
-    int32_t nsrch1, nitems1;
-    int16_t hx[32], hy[32];
-    uint64_t hsad[32];
-    __attribute__((aligned(16))) uint8_t src4[16][32]; // quarter-resolution source, sub rows
-};
 
 // rows of one 1/16 tile row: 8 dwords from quad q0 (two dword-aligned 16-byte loads)
 struct Row8 {
@@ -1245,328 +1226,6 @@ __device__ __forceinline__ int find_search(const S *t, int n, int it) {
 
 #define HT16 2 // position rows per 1/16 tile
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_hme(const DevBatch B) {
-    __shared__ HmeSh sh;
-    const int tid = threadIdx.x, lane = tid & 63, wid = UNI(tid >> 6);
-    uint32_t sb_local;
-    {
-        const DevJob &gj = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
-        const uint32_t *js = (const uint32_t *)&gj;
-        uint32_t *jd       = (uint32_t *)&sh.dj;
-        for (int i = tid; i < (int)(sizeof(DevJob) / 4); i += 256) jd[i] = js[i];
-        if (tid < 8)
-            sh.zzacc[tid] = 0;
-    }
-    __syncthreads();
-    const DevJob &dj        = sh.dj;
-    const svtme_job &job    = dj.job;
-    const svtme_controls &c = job.ctrl;
-    const SbGeo G           = sb_geo(dj, sb_local);
-    const uint32_t vmask    = valid_mask(job);
-    Dec &d                  = sh.d;
-    const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
-    const int kh  = (int)(G.bh >> 2) >> 1; // 1/16 block rows (sub)
-    const int kh1 = (int)(G.bh >> 2);      // 1/4 block rows (sub): (bh / 2) / 2
-    const bool zz_on = c.me_early_exit_th || c.me_safe_limit_zz_th;
-    HME_STAMP(0);
-
-    // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs
-    uint32_t sr[8][4];
-    {
-        const uint8_t *sp = uni_ptr(dj.cur.lv[2].base + (ptrdiff_t)soy * dj.cur.lv[2].stride + sox);
-        const int sst     = UNI(dj.cur.lv[2].stride);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * sst);
-            sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
-        }
-    }
-    // ---- phase 0 (independent work of all waves):
-    //   wave 0: A1 search table of every search the slots may need (geometry only)
-    //   waves 1-3: zz SADs (init_zz_sad, motion_estimation.c:2382-2437), one slot per
-    //              wave at a time (lane = sub row x half row); the quarter-resolution source
-    if (wid == 0) {
-        dec_init(d);
-        if (lane < SVTME_A_N)
-            sh.key[lane] = ~0ull;
-        // lane = slot * 6 + k: k < 2 pre-HME region k, else HME-L0 quadrant k - 2
-        const int s = lane / 6, k = lane - 6 * (lane / 6), l = s >> 2;
-        const bool on = lane < 48 && slot_valid(vmask, s) && tl_or_l0(job, l) &&
-                        (k < 2 ? c.prehme_enable != 0 : (c.enable_hme_flag && c.enable_hme_level0_flag));
-        bool mk   = false;
-        int items = 0;
-        HSrch e;
-        if (on) {
-            const DevPlane &P = dj.ref[l][s & 3].lv[2];
-            const int16_t aw  = k < 2 ? dj.ph_sa[s][k][0] : dj.l0_sa[s][0];
-            const int16_t ah  = k < 2 ? dj.ph_sa[s][k][1] : dj.l0_sa[s][1];
-            int16_t xo, yo, sw, shh;
-            bool skip;
-            if (k < 2) { // prehme_core (motion_estimation.c:1568-1636)
-                prehme_area(P, sox, soy, aw, ah, &xo, &yo, &sw, &shh);
-                skip   = c.prehme_skip_search_line != 0; // compute_sad_c.c:74 (16 wide, <= 16 rows)
-                e.id   = (uint8_t)(SVTME_A_PH + s * 2 + k);
-                e.need = (uint8_t)(s * 2);
-            } else { // hme_level_0 (motion_estimation.c:835-889)
-                hme_l0_rect(c, P, sox, soy, aw, ah, (k - 2) >> 1, (k - 2) & 1, &xo, &yo, &sw, &shh);
-                skip   = false;
-                e.id   = (uint8_t)(SVTME_A_L0 + s * 4 + (k - 2));
-                e.need = (uint8_t)(s * 2 + 1);
-            }
-            sh.kxo[e.id]    = xo;
-            sh.kyo[e.id]    = yo;
-            const int nrows = (sw > 0 && shh > 0) ? (skip ? shh / 2 : shh) : 0;
-            if (nrows > 0) {
-                const uint8_t *w0 = P.base + (ptrdiff_t)(soy + yo) * P.stride + (sox + xo);
-                e.sh              = (uint8_t)((uintptr_t)w0 & 3);
-                e.a0              = w0 - e.sh;
-                e.sa_w            = sw;
-                e.skip            = skip;
-                const int nq      = (e.sh + sw + 3) >> 2;
-                e.ncols           = (int16_t)((nq + HQ16 - 1) / HQ16);
-                if (skip) {
-                    e.cnt0  = (int16_t)nrows;
-                    e.cnt1  = 0;
-                    e.ylast = (int16_t)(2 * nrows - 1 + 2 * (kh - 1));
-                    items   = e.ncols * ((nrows + HT16 - 1) / HT16);
-                } else {
-                    e.cnt0  = (int16_t)((nrows + 1) >> 1);
-                    e.cnt1  = (int16_t)(nrows >> 1);
-                    e.ylast = (int16_t)(nrows - 1 + 2 * (kh - 1));
-                    items   = e.ncols * 2 * ((e.cnt0 + HT16 - 1) / HT16);
-                }
-                mk = true;
-            }
-        }
-        int tot;
-        const int kpos = wave_compact(mk, &tot);
-        const int incl = wave_incl_scan(items);
-        if (mk) {
-            e.item0       = incl - items;
-            sh.srch[kpos] = e;
-        }
-        if (lane == 63)
-            sh.nitems = incl;
-        if (lane == 0)
-            sh.nsrch = tot;
-    } else {
-        if (zz_on) {
-            const int r = lane >> 1, h = lane & 1; // sub row r, half row h
-            for (int s = wid - 1; s < 8; s += 3) { // wave-uniform slot
-                if (!(slot_valid(vmask, s) && tl_or_l0(job, s >> 2)))
-                    continue;
-                const DevPlane &F = dj.ref[s >> 2][s & 3].lv[0];
-                const DevPlane &C = dj.cur.lv[0];
-                uint32_t acc      = 0;
-                if (r < (int)(G.bh >> 1)) {
-                    const uint32_t *rr =
-                        (const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * r) * F.stride + G.ox) + 8 * h;
-                    const uint32_t *cr =
-                        (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox) + 8 * h;
-                    const u32x4a4 a0 = ldg4(rr), a1 = ldg4(rr + 4);
-                    const u32x4a4 b0 = ldg4(cr), b1 = ldg4(cr + 4);
-                    acc = __builtin_amdgcn_sad_u8(a0.x, b0.x, acc);
-                    acc = __builtin_amdgcn_sad_u8(a0.y, b0.y, acc);
-                    acc = __builtin_amdgcn_sad_u8(a0.z, b0.z, acc);
-                    acc = __builtin_amdgcn_sad_u8(a0.w, b0.w, acc);
-                    acc = __builtin_amdgcn_sad_u8(a1.x, b1.x, acc);
-                    acc = __builtin_amdgcn_sad_u8(a1.y, b1.y, acc);
-                    acc = __builtin_amdgcn_sad_u8(a1.z, b1.z, acc);
-                    acc = __builtin_amdgcn_sad_u8(a1.w, b1.w, acc);
-                }
-                acc = wave_sum_u32(acc);
-                if (lane == 0)
-                    sh.zzacc[s] = acc;
-            }
-        }
-        // quarter-resolution source block (32 x 32, even rows) for HME-L1
-        if (c.enable_hme_level1_flag && tid >= 224) {
-            const DevPlane &Q = dj.cur.lv[1];
-            const int row = (tid - 224) >> 1, half = tid & 1;
-            const u32x4a4 v = ldg4((const uint32_t *)(Q.base + (ptrdiff_t)((G.oy >> 1) + 2 * row) * Q.stride +
-                                                      (G.ox >> 1) + 16 * half));
-            ((uint4 *)sh.src4[row])[half] = make_uint4(v.x, v.y, v.z, v.w);
-        }
-    }
-    __syncthreads();
-    HME_STAMP(1);
-    // ---- zz decisions; which searches the reference performs (wave 0)
-    if (wid == 0) {
-        if (lane < 8)
-            d.a[SVTME_A_ZZ + lane] = ARes{sh.zzacc[lane], 0, 0};
-        wave_lds_fence();
-        dec_zz(d, job, G, vmask);
-        const int s    = lane >> 1;
-        const bool act = lane < 16 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && d.do_ref[s];
-        const bool nd  = act && ((lane & 1) ? !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2))
-                                            : !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th));
-        const unsigned long long m = __ballot(nd);
-        if (lane == 0)
-            sh.need = (uint32_t)m;
-    }
-    __syncthreads();
-    HME_STAMP(2);
-    // ---- A1: pre-HME regions and HME-L0 quadrants, one HT16 x HQ tile per thread
-    {
-        const int nitems = sh.nitems, nsrch = sh.nsrch;
-        const uint32_t need = sh.need;
-        const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
-        for (int it = tid; it < nitems; it += 256) {
-            const HSrch &e = sh.srch[find_search(sh.srch, nsrch, it)];
-            if (!((need >> e.need) & 1u))
-                continue;
-            const int local = it - e.item0;
-            const int rt = local / e.ncols, col = local - rt * e.ncols;
-            int yf, tv;
-            if (e.skip) {
-                yf = 2 * HT16 * rt + 1;
-                tv = min(HT16, e.cnt0 - HT16 * rt);
-            } else {
-                const int p = rt & 1, i = rt >> 1;
-                yf = 2 * HT16 * i + p;
-                tv = min(HT16, (p ? e.cnt1 : e.cnt0) - HT16 * i);
-            }
-            if (tv <= 0)
-                continue;
-            const unsigned long long kk =
-                hme_tile16<HT16>(e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
-            if (kk != ~0ull)
-                atomicMin(&sh.key[e.id], kk);
-        }
-    }
-    __syncthreads();
-    HME_STAMP(3);
-    // ---- D: pre-HME and level-0 decisions, then the HME-L1 table (wave 0)
-    const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH; // true on this path
-    if (wid == 0) {
-        if (lane < SVTME_A_N && lane >= SVTME_A_PH) {
-            uint32_t best;
-            int x, y;
-            key_result(sh.key[lane], &best, &x, &y);
-            d.a[lane] = ARes{hsub ? best * 2 : best, i16((x + sh.kxo[lane]) * 4), i16((y + sh.kyo[lane]) * 4)};
-        }
-        wave_lds_fence();
-        dec_prehme(d, job, vmask);
-        dec_l0(d, job, vmask);
-        // HME-L1 per (slot, quadrant), lane = slot * 4 + q (hme_level1_b64, :2041-2122)
-        const int s = lane >> 2, q = lane & 3, l = s >> 2;
-        bool mk   = false;
-        int items = 0;
-        HSrch1 e;
-        if (lane < 32) {
-            int16_t X = 0, Y = 0;
-            uint64_t SD = 0;
-            sh.key1[lane] = ~0ull;
-            const bool listed = c.enable_hme_flag && c.enable_hme_level1_flag && slot_valid(vmask, s) &&
-                                tl_or_l0(job, l);
-            if (listed) {
-                const int16_t X0 = d.lx[s][q], Y0 = d.ly[s][q];
-                const uint64_t S0 = d.lsad[s][q];
-                bool done = false;
-                if (c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2)) {
-                    X = Y = 0;
-                    SD   = 0;
-                    done = true;
-                }
-                if (!done && !d.do_ref[s]) {
-                    X = Y = 0;
-                    SD   = U32MAX;
-                    done = true;
-                }
-                if (!done && c.prev_me_stage_based_exit_th && S0 < (c.prev_me_stage_based_exit_th >> 5)) {
-                    X = X0, Y = Y0, SD = S0;
-                    done = true;
-                }
-                if (!done) { // hme_level_1 (motion_estimation.c:923-1022)
-                    const DevPlane &P = dj.ref[l][s & 3].lv[1];
-                    const int16_t qx = i16(((int16_t)G.ox) >> 1), qy = i16(((int16_t)G.oy) >> 1);
-                    int16_t xo, yo, sw, shh;
-                    hme_refine_rect(1, P, qx, qy, (int16_t)c.hme_l1_sa.width, (int16_t)c.hme_l1_sa.height,
-                                    i16(X0 >> 1), i16(Y0 >> 1), &xo, &yo, &sw, &shh);
-                    sh.x1o[lane] = xo;
-                    sh.y1o[lane] = yo;
-                    SD           = ~0ull; // searched: resolved from key1 below
-                    if (sw > 0 && shh > 0 && kh1 > 0) {
-                        const uint8_t *w0 = P.base + (ptrdiff_t)(qy + yo) * P.stride + (qx + xo);
-                        e.sh              = (uint8_t)((uintptr_t)w0 & 3);
-                        e.a0              = w0 - e.sh;
-                        e.sa_w            = sw;
-                        e.ncols           = (int16_t)((((e.sh + sw + 3) >> 2) + HQ - 1) / HQ);
-                        e.id              = (uint8_t)lane;
-                        items             = e.ncols * shh;
-                        mk                = true;
-                    }
-                }
-            }
-            sh.hx[lane]   = X;
-            sh.hy[lane]   = Y;
-            sh.hsad[lane] = SD;
-        }
-        int tot;
-        const int kpos = wave_compact(mk, &tot);
-        const int incl = wave_incl_scan(items);
-        if (mk) {
-            e.item0     = incl - items;
-            sh.s1[kpos] = e;
-        }
-        if (lane == 63)
-            sh.nitems1 = incl;
-        if (lane == 0)
-            sh.nsrch1 = tot;
-    }
-    __syncthreads();
-    HME_STAMP(4);
-    // ---- B: HME-L1 tiles, 4 lanes (block-row quarters) per tile
-    {
-        const int nlanes = 4 * sh.nitems1, nsrch = sh.nsrch1;
-        const int pstride = dj.cur.lv[1].stride;
-        for (int it4 = tid; it4 < nlanes; it4 += 256) {
-            const int it    = it4 >> 2;
-            const HSrch1 &e = sh.s1[find_search(sh.s1, nsrch, it)];
-            const int local = it - e.item0;
-            const int y = local / e.ncols, col = local - y * e.ncols;
-            const unsigned long long kk = hme_tile32q(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh1, sh.src4);
-            if ((it4 & 3) == 0 && kk != ~0ull)
-                atomicMin(&sh.key1[e.id], kk);
-        }
-    }
-    __syncthreads();
-    HME_STAMP(5);
-    if (wid == 0) {
-        BState *b = dj.bst + sb_local;
-        if (lane < 32) {
-            int16_t X = sh.hx[lane], Y = sh.hy[lane];
-            uint64_t SD = sh.hsad[lane];
-            if (SD == ~0ull) { // searched (hme_level_1 result, full-pel x 2)
-                uint32_t best;
-                int x, y;
-                key_result(sh.key1[lane], &best, &x, &y);
-                SD = hsub ? (uint64_t)best * 2 : best;
-                X  = i16((x + sh.x1o[lane]) * 2);
-                Y  = i16((y + sh.y1o[lane]) * 2);
-            }
-            b->hx[0][lane]         = X;
-            b->hy[0][lane]         = Y;
-            b->hsad[0][lane]       = SD;
-            (&b->lx[0][0])[lane]   = (&d.lx[0][0])[lane];
-            (&b->ly[0][0])[lane]   = (&d.ly[0][0])[lane];
-            (&b->lsad[0][0])[lane] = (&d.lsad[0][0])[lane];
-        }
-        if (lane < 8) {
-            b->zz[lane]     = d.zz[lane];
-            b->do_ref[lane] = d.do_ref[lane];
-        }
-    }
-    HME_STAMP(6);
-}
-
-#ifdef SVTME_STAMPS
-extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks) {
-    if (nblocks > (1u << 17))
-        nblocks = 1u << 17;
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long));
-}
-#endif
 
 // ----------------------------------------------------------------------------
 // Stage C: integer full-pel search with the 85-PU argmin, ME pruning, records,
@@ -2107,7 +1766,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
     }
     if (w0) {
-        const SlotCentre sc = final_centre(dj, sb_local, vmask);
+        const SlotCentre sc = final_centre(job, dj.bst + sb_local, vmask);
         const uint64_t h0   = __shfl(sc.hme_sad, 0, 64);
         const bool tf_exit  = job.me_type == SVTME_ME_MCTF && h0 < job.tf_me_exit_th;
         if (lane < 8) {
@@ -2474,57 +2133,72 @@ __device__ __forceinline__ void fp_rows(PuMin<K32> &M, const uint32_t *a, int sd
 
 #define FP_TQ 3 // position quads per full-pel tile (sub-sampled rows; 2 for full rows)
 
-__device__ __forceinline__ uint32_t rl32(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
-__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
-    return ((uint64_t)rl32((uint32_t)(v >> 32), l) << 32) | rl32((uint32_t)v, l);
+// K32 form of fp_rows: position quads in pairs, one dword-aligned 16-byte
+// global load per plane row and lane (uniform row base in SGPRs + the lane's
+// dword offset), every bound wave-uniform. Reads up to one dword right of the
+// window (plane margins / allocation slack).
+template <bool SUB>
+__device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint32_t *a, int sdw, int sh, int w, int nq, int y0,
+                                          int y1, uint32_t obase, const uint32_t (&src)[SUB ? 4 : 8][2], int by,
+                                          int bx) {
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1, NR = 1 + (ROWS - 1) * RSTEP;
+    a     = uni_ptr(a);
+    sdw   = UNI(sdw);
+    sh    = UNI(sh);
+    w     = UNI(w);
+    nq    = UNI(nq);
+    y0    = UNI(y0);
+    y1    = UNI(y1);
+    obase = (uint32_t)UNI(obase);
+    const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2);
+    for (int ty = y0; ty < y1; ty++) {
+        for (int tq = 0; tq < nq; tq += 2) {
+            const uint32_t *rb = a + (ptrdiff_t)ty * sdw + tq;
+            u32x4a4 T[NR];
+#pragma unroll
+            for (int i = 0; i < NR; i++) T[i] = ldg4(rb + (ptrdiff_t)i * sdw + lo);
+            unsigned long long a0 = 0, a1 = 0;
+#pragma unroll
+            for (int rr = 0; rr < ROWS; rr++) {
+                const u32x4a4 &R = T[rr * RSTEP];
+                a0 = qsad64(pair(R.x, R.y), src[rr][0], a0);
+                a0 = qsad64(pair(R.y, R.z), src[rr][1], a0);
+                a1 = qsad64(pair(R.y, R.z), src[rr][0], a1);
+                a1 = qsad64(pair(R.z, R.w), src[rr][1], a1);
+            }
+            const int x0 = 4 * tq - sh;
+            uint32_t l0 = (uint32_t)a0, h0 = (uint32_t)(a0 >> 32), l1 = (uint32_t)a1, h1 = (uint32_t)(a1 >> 32);
+            if (SUB) { // raw 8x4 SADs <= 8160: doubling stays inside each u16
+                l0 <<= 1, h0 <<= 1, l1 <<= 1, h1 <<= 1;
+            }
+            const uint32_t ob = obase + (uint32_t)(ty * w + x0);
+            M.add_quad(l0, h0, ob, x0, w);
+            if (tq + 1 < nq)
+                M.add_quad(l1, h1, ob + 4, x0 + 4, w);
+        }
+    }
 }
 
-// K32: every order fits 12 bits (the host bounds the area, svtme_fp_k32)
-template <bool SUB, bool K32>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 5 : 4, 8))) k_stage_c1(const DevBatch B) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
-    if (u >= B.total)
-        return;
-    uint32_t gw;
-    const DevJob &dj        = batch_job(B, u, &gw);
+
+
+
+// integer_search_b64 of one reference slot s by one wavefront (motion_estimation.c:
+// 1249-1516): search area, check_00_center, the 8x8-variance centre probe and
+// the full-pel search of search rows [h * part / parts, h * (part + 1) / parts);
+// the 85-PU argmin keys go to kp (atomic min when parts > 1), the slot state
+// to cs (part 0). src: this lane's 8x8 source block rows (lane = block by, bx).
+template <bool SUB, bool K32, int TQ = (SUB ? FP_TQ : 2)>
+__device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s, const uint32_t (&src)[SUB ? 4 : 8][2],
+                                        int by, int bx, uint64_t hme_sad, uint32_t zz, uint32_t rdiv, int16_t sc_x,
+                                        int16_t sc_y, uint8_t dref, uint8_t tf_exit, int part, uint32_t parts,
+                                        unsigned long long *kp, CSlot *cs) {
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const uint32_t parts  = dj.parts;
-    const uint32_t per_sb = dj.R * parts;
-    const uint32_t sb_local = UNI(gw / per_sb);
-    const uint32_t rem      = gw - sb_local * per_sb;
-    const int k             = UNI(rem / parts);
-    const int part          = UNI(rem - (uint32_t)k * parts);
-    const int s             = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
+    const int lane          = threadIdx.x & 63;
     const int l = s >> 2, r = s & 3;
-    const SbGeo G     = sb_geo(dj, sb_local);
     const uint32_t ox = G.ox, oy = G.oy;
     const bool mctf   = job.me_type == SVTME_ME_MCTF;
-    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1;
-    const int z16 = lane >> 2, k4 = lane & 3;
-    const int by  = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
-    const int bx  = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
-
-    // this lane's 8x8 source block, read in place (me_process.c:183-214), issued first
     const DevPlane &C = dj.cur.lv[0];
-    uint32_t src[ROWS][2];
-#pragma unroll
-    for (int rr = 0; rr < ROWS; rr++) {
-        const uint32_t *sp =
-            (const uint32_t *)(C.base + (ptrdiff_t)(oy + by * 8 + rr * RSTEP) * C.stride + ox + bx * 8);
-        src[rr][0] = sp[0];
-        src[rr][1] = sp[1];
-    }
-    // search centre and HME pruning of the SB (lane = slot)
-    const SlotCentre scv   = final_centre(dj, sb_local, valid_mask(job));
-    const uint64_t hme_sad = rl64(scv.hme_sad, s);
-    const uint32_t zz = rl32(scv.zz, s), rdiv = rl32(scv.reduce_div, s);
-    const int16_t sc_x = (int16_t)rl32((uint32_t)(int32_t)scv.sc_x, s);
-    const int16_t sc_y = (int16_t)rl32((uint32_t)(int32_t)scv.sc_y, s);
-    const uint8_t dref = (uint8_t)rl32(scv.do_ref, s);
-    const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
-    CSlot *cs = dj.cslot + (size_t)sb_local * dj.R + k;
     if (!dref || tf_exit) {
         if (part == 0 && lane == 0)
             *cs = CSlot{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
@@ -2581,7 +2255,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
     if (probe) {
         const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc);
         const int sh     = (int)((uintptr_t)g & 3);
-        fp_rows<SUB, K32, 1>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
+        if constexpr (K32)
+            fp_rows32<SUB>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
+        else
+            fp_rows<SUB, K32, 1>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
         M.finalize();
         const uint32_t p8   = (uint32_t)(PuMin<K32>::wide(M.b8) >> 32);
         const uint32_t p64  = rl32((uint32_t)(PuMin<K32>::wide(M.b64) >> 32), 63);
@@ -2622,11 +2299,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
     const int nq     = (sh + w + 3) >> 2;
     const int y0 = (int)(((uint32_t)h * part) / parts), y1 = (int)(((uint32_t)h * (part + 1)) / parts);
     const uint32_t obase = probe ? 1u : 0u; // the centre probe wins ties: order 0
-    fp_rows<SUB, K32, SUB ? FP_TQ : 2>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
+    if constexpr (K32)
+        fp_rows32<SUB>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
+    else
+        fp_rows<SUB, K32, TQ>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
     M.finalize();
     const unsigned long long k8 = PuMin<K32>::wide(M.b8), k16 = PuMin<K32>::wide(M.b16);
     const unsigned long long k32 = PuMin<K32>::wide(M.b32), k64 = PuMin<K32>::wide(M.b64);
-    unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
     if (parts == 1) {
         kp[21 + lane] = k8;
         if ((lane & 3) == 0)
@@ -2648,18 +2327,65 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
         *cs = CSlot{hme_sad, zz, sc_x, sc_y, xo, yo, w, xc, yc, 1, dref, (uint8_t)probe, 0};
 }
 
-// Per SB: decode the argmin keys into best SAD / MV per PU (strict-< first
-// minimum in search order), then stage_c_tail
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_e(const DevBatch B) {
-    __shared__ StC st;
-    __shared__ CSlot csl[8];
-    uint32_t sb_local;
-    const DevJob &dj        = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
+
+// K32: every order fits 12 bits (the host bounds the area, svtme_fp_k32)
+template <bool SUB, bool K32>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 5 : 4, 8))) k_stage_c1(const DevBatch B) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total)
+        return;
+    uint32_t gw;
+    const DevJob &dj        = batch_job(B, u, &gw);
     const svtme_job &job    = dj.job;
-    const int tid           = threadIdx.x;
-    const SbGeo G           = sb_geo(dj, sb_local);
-    const uint32_t vmask    = valid_mask(job);
-    const int R             = (int)dj.R;
+    const uint32_t parts  = dj.parts;
+    const uint32_t per_sb = dj.R * parts;
+    const uint32_t sb_local = UNI(gw / per_sb);
+    const uint32_t rem      = gw - sb_local * per_sb;
+    const int k             = UNI(rem / parts);
+    const int part          = UNI(rem - (uint32_t)k * parts);
+    const int s             = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
+    const SbGeo G     = sb_geo(dj, sb_local);
+    const uint32_t ox = G.ox, oy = G.oy;
+    const bool mctf   = job.me_type == SVTME_ME_MCTF;
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1;
+    const int z16 = lane >> 2, k4 = lane & 3;
+    const int by  = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
+    const int bx  = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
+
+    // this lane's 8x8 source block, read in place (me_process.c:183-214), issued first
+    const DevPlane &C = dj.cur.lv[0];
+    uint32_t src[ROWS][2];
+#pragma unroll
+    for (int rr = 0; rr < ROWS; rr++) {
+        const uint32_t *sp =
+            (const uint32_t *)(C.base + (ptrdiff_t)(oy + by * 8 + rr * RSTEP) * C.stride + ox + bx * 8);
+        src[rr][0] = sp[0];
+        src[rr][1] = sp[1];
+    }
+    // search centre and HME pruning of the SB (lane = slot)
+    const SlotCentre scv   = final_centre(job, dj.bst + sb_local, valid_mask(job));
+    const uint64_t hme_sad = rl64(scv.hme_sad, s);
+    const uint32_t zz = rl32(scv.zz, s), rdiv = rl32(scv.reduce_div, s);
+    const int16_t sc_x = (int16_t)rl32((uint32_t)(int32_t)scv.sc_x, s);
+    const int16_t sc_y = (int16_t)rl32((uint32_t)(int32_t)scv.sc_y, s);
+    const uint8_t dref = (uint8_t)rl32(scv.do_ref, s);
+    const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
+    CSlot *cs = dj.cslot + (size_t)sb_local * dj.R + k;
+    unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
+    fp_slot<SUB, K32>(dj, G, s, src, by, bx, hme_sad, zz, rdiv, sc_x, sc_y, dref, tf_exit, part, parts, kp, cs);
+}
+
+// Per SB: decode the argmin keys kb[k][85] of the R records (slot state cin[k])
+// into best SAD / MV per PU (strict-< first minimum in search order), then
+// stage_c_tail; all threads of the workgroup. reset: leave kb at ~0 (banded
+// jobs merge into it with atomic min).
+__device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const DevJob &dj, uint32_t sb_local,
+                                             const SbGeo &G, uint32_t vmask, const CSlot *cin,
+                                             unsigned long long *kb, bool reset) {
+    const svtme_job &job = dj.job;
+    const int tid        = threadIdx.x;
+    const int R          = (int)dj.R;
     if (tid == 0) {
 #pragma unroll
         for (int s = 0; s < 8; s++) {
@@ -2679,7 +2405,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     __syncthreads();
     if (tid < R) {
         const int s     = tid < job.num_refs[0] ? tid : 4 + (tid - job.num_refs[0]);
-        const CSlot v   = dj.cslot[(size_t)sb_local * R + tid];
+        const CSlot v   = cin[tid];
         csl[s]          = v;
         st.hme_sad[s]   = v.hme_sad;
         st.zz[s]        = v.zz;
@@ -2691,14 +2417,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             st.tf_exit = v.tf_exit;
     }
     __syncthreads();
-    unsigned long long *kb = dj.keys + (size_t)sb_local * R * SVTME_PU_COUNT;
     for (int e = tid; e < R * SVTME_PU_COUNT; e += 256) {
         const int kk = e / SVTME_PU_COUNT, pu = e - kk * SVTME_PU_COUNT;
         const int s  = kk < job.num_refs[0] ? kk : 4 + (kk - job.num_refs[0]);
         uint32_t sad = U32MAX, mv = 0;
         if (st.searched[s]) {
             const unsigned long long key = kb[e];
-            if (dj.parts > 1)
+            if (reset)
                 kb[e] = ~0ull; // keys rest at ~0 for the next banded job
             const CSlot &v   = csl[s];
             const uint32_t o = (uint32_t)key;
@@ -2720,6 +2445,409 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     __syncthreads();
     stage_c_tail(st, dj, sb_local, G.bw, G.bh, vmask);
 }
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_e(const DevBatch B) {
+    __shared__ StC st;
+    __shared__ CSlot csl[8];
+    uint32_t sb_local;
+    const DevJob &dj     = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
+    const SbGeo G        = sb_geo(dj, sb_local);
+    const uint32_t vmask = valid_mask(dj.job);
+    stage_e_body(st, csl, dj, sb_local, G, vmask, dj.cslot + (size_t)sb_local * dj.R,
+                 dj.keys + (size_t)sb_local * dj.R * SVTME_PU_COUNT, dj.parts > 1);
+}
+
+struct HmeA { // state of phases A0 .. B
+    Dec d;
+    unsigned long long key[SVTME_A_N]; // search minima by ARes index
+    int16_t kxo[SVTME_A_N], kyo[SVTME_A_N];
+    uint32_t zzacc[8];
+    uint32_t need;                     // bit slot * 2: pre-HME searched, slot * 2 + 1: HME-L0 searched
+    HSrch srch[48];
+    int32_t nsrch, nitems;
+    unsigned long long key1[32];
+    int16_t x1o[32], y1o[32];
+    HSrch1 s1[32];
+    int32_t nsrch1, nitems1;
+    int16_t hx[32], hy[32];
+    uint64_t hsad[32];
+    __attribute__((aligned(16))) uint8_t src4[16][32]; // quarter-resolution source, sub rows
+};
+
+// k_hme shared memory: the job copy, the SB's HME state, the per-record
+// full-pel results, and the phase-A..B state overlaid by the stage-C/E state
+// (dead by then)
+struct HmeSh {
+    DevJob dj; // the job, copied once: every later job / control read is an LDS read
+    BState bs;
+    CSlot cin[8]; // by record
+    CSlot csl[8]; // by slot (stage_e_body)
+    union U {
+        HmeA a;
+        StC st;
+    } u;
+};
+
+// FP: the whole ME pass of the SB in this workgroup (k_stage_c1 with one band
+// per record, then k_stage_e); else the HME state goes to BState for them.
+template <bool FP, bool SUB_ME, bool K32>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_hme(const DevBatch B) {
+    __shared__ HmeSh sh;
+    const int tid = threadIdx.x, lane = tid & 63, wid = UNI(tid >> 6);
+    uint32_t sb_local;
+    {
+        const DevJob &gj = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
+        const uint32_t *js = (const uint32_t *)&gj;
+        uint32_t *jd       = (uint32_t *)&sh.dj;
+        for (int i = tid; i < (int)(sizeof(DevJob) / 4); i += 256) jd[i] = js[i];
+        if (tid < 8)
+            sh.u.a.zzacc[tid] = 0;
+    }
+    __syncthreads();
+    const DevJob &dj        = sh.dj;
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const SbGeo G           = sb_geo(dj, sb_local);
+    const uint32_t vmask    = valid_mask(job);
+    Dec &d                  = sh.u.a.d;
+    const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
+    const int kh  = (int)(G.bh >> 2) >> 1; // 1/16 block rows (sub)
+    const int kh1 = (int)(G.bh >> 2);      // 1/4 block rows (sub): (bh / 2) / 2
+    const bool zz_on = c.me_early_exit_th || c.me_safe_limit_zz_th;
+    HME_STAMP(0);
+
+    // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs
+    uint32_t sr[8][4];
+    {
+        const uint8_t *sp = uni_ptr(dj.cur.lv[2].base + (ptrdiff_t)soy * dj.cur.lv[2].stride + sox);
+        const int sst     = UNI(dj.cur.lv[2].stride);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * sst);
+            sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
+        }
+    }
+    // ---- phase 0 (independent work of all waves):
+    //   wave 0: A1 search table of every search the slots may need (geometry only)
+    //   waves 1-3: zz SADs (init_zz_sad, motion_estimation.c:2382-2437), one slot per
+    //              wave at a time (lane = sub row x half row); the quarter-resolution source
+    if (wid == 0) {
+        dec_init(d);
+        if (lane < SVTME_A_N)
+            sh.u.a.key[lane] = ~0ull;
+        // lane = slot * 6 + k: k < 2 pre-HME region k, else HME-L0 quadrant k - 2
+        const int s = lane / 6, k = lane - 6 * (lane / 6), l = s >> 2;
+        const bool on = lane < 48 && slot_valid(vmask, s) && tl_or_l0(job, l) &&
+                        (k < 2 ? c.prehme_enable != 0 : (c.enable_hme_flag && c.enable_hme_level0_flag));
+        bool mk   = false;
+        int items = 0;
+        HSrch e;
+        if (on) {
+            const DevPlane &P = dj.ref[l][s & 3].lv[2];
+            const int16_t aw  = k < 2 ? dj.ph_sa[s][k][0] : dj.l0_sa[s][0];
+            const int16_t ah  = k < 2 ? dj.ph_sa[s][k][1] : dj.l0_sa[s][1];
+            int16_t xo, yo, sw, shh;
+            bool skip;
+            if (k < 2) { // prehme_core (motion_estimation.c:1568-1636)
+                prehme_area(P, sox, soy, aw, ah, &xo, &yo, &sw, &shh);
+                skip   = c.prehme_skip_search_line != 0; // compute_sad_c.c:74 (16 wide, <= 16 rows)
+                e.id   = (uint8_t)(SVTME_A_PH + s * 2 + k);
+                e.need = (uint8_t)(s * 2);
+            } else { // hme_level_0 (motion_estimation.c:835-889)
+                hme_l0_rect(c, P, sox, soy, aw, ah, (k - 2) >> 1, (k - 2) & 1, &xo, &yo, &sw, &shh);
+                skip   = false;
+                e.id   = (uint8_t)(SVTME_A_L0 + s * 4 + (k - 2));
+                e.need = (uint8_t)(s * 2 + 1);
+            }
+            sh.u.a.kxo[e.id]    = xo;
+            sh.u.a.kyo[e.id]    = yo;
+            const int nrows = (sw > 0 && shh > 0) ? (skip ? shh / 2 : shh) : 0;
+            if (nrows > 0) {
+                const uint8_t *w0 = P.base + (ptrdiff_t)(soy + yo) * P.stride + (sox + xo);
+                e.sh              = (uint8_t)((uintptr_t)w0 & 3);
+                e.a0              = w0 - e.sh;
+                e.sa_w            = sw;
+                e.skip            = skip;
+                const int nq      = (e.sh + sw + 3) >> 2;
+                e.ncols           = (int16_t)((nq + HQ16 - 1) / HQ16);
+                if (skip) {
+                    e.cnt0  = (int16_t)nrows;
+                    e.cnt1  = 0;
+                    e.ylast = (int16_t)(2 * nrows - 1 + 2 * (kh - 1));
+                    items   = e.ncols * ((nrows + HT16 - 1) / HT16);
+                } else {
+                    e.cnt0  = (int16_t)((nrows + 1) >> 1);
+                    e.cnt1  = (int16_t)(nrows >> 1);
+                    e.ylast = (int16_t)(nrows - 1 + 2 * (kh - 1));
+                    items   = e.ncols * 2 * ((e.cnt0 + HT16 - 1) / HT16);
+                }
+                mk = true;
+            }
+        }
+        int tot;
+        const int kpos = wave_compact(mk, &tot);
+        const int incl = wave_incl_scan(items);
+        if (mk) {
+            e.item0       = incl - items;
+            sh.u.a.srch[kpos] = e;
+        }
+        if (lane == 63)
+            sh.u.a.nitems = incl;
+        if (lane == 0)
+            sh.u.a.nsrch = tot;
+    } else {
+        if (zz_on) {
+            const int r = lane >> 1, h = lane & 1; // sub row r, half row h
+            for (int s = wid - 1; s < 8; s += 3) { // wave-uniform slot
+                if (!(slot_valid(vmask, s) && tl_or_l0(job, s >> 2)))
+                    continue;
+                const DevPlane &F = dj.ref[s >> 2][s & 3].lv[0];
+                const DevPlane &C = dj.cur.lv[0];
+                uint32_t acc      = 0;
+                if (r < (int)(G.bh >> 1)) {
+                    const uint32_t *rr =
+                        (const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * r) * F.stride + G.ox) + 8 * h;
+                    const uint32_t *cr =
+                        (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox) + 8 * h;
+                    const u32x4a4 a0 = ldg4(rr), a1 = ldg4(rr + 4);
+                    const u32x4a4 b0 = ldg4(cr), b1 = ldg4(cr + 4);
+                    acc = __builtin_amdgcn_sad_u8(a0.x, b0.x, acc);
+                    acc = __builtin_amdgcn_sad_u8(a0.y, b0.y, acc);
+                    acc = __builtin_amdgcn_sad_u8(a0.z, b0.z, acc);
+                    acc = __builtin_amdgcn_sad_u8(a0.w, b0.w, acc);
+                    acc = __builtin_amdgcn_sad_u8(a1.x, b1.x, acc);
+                    acc = __builtin_amdgcn_sad_u8(a1.y, b1.y, acc);
+                    acc = __builtin_amdgcn_sad_u8(a1.z, b1.z, acc);
+                    acc = __builtin_amdgcn_sad_u8(a1.w, b1.w, acc);
+                }
+                acc = wave_sum_u32(acc);
+                if (lane == 0)
+                    sh.u.a.zzacc[s] = acc;
+            }
+        }
+        // quarter-resolution source block (32 x 32, even rows) for HME-L1
+        if (c.enable_hme_level1_flag && tid >= 224) {
+            const DevPlane &Q = dj.cur.lv[1];
+            const int row = (tid - 224) >> 1, half = tid & 1;
+            const u32x4a4 v = ldg4((const uint32_t *)(Q.base + (ptrdiff_t)((G.oy >> 1) + 2 * row) * Q.stride +
+                                                      (G.ox >> 1) + 16 * half));
+            ((uint4 *)sh.u.a.src4[row])[half] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+    }
+    __syncthreads();
+    HME_STAMP(1);
+    // ---- zz decisions; which searches the reference performs (wave 0)
+    if (wid == 0) {
+        if (lane < 8)
+            d.a[SVTME_A_ZZ + lane] = ARes{sh.u.a.zzacc[lane], 0, 0};
+        wave_lds_fence();
+        dec_zz(d, job, G, vmask);
+        const int s    = lane >> 1;
+        const bool act = lane < 16 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && d.do_ref[s];
+        const bool nd  = act && ((lane & 1) ? !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2))
+                                            : !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th));
+        const unsigned long long m = __ballot(nd);
+        if (lane == 0)
+            sh.u.a.need = (uint32_t)m;
+    }
+    __syncthreads();
+    HME_STAMP(2);
+    // ---- A1: pre-HME regions and HME-L0 quadrants, one HT16 x HQ tile per thread
+    {
+        const int nitems = sh.u.a.nitems, nsrch = sh.u.a.nsrch;
+        const uint32_t need = sh.u.a.need;
+        const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
+        for (int it = tid; it < nitems; it += 256) {
+            const HSrch &e = sh.u.a.srch[find_search(sh.u.a.srch, nsrch, it)];
+            if (!((need >> e.need) & 1u))
+                continue;
+            const int local = it - e.item0;
+            const int rt = local / e.ncols, col = local - rt * e.ncols;
+            int yf, tv;
+            if (e.skip) {
+                yf = 2 * HT16 * rt + 1;
+                tv = min(HT16, e.cnt0 - HT16 * rt);
+            } else {
+                const int p = rt & 1, i = rt >> 1;
+                yf = 2 * HT16 * i + p;
+                tv = min(HT16, (p ? e.cnt1 : e.cnt0) - HT16 * i);
+            }
+            if (tv <= 0)
+                continue;
+            const unsigned long long kk =
+                hme_tile16<HT16>(e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
+            if (kk != ~0ull)
+                atomicMin(&sh.u.a.key[e.id], kk);
+        }
+    }
+    __syncthreads();
+    HME_STAMP(3);
+    // ---- D: pre-HME and level-0 decisions, then the HME-L1 table (wave 0)
+    const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH; // true on this path
+    if (wid == 0) {
+        if (lane < SVTME_A_N && lane >= SVTME_A_PH) {
+            uint32_t best;
+            int x, y;
+            key_result(sh.u.a.key[lane], &best, &x, &y);
+            d.a[lane] = ARes{hsub ? best * 2 : best, i16((x + sh.u.a.kxo[lane]) * 4), i16((y + sh.u.a.kyo[lane]) * 4)};
+        }
+        wave_lds_fence();
+        dec_prehme(d, job, vmask);
+        dec_l0(d, job, vmask);
+        // HME-L1 per (slot, quadrant), lane = slot * 4 + q (hme_level1_b64, :2041-2122)
+        const int s = lane >> 2, q = lane & 3, l = s >> 2;
+        bool mk   = false;
+        int items = 0;
+        HSrch1 e;
+        if (lane < 32) {
+            int16_t X = 0, Y = 0;
+            uint64_t SD = 0;
+            sh.u.a.key1[lane] = ~0ull;
+            const bool listed = c.enable_hme_flag && c.enable_hme_level1_flag && slot_valid(vmask, s) &&
+                                tl_or_l0(job, l);
+            if (listed) {
+                const int16_t X0 = d.lx[s][q], Y0 = d.ly[s][q];
+                const uint64_t S0 = d.lsad[s][q];
+                bool done = false;
+                if (c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2)) {
+                    X = Y = 0;
+                    SD   = 0;
+                    done = true;
+                }
+                if (!done && !d.do_ref[s]) {
+                    X = Y = 0;
+                    SD   = U32MAX;
+                    done = true;
+                }
+                if (!done && c.prev_me_stage_based_exit_th && S0 < (c.prev_me_stage_based_exit_th >> 5)) {
+                    X = X0, Y = Y0, SD = S0;
+                    done = true;
+                }
+                if (!done) { // hme_level_1 (motion_estimation.c:923-1022)
+                    const DevPlane &P = dj.ref[l][s & 3].lv[1];
+                    const int16_t qx = i16(((int16_t)G.ox) >> 1), qy = i16(((int16_t)G.oy) >> 1);
+                    int16_t xo, yo, sw, shh;
+                    hme_refine_rect(1, P, qx, qy, (int16_t)c.hme_l1_sa.width, (int16_t)c.hme_l1_sa.height,
+                                    i16(X0 >> 1), i16(Y0 >> 1), &xo, &yo, &sw, &shh);
+                    sh.u.a.x1o[lane] = xo;
+                    sh.u.a.y1o[lane] = yo;
+                    SD           = ~0ull; // searched: resolved from key1 below
+                    if (sw > 0 && shh > 0 && kh1 > 0) {
+                        const uint8_t *w0 = P.base + (ptrdiff_t)(qy + yo) * P.stride + (qx + xo);
+                        e.sh              = (uint8_t)((uintptr_t)w0 & 3);
+                        e.a0              = w0 - e.sh;
+                        e.sa_w            = sw;
+                        e.ncols           = (int16_t)((((e.sh + sw + 3) >> 2) + HQ - 1) / HQ);
+                        e.id              = (uint8_t)lane;
+                        items             = e.ncols * shh;
+                        mk                = true;
+                    }
+                }
+            }
+            sh.u.a.hx[lane]   = X;
+            sh.u.a.hy[lane]   = Y;
+            sh.u.a.hsad[lane] = SD;
+        }
+        int tot;
+        const int kpos = wave_compact(mk, &tot);
+        const int incl = wave_incl_scan(items);
+        if (mk) {
+            e.item0     = incl - items;
+            sh.u.a.s1[kpos] = e;
+        }
+        if (lane == 63)
+            sh.u.a.nitems1 = incl;
+        if (lane == 0)
+            sh.u.a.nsrch1 = tot;
+    }
+    __syncthreads();
+    HME_STAMP(4);
+    // ---- B: HME-L1 tiles, 4 lanes (block-row quarters) per tile
+    {
+        const int nlanes = 4 * sh.u.a.nitems1, nsrch = sh.u.a.nsrch1;
+        const int pstride = dj.cur.lv[1].stride;
+        for (int it4 = tid; it4 < nlanes; it4 += 256) {
+            const int it    = it4 >> 2;
+            const HSrch1 &e = sh.u.a.s1[find_search(sh.u.a.s1, nsrch, it)];
+            const int local = it - e.item0;
+            const int y = local / e.ncols, col = local - y * e.ncols;
+            const unsigned long long kk = hme_tile32q(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh1, sh.u.a.src4);
+            if ((it4 & 3) == 0 && kk != ~0ull)
+                atomicMin(&sh.u.a.key1[e.id], kk);
+        }
+    }
+    __syncthreads();
+    HME_STAMP(5);
+    BState *b = FP ? &sh.bs : dj.bst + sb_local;
+    if (wid == 0) {
+        if (lane < 32) {
+            int16_t X = sh.u.a.hx[lane], Y = sh.u.a.hy[lane];
+            uint64_t SD = sh.u.a.hsad[lane];
+            if (SD == ~0ull) { // searched (hme_level_1 result, full-pel x 2)
+                uint32_t best;
+                int x, y;
+                key_result(sh.u.a.key1[lane], &best, &x, &y);
+                SD = hsub ? (uint64_t)best * 2 : best;
+                X  = i16((x + sh.u.a.x1o[lane]) * 2);
+                Y  = i16((y + sh.u.a.y1o[lane]) * 2);
+            }
+            b->hx[0][lane]         = X;
+            b->hy[0][lane]         = Y;
+            b->hsad[0][lane]       = SD;
+            (&b->lx[0][0])[lane]   = (&d.lx[0][0])[lane];
+            (&b->ly[0][0])[lane]   = (&d.ly[0][0])[lane];
+            (&b->lsad[0][0])[lane] = (&d.lsad[0][0])[lane];
+        }
+        if (lane < 8) {
+            b->zz[lane]     = d.zz[lane];
+            b->do_ref[lane] = d.do_ref[lane];
+        }
+    }
+    if (!FP) {
+        HME_STAMP(6);
+        return;
+    }
+    __syncthreads(); // phase A..B state is dead from here (StC overlays it)
+    // ---- C: integer_search_b64 of every record, one wavefront each (k_stage_c1, one band)
+    {
+        constexpr int ROWS = SUB_ME ? 4 : 8, RSTEP = SUB_ME ? 2 : 1;
+        const int z16 = lane >> 2, k4 = lane & 3;
+        const int by  = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
+        const int bx  = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
+        const DevPlane &C = dj.cur.lv[0];
+        uint32_t src[ROWS][2];
+#pragma unroll
+        for (int rr = 0; rr < ROWS; rr++) {
+            const uint32_t *sp =
+                (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + by * 8 + rr * RSTEP) * C.stride + G.ox + bx * 8);
+            src[rr][0] = sp[0];
+            src[rr][1] = sp[1];
+        }
+        const SlotCentre scv = final_centre(job, &sh.bs, vmask); // lane = slot
+        const bool mctf      = job.me_type == SVTME_ME_MCTF;
+        const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
+        for (int k = wid; k < (int)dj.R; k += 4) {
+            const int s = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
+            fp_slot<SUB_ME, K32, 2>(dj, G, s, src, by, bx, rl64(scv.hme_sad, s), rl32(scv.zz, s),
+                                 rl32(scv.reduce_div, s), (int16_t)rl32((uint32_t)(int32_t)scv.sc_x, s),
+                                 (int16_t)rl32((uint32_t)(int32_t)scv.sc_y, s), (uint8_t)rl32(scv.do_ref, s), tf_exit,
+                                 0, 1u, &sh.u.st.keys[k][0], &sh.cin[k]);
+        }
+    }
+    __syncthreads();
+    HME_STAMP(6);
+    // ---- E: decode, me_prune_ref, records, candidates / distortions / GM detection
+    stage_e_body(sh.u.st, sh.csl, dj, sb_local, G, vmask, sh.cin, &sh.u.st.keys[0][0], false);
+    HME_STAMP(7);
+}
+
+#ifdef SVTME_STAMPS
+extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks) {
+    if (nblocks > (1u << 17))
+        nblocks = 1u << 17;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long));
+}
+#endif
 
 } // namespace svtme
 
@@ -2837,7 +2965,8 @@ extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {
 extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
     const bool full = dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     return (uint32_t)full | (uint32_t)(dj->parts != 0) << 1 | (uint32_t)svtme_fp_k32(&dj->job.ctrl) << 2 |
-           (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4;
+           (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4 |
+           (uint32_t)(dj->parts == 1) << 5;
 }
 
 static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
@@ -2877,8 +3006,21 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     if (mask)
         *mask = 0;
     const DevBatch bd = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
+    const bool full = h0.job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
+    const bool k32  = svtme_fp_k32(&h0.job.ctrl);
+    if (svtme_hme_fused(&h0.job) && h0.parts == 1 && getenv("SVTME_FUSED_FP")) { // the whole pass in one launch
+        if (full && k32)
+            SVTME_LAUNCH((svtme::k_hme<true, false, true>), dim3(bd.total), 0, bd);
+        else if (full)
+            SVTME_LAUNCH((svtme::k_hme<true, false, false>), dim3(bd.total), 0, bd);
+        else if (k32)
+            SVTME_LAUNCH((svtme::k_hme<true, true, true>), dim3(bd.total), 0, bd);
+        else
+            SVTME_LAUNCH((svtme::k_hme<true, true, false>), dim3(bd.total), 0, bd);
+        return hipGetLastError();
+    }
     if (svtme_hme_fused(&h0.job)) {
-        SVTME_LAUNCH(svtme::k_hme, dim3(bd.total), 0, bd);
+        SVTME_LAUNCH((svtme::k_hme<false, true, true>), dim3(bd.total), 0, bd);
     } else {
     const DevBatch ba = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta_count; });
     if (ba.total)
@@ -2892,12 +3034,10 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
             SVTME_LAUNCH(svtme::k_stage_b<false>, dim3((bb.total + 3) / 4), 2, bb);
     }
     }
-    const bool full = h0.job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     const DevBatch be = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
     if (h0.parts) { // wide full-pel stage + per-SB decode
         const DevBatch bc = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.R * j.parts; });
         const dim3 grid((bc.total + 3) / 4);
-        const bool k32 = svtme_fp_k32(&h0.job.ctrl);
         if (full && k32)
             SVTME_LAUNCH((svtme::k_stage_c1<false, true>), grid, 3, bc);
         else if (full)
