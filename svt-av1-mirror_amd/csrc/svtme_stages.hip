@@ -2516,17 +2516,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     const bool zz_on = c.me_early_exit_th || c.me_safe_limit_zz_th;
     HME_STAMP(0);
 
-    // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs
-    uint32_t sr[8][4];
-    {
-        const uint8_t *sp = uni_ptr(dj.cur.lv[2].base + (ptrdiff_t)soy * dj.cur.lv[2].stride + sox);
-        const int sst     = UNI(dj.cur.lv[2].stride);
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * sst);
-            sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
-        }
-    }
     // ---- phase 0 (independent work of all waves):
     //   wave 0: A1 search table of every search the slots may need (geometry only)
     //   waves 1-3: zz SADs (init_zz_sad, motion_estimation.c:2382-2437), one slot per
@@ -2654,6 +2643,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     HME_STAMP(2);
     // ---- A1: pre-HME regions and HME-L0 quadrants, one HT16 x HQ tile per thread
     {
+        // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs (live in A1 only)
+        uint32_t sr[8][4];
+        {
+            const uint8_t *sp = uni_ptr(dj.cur.lv[2].base + (ptrdiff_t)soy * dj.cur.lv[2].stride + sox);
+            const int sst     = UNI(dj.cur.lv[2].stride);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * sst);
+                sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
+            }
+        }
         const int nitems = sh.u.a.nitems, nsrch = sh.u.a.nsrch;
         const uint32_t need = sh.u.a.need;
         const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
