@@ -357,6 +357,25 @@ void svt_aom_downsample_2d_hip(uint8_t *input_samples, uint32_t input_stride, ui
 uint32_t svt_aom_sad_16b_kernel_hip(uint16_t *src, uint32_t src_stride, uint16_t *ref, uint32_t ref_stride,
                                     uint32_t height, uint32_t width);
 
+/* aom_dsp_rtcd.h:868 svt_pme_sad_loop_kernel (mode decision's full-pel MV
+ * refinement, C at product_coding_loop.c:1811): SAD + MV rate of every visited
+ * position of a (search_step-strided) area, strict-< update of *best_cost /
+ * *best_mvx / *best_mvy (1/8-pel units). mv_cost_params is the reference's
+ * MV_COST_PARAMS (mcomp.h:37); this library reads it through the layout below,
+ * which integration/svtme_svt_glue.c checks against the reference header. */
+struct svt_mv_cost_param;
+#define SVTME_MVCOST_OFF_REF_MV 0         /* const MV *ref_mv (int16 row, col) */
+#define SVTME_MVCOST_OFF_TYPE 12          /* MV_COST_TYPE (uint8): 0 entropy .. 5 none */
+#define SVTME_MVCOST_OFF_MVJCOST 16       /* const int *mvjcost (4 joints) */
+#define SVTME_MVCOST_OFF_MVCOST 24        /* const int *mvcost[2] (row, col; centred) */
+#define SVTME_MVCOST_OFF_ERROR_PER_BIT 40 /* int error_per_bit */
+void svt_pme_sad_loop_kernel_hip(const struct svt_mv_cost_param *mv_cost_params, uint8_t *src, uint32_t src_stride,
+                                 uint8_t *ref, uint32_t ref_stride, uint32_t block_height, uint32_t block_width,
+                                 uint32_t *best_cost, int16_t *best_mvx, int16_t *best_mvy,
+                                 int16_t search_position_start_x, int16_t search_position_start_y,
+                                 int16_t search_area_width, int16_t search_area_height, int16_t search_step,
+                                 int16_t mvx, int16_t mvy);
+
 #ifdef __cplusplus
 }
 #endif

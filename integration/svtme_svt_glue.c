@@ -29,10 +29,12 @@
  *                                     a picture's planes (temporal_filtering.c:
  *                                     3895-3931 pad_and_decimate_filtered_pic).
  */
+#include <stddef.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "aom_dsp_rtcd.h"
+#include "mcomp.h"
 #include "me_context.h"
 #include "me_sb_results.h"
 #include "pcs.h"
@@ -42,7 +44,7 @@
 #include "svtme.h"
 
 /* --------------------------------------------------------------------------
- * rtcd registration (aom_dsp_rtcd.h:779, 841, 842, 848, 853-856, 863)
+ * rtcd registration (aom_dsp_rtcd.h:779, 841, 842, 848, 853-856, 863, 868)
  * ------------------------------------------------------------------------ */
 static struct {
     void (*sad_loop)(uint8_t *, uint32_t, uint8_t *, uint32_t, uint32_t, uint32_t, uint64_t *, int16_t *,
@@ -58,7 +60,19 @@ static struct {
     void (*init32)(uint32_t *, uint32_t, uint32_t, uint32_t);
     void (*downsample)(uint8_t *, uint32_t, uint32_t, uint32_t, uint8_t *, uint32_t, uint32_t);
     uint32_t (*sad16b)(uint16_t *, uint32_t, uint16_t *, uint32_t, uint32_t, uint32_t);
+    void (*pme)(const struct svt_mv_cost_param *, uint8_t *, uint32_t, uint8_t *, uint32_t, uint32_t, uint32_t,
+                uint32_t *, int16_t *, int16_t *, int16_t, int16_t, int16_t, int16_t, int16_t, int16_t, int16_t);
 } g_prev;
+
+/* the MV_COST_PARAMS layout (mcomp.h:37-48) svt_pme_sad_loop_kernel_hip reads */
+_Static_assert(offsetof(MV_COST_PARAMS, ref_mv) == SVTME_MVCOST_OFF_REF_MV, "MV_COST_PARAMS.ref_mv");
+_Static_assert(offsetof(MV_COST_PARAMS, mv_cost_type) == SVTME_MVCOST_OFF_TYPE, "MV_COST_PARAMS.mv_cost_type");
+_Static_assert(sizeof(((MV_COST_PARAMS *)0)->mv_cost_type) == 1, "MV_COST_TYPE is one byte");
+_Static_assert(offsetof(MV_COST_PARAMS, mvjcost) == SVTME_MVCOST_OFF_MVJCOST, "MV_COST_PARAMS.mvjcost");
+_Static_assert(offsetof(MV_COST_PARAMS, mvcost) == SVTME_MVCOST_OFF_MVCOST, "MV_COST_PARAMS.mvcost");
+_Static_assert(offsetof(MV_COST_PARAMS, error_per_bit) == SVTME_MVCOST_OFF_ERROR_PER_BIT,
+               "MV_COST_PARAMS.error_per_bit");
+_Static_assert(offsetof(MV, row) == 0 && offsetof(MV, col) == 2, "MV is (row, col) int16");
 
 static void glue_sad_loop(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride, uint32_t bh,
                           uint32_t bw, uint64_t *best_sad, int16_t *x, int16_t *y, uint32_t src_stride_raw,
@@ -123,6 +137,17 @@ static uint32_t glue_sad16b(uint16_t *src, uint32_t src_stride, uint16_t *ref, u
     return svtme_rtcd_failed() ? g_prev.sad16b(src, src_stride, ref, ref_stride, h, w) : v;
 }
 
+static void glue_pme(const struct svt_mv_cost_param *p, uint8_t *src, uint32_t src_stride, uint8_t *ref,
+                     uint32_t ref_stride, uint32_t bh, uint32_t bw, uint32_t *best_cost, int16_t *best_mvx,
+                     int16_t *best_mvy, int16_t sx, int16_t sy, int16_t sa_w, int16_t sa_h, int16_t step, int16_t mvx,
+                     int16_t mvy) {
+    svt_pme_sad_loop_kernel_hip(p, src, src_stride, ref, ref_stride, bh, bw, best_cost, best_mvx, best_mvy, sx, sy,
+                                sa_w, sa_h, step, mvx, mvy);
+    if (svtme_rtcd_failed())
+        g_prev.pme(p, src, src_stride, ref, ref_stride, bh, bw, best_cost, best_mvx, best_mvy, sx, sy, sa_w, sa_h,
+                   step, mvx, mvy);
+}
+
 /* Call right after svt_aom_setup_rtcd_internal(): the pointers it set become the
  * fallbacks, the HIP variants the active ones. */
 void svt_aom_setup_rtcd_hip(void) {
@@ -135,6 +160,7 @@ void svt_aom_setup_rtcd_hip(void) {
     g_prev.init32                = svt_initialize_buffer_32bits;
     g_prev.downsample            = downsample_2d;
     g_prev.sad16b                = sad_16b_kernel;
+    g_prev.pme                   = svt_pme_sad_loop_kernel;
 
     svt_sad_loop_kernel                       = glue_sad_loop;                /* :779 */
     svt_nxm_sad_kernel                        = glue_nxm;                     /* :856 */
@@ -145,6 +171,7 @@ void svt_aom_setup_rtcd_hip(void) {
     svt_initialize_buffer_32bits              = glue_init32;                  /* :855 */
     downsample_2d                             = glue_downsample;              /* :841 */
     sad_16b_kernel                            = glue_sad16b;                  /* :863 */
+    svt_pme_sad_loop_kernel                   = glue_pme;                     /* :868 */
 }
 
 /* --------------------------------------------------------------------------

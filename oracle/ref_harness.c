@@ -49,7 +49,19 @@ void svt_ext_all_sad_calculation_8x8_16x16_c(uint8_t *src, uint32_t src_stride, 
 void svt_ext_eight_sad_calculation_32x32_64x64_c(uint32_t p_sad16x16[16][8], uint32_t *p_best_sad_32x32,
                                                  uint32_t *p_best_sad_64x64, uint32_t *p_best_mv32x32,
                                                  uint32_t *p_best_mv64x64, uint32_t mv, uint32_t p_sad32x32[4][8]);
+void svt_pme_sad_loop_kernel_c(const struct svt_mv_cost_param *mv_cost_params, uint8_t *src, uint32_t src_stride,
+                               uint8_t *ref, uint32_t ref_stride, uint32_t block_height, uint32_t block_width,
+                               uint32_t *best_cost, int16_t *best_mvx, int16_t *best_mvy,
+                               int16_t search_position_start_x, int16_t search_position_start_y,
+                               int16_t search_area_width, int16_t search_area_height, int16_t search_step,
+                               int16_t mvx, int16_t mvy); /* product_coding_loop.c:1811 */
 #ifdef SVTREF_WITH_SIMD
+void svt_pme_sad_loop_kernel_avx2(const struct svt_mv_cost_param *mv_cost_params, uint8_t *src, uint32_t src_stride,
+                                  uint8_t *ref, uint32_t ref_stride, uint32_t block_height, uint32_t block_width,
+                                  uint32_t *best_cost, int16_t *best_mvx, int16_t *best_mvy,
+                                  int16_t search_position_start_x, int16_t search_position_start_y,
+                                  int16_t search_area_width, int16_t search_area_height, int16_t search_step,
+                                  int16_t mvx, int16_t mvy);
 void svt_sad_loop_kernel_avx2_intrin(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
                                      uint32_t block_height, uint32_t block_width, uint64_t *best_sad,
                                      int16_t *x_search_center, int16_t *y_search_center, uint32_t src_stride_raw,
@@ -92,8 +104,10 @@ void svtref_set_simd(int simd) {
     svt_ext_eight_sad_calculation_32x32_64x64 = svt_ext_eight_sad_calculation_32x32_64x64_c;
     svt_initialize_buffer_32bits              = svt_initialize_buffer_32bits_c;
     svt_nxm_sad_kernel                        = svt_nxm_sad_kernel_helper_c;
+    svt_pme_sad_loop_kernel                   = svt_pme_sad_loop_kernel_c;
 #ifdef SVTREF_WITH_SIMD
     if (simd) {
+        svt_pme_sad_loop_kernel                   = svt_pme_sad_loop_kernel_avx2;
         svt_sad_loop_kernel                       = svt_sad_loop_kernel_avx2_intrin;
         downsample_2d                             = svt_aom_downsample_2d_avx2;
         svt_ext_sad_calculation_8x8_16x16         = svt_ext_sad_calculation_8x8_16x16_avx2_intrin;
@@ -646,4 +660,16 @@ void svtref_downsample_2d(uint8_t *input_samples, uint32_t input_stride, uint32_
     ensure_kernels();
     downsample_2d(input_samples, input_stride, input_area_width, input_area_height, decim_samples, decim_stride,
                   decim_step);
+}
+
+void svtref_pme_sad_loop_kernel(const struct svt_mv_cost_param *mv_cost_params, uint8_t *src, uint32_t src_stride,
+                                uint8_t *ref, uint32_t ref_stride, uint32_t block_height, uint32_t block_width,
+                                uint32_t *best_cost, int16_t *best_mvx, int16_t *best_mvy,
+                                int16_t search_position_start_x, int16_t search_position_start_y,
+                                int16_t search_area_width, int16_t search_area_height, int16_t search_step,
+                                int16_t mvx, int16_t mvy) {
+    ensure_kernels();
+    svt_pme_sad_loop_kernel(mv_cost_params, src, src_stride, ref, ref_stride, block_height, block_width, best_cost,
+                            best_mvx, best_mvy, search_position_start_x, search_position_start_y, search_area_width,
+                            search_area_height, search_step, mvx, mvy);
 }

@@ -168,3 +168,78 @@ void svtora_downsample_2d(const uint8_t *input_samples, uint32_t input_stride, u
         }
     }
 }
+
+/* MV_COST_PARAMS (mcomp.h:37-48), restated layout: this file does not include
+ * the reference headers */
+typedef struct {
+    const int16_t *ref_mv; /* MV: row, col */
+    int16_t full_ref_mv[2];
+    uint8_t mv_cost_type; /* MV_COST_TYPE: UENUM1BYTE (mcomp.h:29-36) */
+    const int *mvjcost;
+    const int *mvcost[2];
+    int error_per_bit, early_exit_th, sad_per_bit;
+} ora_mv_cost_params;
+
+/* svt_mv_err_cost (mcomp.c:44-68) with svt_mv_cost (mcomp.h:134-137) and
+ * svt_av1_get_mv_joint (rd_cost.c:55-60); shift = RDDIV_BITS 7 +
+ * AV1_PROB_COST_SHIFT 9 - RD_EPB_SHIFT 6 + PIXEL_TRANSFORM_ERROR_SCALE 4 */
+static int ora_mv_err_cost(int16_t row, int16_t col, const ora_mv_cost_params *p) {
+    const int dr = (int16_t)(row - p->ref_mv[0]), dc = (int16_t)(col - p->ref_mv[1]);
+    const int ar = dr < 0 ? -dr : dr, ac = dc < 0 ? -dc : dc;
+    const int sh = 14;
+    switch (p->mv_cost_type) {
+    case 0: { /* the reference's `if (mvcost)` tests the array parameter: always taken */
+        const int j  = dr == 0 ? (dc == 0 ? 0 : 1) : (dc == 0 ? 2 : 3);
+        const int cr = dr < -16384 ? -16384 : (dr > 16384 ? 16384 : dr);
+        const int cc = dc < -16384 ? -16384 : (dc > 16384 ? 16384 : dc);
+        const int64_t v = (int64_t)(p->mvjcost[j] + p->mvcost[0][cr] + p->mvcost[1][cc]) * p->error_per_bit;
+        return (int)((v + (((int64_t)1 << sh) >> 1)) >> sh);
+    }
+    case 1: return (2 * (ar + ac)) >> 3;
+    case 2: return 0;
+    case 3: return (1 * (ar + ac)) >> 3;
+    case 4: {
+        const int64_t v = (int64_t)((ar + ac) << 8) * p->error_per_bit;
+        return (int)((v + (((int64_t)1 << sh) >> 1)) >> sh);
+    }
+    default: return 0;
+    }
+}
+
+/* svt_pme_sad_loop_kernel_c (product_coding_loop.c:1811-1860): the column
+ * counter and x step carry across rows; columns with fewer than 8 left are
+ * skipped while the counter is 0 */
+void svtora_pme_sad_loop_kernel(const void *mv_cost_params, const uint8_t *src, uint32_t src_stride,
+                                const uint8_t *ref, uint32_t ref_stride, uint32_t block_height,
+                                uint32_t block_width, uint32_t *best_cost, int16_t *best_mvx, int16_t *best_mvy,
+                                int16_t search_position_start_x, int16_t search_position_start_y,
+                                int16_t search_area_width, int16_t search_area_height, int16_t search_step,
+                                int16_t mvx, int16_t mvy) {
+    const ora_mv_cost_params *p = (const ora_mv_cost_params *)mv_cost_params;
+    int16_t col_num = 0, step_x = 1;
+    for (int16_t y = 0; y < search_area_height; y += search_step) {
+        for (int16_t x = 0; x < search_area_width; x += step_x) {
+            if ((search_area_width - x) < 8 && col_num == 0)
+                continue;
+            if (col_num == 7) {
+                col_num = 0;
+                step_x  = search_step;
+            } else {
+                col_num++;
+                step_x = 1;
+            }
+            uint32_t cost = 0;
+            for (uint32_t r = 0; r < block_height; r++)
+                for (uint32_t c = 0; c < block_width; c++)
+                    cost += absd(src[r * src_stride + c], ref[(size_t)y * ref_stride + x + r * ref_stride + c]);
+            const uint32_t rx = (uint32_t)(search_position_start_x + x), ry = (uint32_t)(search_position_start_y + y);
+            const int16_t col = (int16_t)(mvx + rx * 8), row = (int16_t)(mvy + ry * 8);
+            cost += (uint32_t)ora_mv_err_cost(row, col, p);
+            if (cost < *best_cost) {
+                *best_mvx  = col;
+                *best_mvy  = row;
+                *best_cost = cost;
+            }
+        }
+    }
+}

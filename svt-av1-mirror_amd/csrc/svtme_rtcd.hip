@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "svtme_device.h"
 
@@ -260,6 +261,33 @@ __global__ void k_downsample(const uint8_t *in, uint32_t in_stride, uint32_t w, 
     out[(size_t)oy * out_stride + ox] = (uint8_t)((s + 2) >> 2);
 }
 
+// --------------------------------------------------------------------------
+// svt_pme_sad_loop_kernel (product_coding_loop.c:1811-1860): one thread per
+// visited position (the host lists them in the reference's visit order with
+// their MV rate); block-level argmin by (sad + rate, visit index).
+// --------------------------------------------------------------------------
+__global__ void k_pme(const uint8_t *src, uint32_t src_stride, const uint8_t *ref, uint32_t ref_stride, uint32_t bh,
+                      uint32_t bw, const int16_t *px, const int16_t *py, const uint32_t *rate, int n,
+                      unsigned long long *best) {
+    __shared__ unsigned long long sbest;
+    if (threadIdx.x == 0)
+        sbest = ~0ull;
+    __syncthreads();
+    unsigned long long k = ~0ull;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint8_t *r = ref + (size_t)py[i] * ref_stride + px[i];
+        uint32_t sad     = 0;
+        for (uint32_t y = 0; y < bh; y++)
+            for (uint32_t x = 0; x < bw; x++) sad += absd(src[y * src_stride + x], r[(size_t)y * ref_stride + x]);
+        const unsigned long long kk = ((unsigned long long)(sad + rate[i]) << 32) | (uint32_t)i;
+        k                           = kk < k ? kk : k;
+    }
+    atomicMin(&sbest, k);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        *best = sbest;
+}
+
 } // namespace
 
 // --------------------------------------------------------------------------
@@ -495,4 +523,106 @@ extern "C" void svt_aom_downsample_2d_hip(uint8_t *input_samples, uint32_t input
     RT_CHECK(hipGetLastError(), "k_downsample");
     RT_CHECK(hipMemcpyAsync(decim_samples, dout, out_bytes, hipMemcpyDeviceToHost, g_rt.stream), "ds D2H");
     RT_CHECK(hipStreamSynchronize(g_rt.stream), "ds sync");
+}
+
+// MV rate of a full-pel candidate (svt_mv_err_cost, mcomp.c:44-68; svt_mv_cost,
+// mcomp.h:134; svt_av1_get_mv_joint, rd_cost.c:55), read through the
+// MV_COST_PARAMS layout of include/svtme.h
+static uint32_t pme_rate(const uint8_t *p, int16_t row, int16_t col) {
+    const int16_t *ref_mv = *(const int16_t *const *)(p + SVTME_MVCOST_OFF_REF_MV);
+    const int dr = row - ref_mv[0], dc = col - ref_mv[1];
+    const int ar = dr < 0 ? -dr : dr, ac = dc < 0 ? -dc : dc;
+    const int epb = *(const int *)(p + SVTME_MVCOST_OFF_ERROR_PER_BIT);
+    const int shift = 7 + 9 - 6 + 4; // RDDIV_BITS + AV1_PROB_COST_SHIFT - RD_EPB_SHIFT + PIXEL_TRANSFORM_ERROR_SCALE
+    switch (p[SVTME_MVCOST_OFF_TYPE]) {
+    case 0: { // MV_COST_ENTROPY (`if (mvcost)` tests the array parameter: always taken)
+        const int *jc = *(const int *const *)(p + SVTME_MVCOST_OFF_MVJCOST);
+        const int *const *cc = (const int *const *)(p + SVTME_MVCOST_OFF_MVCOST); // the reference's
+        const int joint = dr == 0 ? (dc == 0 ? 0 : 1) : (dc == 0 ? 2 : 3);
+        const int cr = dr < -(1 << 14) ? -(1 << 14) : dr > (1 << 14) ? (1 << 14) : dr;
+        const int ccl = dc < -(1 << 14) ? -(1 << 14) : dc > (1 << 14) ? (1 << 14) : dc;
+        const int64_t c = (int64_t)(jc[joint] + cc[0][cr] + cc[1][ccl]) * epb;
+        return (uint32_t)(int)((c + (((int64_t)1 << shift) >> 1)) >> shift);
+    }
+    case 1: return (uint32_t)((2 * (ar + ac)) >> 3); // MV_COST_L1_LOWRES
+    case 2: return 0;                                // MV_COST_L1_MIDRES (lambda 0)
+    case 3: return (uint32_t)((ar + ac) >> 3);       // MV_COST_L1_HDRES
+    case 4: {                                        // MV_COST_OPT
+        const int64_t c = (int64_t)((ar + ac) << 8) * epb;
+        return (uint32_t)(int)((c + (((int64_t)1 << shift) >> 1)) >> shift);
+    }
+    default: return 0; // MV_COST_NONE
+    }
+}
+
+extern "C" void svt_pme_sad_loop_kernel_hip(const struct svt_mv_cost_param *mv_cost_params, uint8_t *src,
+                                            uint32_t src_stride, uint8_t *ref, uint32_t ref_stride,
+                                            uint32_t block_height, uint32_t block_width, uint32_t *best_cost,
+                                            int16_t *best_mvx, int16_t *best_mvy, int16_t search_position_start_x,
+                                            int16_t search_position_start_y, int16_t search_area_width,
+                                            int16_t search_area_height, int16_t search_step, int16_t mvx,
+                                            int16_t mvy) {
+    if (search_area_width <= 0 || search_area_height <= 0 || search_step <= 0)
+        return;
+    // the reference's visit order (product_coding_loop.c:1823-1836): col_num and
+    // the x step persist across rows; a column whose remaining width is below 8
+    // is skipped while col_num == 0 (the step of the previous column applies)
+    std::vector<int16_t> px, py;
+    std::vector<uint32_t> rate;
+    const uint8_t *cp = (const uint8_t *)mv_cost_params;
+    int16_t col_num = 0, step_x = 1;
+    int maxx = 0, maxy = 0;
+    for (int16_t y = 0; y < search_area_height; y = (int16_t)(y + search_step)) {
+        for (int16_t x = 0; x < search_area_width; x = (int16_t)(x + step_x)) {
+            if ((search_area_width - x) < 8 && col_num == 0)
+                continue;
+            if (col_num == 7) {
+                col_num = 0;
+                step_x  = search_step;
+            } else {
+                col_num++;
+                step_x = 1;
+            }
+            const uint32_t rx = (uint32_t)(search_position_start_x + x), ry = (uint32_t)(search_position_start_y + y);
+            const int16_t mvc = (int16_t)(mvx + (rx * 8)), mvr = (int16_t)(mvy + (ry * 8));
+            px.push_back(x);
+            py.push_back(y);
+            rate.push_back(pme_rate(cp, mvr, mvc));
+            maxx = x > maxx ? x : maxx;
+            maxy = y > maxy ? y : maxy;
+        }
+    }
+    const int n = (int)px.size();
+    if (n == 0 || block_height == 0 || block_width == 0)
+        return;
+    const size_t sspan = span(block_height, src_stride, block_width);
+    const size_t rspan = (size_t)(maxy + block_height - 1) * ref_stride + maxx + block_width;
+    const size_t pos   = (size_t)n * (2 + 2 + 4);
+    uint8_t *d = scratch(sspan + rspan + pos + 64);
+    if (!d)
+        return;
+    uint8_t *ds = d, *dr = d + ((sspan + 15) & ~(size_t)15);
+    uint8_t *dp = dr + ((rspan + 15) & ~(size_t)15);
+    int16_t *dx = (int16_t *)dp, *dy = dx + n;
+    uint32_t *drate = (uint32_t *)(dp + (((size_t)n * 4 + 15) & ~(size_t)15));
+    unsigned long long *db = (unsigned long long *)((uint8_t *)drate + (((size_t)n * 4 + 15) & ~(size_t)15));
+    RT_CHECK(hipMemcpyAsync(ds, src, sspan, hipMemcpyHostToDevice, g_rt.stream), "pme H2D");
+    RT_CHECK(hipMemcpyAsync(dr, ref, rspan, hipMemcpyHostToDevice, g_rt.stream), "pme H2D");
+    RT_CHECK(hipMemcpyAsync(dx, px.data(), (size_t)n * 2, hipMemcpyHostToDevice, g_rt.stream), "pme H2D");
+    RT_CHECK(hipMemcpyAsync(dy, py.data(), (size_t)n * 2, hipMemcpyHostToDevice, g_rt.stream), "pme H2D");
+    RT_CHECK(hipMemcpyAsync(drate, rate.data(), (size_t)n * 4, hipMemcpyHostToDevice, g_rt.stream), "pme H2D");
+    hipLaunchKernelGGL(k_pme, dim3(1), dim3(256), 0, g_rt.stream, ds, src_stride, dr, ref_stride, block_height,
+                       block_width, dx, dy, drate, n, db);
+    RT_CHECK(hipGetLastError(), "k_pme");
+    unsigned long long k = ~0ull;
+    RT_CHECK(hipMemcpyAsync(&k, db, 8, hipMemcpyDeviceToHost, g_rt.stream), "pme D2H");
+    RT_CHECK(hipStreamSynchronize(g_rt.stream), "pme sync");
+    const uint32_t cost = (uint32_t)(k >> 32);
+    const int i         = (int)(uint32_t)k;
+    if (k != ~0ull && cost < *best_cost) {
+        const uint32_t rx = (uint32_t)(search_position_start_x + px[i]), ry = (uint32_t)(search_position_start_y + py[i]);
+        *best_mvx  = (int16_t)(mvx + (rx * 8));
+        *best_mvy  = (int16_t)(mvy + (ry * 8));
+        *best_cost = cost;
+    }
 }

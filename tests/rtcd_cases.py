@@ -69,6 +69,19 @@ EXT8 = [(sub, ss, rs, off, seed) for sub in (False, True) for (ss, rs, off, seed
 EXTALL = [(sub, ss, rs, off, seed) for sub in (False, True) for (ss, rs, off, seed) in
           [(64, 128, 0, 11), (127, 133, 1, 12), (64, 80, 3, 13)]]
 DOWNSAMPLE = [(w, h, step) for (w, h, step) in [(64, 64, 2), (37, 21, 2), (128, 72, 4), (9, 9, 4), (3, 2, 2)]]
+# svt_pme_sad_loop_kernel: (bw, bh, sa_w, sa_h, step, start_x, start_y, mvx, mvy, cost_type, src_stride,
+# ref_stride, content, error_per_bit, initial best cost)
+PME = [
+    (8, 8, 16, 12, 1, -8, -6, 24, -40, 0, 64, 160, "rand", 100, 0xFFFFFFFF),   # entropy rate
+    (16, 16, 30, 9, 2, -15, -4, 0, 0, 1, 127, 131, "rand", 60, 0xFFFFFFFF),    # L1 low-res, step 2, ragged width
+    (32, 32, 24, 16, 3, -12, -8, -100, 56, 3, 96, 200, "rand", 80, 0xFFFFFFFF),  # L1 HD, step 3
+    (64, 64, 17, 5, 1, -8, -2, 8, 8, 4, 64, 160, "rand", 1000, 0xFFFFFFFF),    # OPT
+    (8, 4, 7, 3, 1, -3, -1, 0, 0, 0, 8, 24, "rand", 90, 0xFFFFFFFF),           # width < 8: nothing visited
+    (4, 4, 40, 6, 2, -20, -3, 16, -16, 5, 16, 64, "flat", 0, 0xFFFFFFFF),      # no rate, ties: first minimum
+    (128, 64, 12, 4, 1, -6, -2, -8, 24, 2, 128, 160, "rand", 70, 0xFFFFFFFF),  # mid-res lambda 0
+    (16, 8, 33, 17, 2, -16, -8, 40, -8, 0, 32, 80, "sat", 200, 0xFFFFFFFF),    # saturated, entropy
+    (8, 8, 24, 8, 1, -12, -4, 0, 0, 0, 64, 64, "flat", 50, 1),                  # initial best beats all
+]
 
 
 def _mv(rng):
@@ -91,7 +104,8 @@ def _fn(lib, prefix, name):
     if prefix == "svt_":
         names = {"sad_loop_kernel": "svt_sad_loop_kernel_hip", "nxm_sad_kernel": "svt_nxm_sad_kernel_hip",
                  "sad_16b_kernel": "svt_aom_sad_16b_kernel_hip", "downsample_2d": "svt_aom_downsample_2d_hip",
-                 "initialize_buffer_32bits": "svt_initialize_buffer_32bits_hip"}
+                 "initialize_buffer_32bits": "svt_initialize_buffer_32bits_hip",
+                 "pme_sad_loop_kernel": "svt_pme_sad_loop_kernel_hip"}
         return getattr(lib, names.get(name, "svt_" + name + "_hip"))
     return getattr(lib, prefix + name)
 
@@ -211,6 +225,38 @@ def run_downsample(lib, prefix, case, seed):
     return {"out": out}
 
 
+class MvCostParams(C.Structure):
+    """MV_COST_PARAMS (reference mcomp.h:37-48)."""
+    _fields_ = [("ref_mv", C.POINTER(C.c_int16)), ("full_ref_mv", C.c_int16 * 2), ("mv_cost_type", C.c_uint8),
+                ("mvjcost", C.POINTER(C.c_int)), ("mvcost", C.POINTER(C.c_int) * 2), ("error_per_bit", C.c_int),
+                ("early_exit_th", C.c_int), ("sad_per_bit", C.c_int)]
+
+
+def run_pme(lib, prefix, case, seed):
+    bw, bh, sa_w, sa_h, step, sx, sy, mvx, mvy, ctype, ss, rs, kind, epb, best0 = case
+    rng = np.random.default_rng(seed)
+    src = _content(rng, ss * bh + bw + 16, kind)
+    ref = _content(rng, rs * (sa_h + bh + 1) + sa_w + bw + 16, kind)
+    ref_mv = np.array([int(rng.integers(-64, 64)), int(rng.integers(-64, 64))], np.int16)
+    jc = rng.integers(100, 2000, 4).astype(np.int32)
+    tabs = [rng.integers(0, 4000, 2 * 16384 + 1).astype(np.int32) for _ in range(2)]
+    p = MvCostParams()
+    p.ref_mv = ref_mv.ctypes.data_as(C.POINTER(C.c_int16))
+    p.mv_cost_type = ctype
+    p.mvjcost = jc.ctypes.data_as(C.POINTER(C.c_int))
+    for k in range(2):
+        p.mvcost[k] = C.cast(C.c_void_p(tabs[k].ctypes.data + 4 * 16384), C.POINTER(C.c_int))
+    p.error_per_bit = epb
+    best = C.c_uint32(best0)
+    bx, by = C.c_int16(-5), C.c_int16(-7)
+    f = _fn(lib, prefix, "pme_sad_loop_kernel")
+    f.restype = None
+    f(C.byref(p), _u8(src), C.c_uint32(ss), _u8(ref), C.c_uint32(rs), C.c_uint32(bh), C.c_uint32(bw), C.byref(best),
+      C.byref(bx), C.byref(by), C.c_int16(sx), C.c_int16(sy), C.c_int16(sa_w), C.c_int16(sa_h), C.c_int16(step),
+      C.c_int16(mvx), C.c_int16(mvy))
+    return {"cost": np.array([best.value], np.uint32), "mv": np.array([bx.value, by.value], np.int16)}
+
+
 def all_cases():
     """(name, callable(lib, prefix) -> dict) for every case."""
     cases = []
@@ -231,4 +277,6 @@ def all_cases():
         cases.append((f"init32_{i}", lambda lib, p, a=a, b=b, v=v: run_init(lib, p, a, b, v)))
     for i, c in enumerate(DOWNSAMPLE):
         cases.append((f"downsample_{i}", lambda lib, p, c=c, i=i: run_downsample(lib, p, c, 600 + i)))
+    for i, c in enumerate(PME):
+        cases.append((f"pme_{i}", lambda lib, p, c=c, i=i: run_pme(lib, p, c, 700 + i)))
     return cases

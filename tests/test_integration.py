@@ -31,13 +31,13 @@ def test_glue_compiles_against_reference_headers(tmp_path):
     # defines the glue, binds the reference's rtcd pointers and the library's C ABI
     for s in ("T svt_aom_setup_rtcd_hip", "T svtme_controls_from_me_context", "T svtme_job_from_pcs",
               "T svtme_scatter_sb", "T svtme_me_picture", "T svtme_picture_redecimated",
-              "U svt_sad_loop_kernel_hip", "U svtme_rtcd_failed", "U svtme_submit_picture",
+              "U svt_sad_loop_kernel_hip", "U svt_pme_sad_loop_kernel_hip", "U svtme_rtcd_failed", "U svtme_submit_picture",
               "U svtme_picture_invalidate"):
         assert s in syms, s
     for ptr in ("svt_sad_loop_kernel", "svt_nxm_sad_kernel", "downsample_2d", "sad_16b_kernel",
                 "svt_ext_all_sad_calculation_8x8_16x16", "svt_ext_eight_sad_calculation_32x32_64x64",
                 "svt_initialize_buffer_32bits", "svt_ext_sad_calculation_8x8_16x16",
-                "svt_ext_sad_calculation_32x32_64x64"):
+                "svt_ext_sad_calculation_32x32_64x64", "svt_pme_sad_loop_kernel"):
         assert f" {ptr}\n" in syms, ptr  # the RTCD_EXTERN pointer itself (aom_dsp_rtcd.h)
 
 
