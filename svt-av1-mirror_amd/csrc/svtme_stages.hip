@@ -1210,6 +1210,58 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
     return ((unsigned long long)(mt >> 15) << 32) | ((unsigned long long)(uint32_t)y << 16) | (mt & 0x7FFFu);
 }
 
+// One sixteenth of the SADs of the 64 x kh2 (sub) full-resolution source
+// block (LDS, rows 64 bytes apart) at HQ quads of position row y of a
+// full-resolution window (HME-L2): block rows 2g, 2g + 1 of lane g = lane & 15;
+// the 16 lanes of a row then sum their partial SADs (DPP) and every lane
+// returns the row's minimum key.
+__device__ __forceinline__ unsigned long long hme_tile64(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
+                                                         int y, int kh2, const uint8_t (*src)[64]) {
+    const int g = threadIdx.x & 15;
+    unsigned long long acc[HQ] = {0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < 2; kk++) {
+        const int k = 2 * g + kk;
+        if (k < kh2) {
+            const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)(y + 2 * k) * stride) + q0;
+            u32x4a4 L[5];
+#pragma unroll
+            for (int v = 0; v < 5; v++) L[v] = ldg4(rp + 4 * v);
+            uint32_t d[20];
+#pragma unroll
+            for (int v = 0; v < 5; v++) d[4 * v] = L[v].x, d[4 * v + 1] = L[v].y, d[4 * v + 2] = L[v].z, d[4 * v + 3] = L[v].w;
+#pragma unroll
+            for (int j4 = 0; j4 < 4; j4++) {
+                const uint4 sv = ((const uint4 *)src[k])[j4];
+                const uint32_t s4[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+                for (int jj = 0; jj < 4; jj++) {
+                    const int j = 4 * j4 + jj;
+#pragma unroll
+                    for (int qq = 0; qq < HQ; qq++) acc[qq] = qsad64(pair(d[qq + j], d[qq + j + 1]), s4[jj], acc[qq]);
+                }
+            }
+        }
+    }
+    uint32_t mt = U32MAX; // sad (< 2^19) << 13 | x (< 2^13)
+#pragma unroll
+    for (int qq = 0; qq < HQ; qq++) {
+        uint32_t a[4] = {0, 0, 0, 0};
+        qsad_unpack(acc[qq], a);
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            // the row's 16 lanes: quad xor 1 / 2, row_half_mirror, row_mirror
+            const uint32_t v = dpp_add<0x140>(dpp_add<0x141>(dpp_add<0x4E>(dpp_add<0xB1>(a[e]))));
+            const int x      = 4 * (q0 + qq) - sh + e;
+            if (x >= 0 && x < sa_w)
+                mt = min_u32(mt, (v << 13) | (uint32_t)x);
+        }
+    }
+    if (mt == U32MAX)
+        return ~0ull;
+    return ((unsigned long long)(mt >> 13) << 32) | ((unsigned long long)(uint32_t)y << 16) | (mt & 0x1FFFu);
+}
+
 // flat tile index -> search (binary search over item0, n > 0 searches)
 template <typename S>
 __device__ __forceinline__ int find_search(const S *t, int n, int it) {
@@ -2472,6 +2524,7 @@ struct HmeA { // state of phases A0 .. B
     int16_t hx[32], hy[32];
     uint64_t hsad[32];
     __attribute__((aligned(16))) uint8_t src4[16][32]; // quarter-resolution source, sub rows
+    __attribute__((aligned(16))) uint8_t src1[32][64]; // full-resolution source, sub rows (HME-L2)
 };
 
 // k_hme shared memory: the job copy, the SB's HME state, the per-record
@@ -2614,6 +2667,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
                     sh.u.a.zzacc[s] = acc;
             }
         }
+        // full-resolution source block (64 x 64, even rows) for HME-L2
+        if (c.enable_hme_level2_flag && tid >= 96 && tid < 224) {
+            const DevPlane &F = dj.cur.lv[0];
+            const int row = (tid - 96) >> 2, part = tid & 3;
+            const u32x4a4 v = ldg4((const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * row) * F.stride + G.ox + 16 * part));
+            ((uint4 *)sh.u.a.src1[row])[part] = make_uint4(v.x, v.y, v.z, v.w);
+        }
         // quarter-resolution source block (32 x 32, even rows) for HME-L1
         if (c.enable_hme_level1_flag && tid >= 224) {
             const DevPlane &Q = dj.cur.lv[1];
@@ -2705,7 +2765,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             sh.u.a.key1[lane] = ~0ull;
             const bool listed = c.enable_hme_flag && c.enable_hme_level1_flag && slot_valid(vmask, s) &&
                                 tl_or_l0(job, l);
-            if (listed) {
+            if (listed) { // hme_level1_b64 (motion_estimation.c:2041-2122)
                 const int16_t X0 = d.lx[s][q], Y0 = d.ly[s][q];
                 const uint64_t S0 = d.lsad[s][q];
                 bool done = false;
@@ -2777,23 +2837,90 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         }
     }
     __syncthreads();
+    // resolve the searched level-1 refinements (full-pel units: x 2)
+    if (wid == 0 && lane < 32 && sh.u.a.hsad[lane] == ~0ull) {
+        uint32_t best;
+        int x, y;
+        key_result(sh.u.a.key1[lane], &best, &x, &y);
+        sh.u.a.hsad[lane] = hsub ? (uint64_t)best * 2 : best;
+        sh.u.a.hx[lane]   = i16((x + sh.u.a.x1o[lane]) * 2);
+        sh.u.a.hy[lane]   = i16((y + sh.u.a.y1o[lane]) * 2);
+    }
+    if (c.enable_hme_level2_flag) { // hme_level2_b64 (motion_estimation.c:2127-2177), every listed (slot, quadrant)
+        if (wid == 0) {
+            const int s = lane >> 2, l = s >> 2;
+            bool mk   = false;
+            int items = 0;
+            HSrch1 e;
+            if (lane < 32) {
+                sh.u.a.key1[lane] = ~0ull;
+                const bool listed = c.enable_hme_flag && slot_valid(vmask, s) && tl_or_l0(job, l);
+                const bool keep   = c.prev_me_stage_based_exit_th &&
+                                  sh.u.a.hsad[lane] < (c.prev_me_stage_based_exit_th >> 2);
+                if (listed && !keep) { // hme_level_2 (:1025-1113) around the level-1 centre
+                    const DevPlane &P = dj.ref[l][s & 3].lv[0];
+                    int16_t xo, yo, sw, shh;
+                    hme_refine_rect(2, P, (int16_t)G.ox, (int16_t)G.oy, (int16_t)c.hme_l2_sa.width,
+                                    (int16_t)c.hme_l2_sa.height, sh.u.a.hx[lane], sh.u.a.hy[lane], &xo, &yo, &sw, &shh);
+                    sh.u.a.x1o[lane]  = xo;
+                    sh.u.a.y1o[lane]  = yo;
+                    sh.u.a.hsad[lane] = ~0ull; // searched: resolved from key1 below
+                    if (sw > 0 && shh > 0) {
+                        const uint8_t *w0 = P.base + (ptrdiff_t)((int16_t)G.oy + yo) * P.stride + ((int16_t)G.ox + xo);
+                        e.sh              = (uint8_t)((uintptr_t)w0 & 3);
+                        e.a0              = w0 - e.sh;
+                        e.sa_w            = sw;
+                        e.ncols           = (int16_t)((((e.sh + sw + 3) >> 2) + HQ - 1) / HQ);
+                        e.id              = (uint8_t)lane;
+                        items             = e.ncols * shh;
+                        mk                = true;
+                    }
+                }
+            }
+            int tot;
+            const int kpos = wave_compact(mk, &tot);
+            const int incl = wave_incl_scan(items);
+            if (mk) {
+                e.item0            = incl - items;
+                sh.u.a.s1[kpos] = e;
+            }
+            if (lane == 63)
+                sh.u.a.nitems1 = incl;
+            if (lane == 0)
+                sh.u.a.nsrch1 = tot;
+        }
+        __syncthreads();
+        {
+            const int nlanes = 16 * sh.u.a.nitems1, nsrch = sh.u.a.nsrch1;
+            const int pstride = dj.cur.lv[0].stride;
+            const int kh2     = (int)(G.bh >> 1);
+            for (int it16 = tid; it16 < nlanes; it16 += 256) {
+                const int it    = it16 >> 4;
+                const HSrch1 &e = sh.u.a.s1[find_search(sh.u.a.s1, nsrch, it)];
+                const int local = it - e.item0;
+                const int y = local / e.ncols, col = local - y * e.ncols;
+                const unsigned long long kk = hme_tile64(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh2, sh.u.a.src1);
+                if ((it16 & 15) == 0 && kk != ~0ull)
+                    atomicMin(&sh.u.a.key1[e.id], kk);
+            }
+        }
+        __syncthreads();
+        if (wid == 0 && lane < 32 && sh.u.a.hsad[lane] == ~0ull) {
+            uint32_t best;
+            int x, y;
+            key_result(sh.u.a.key1[lane], &best, &x, &y);
+            sh.u.a.hsad[lane] = hsub ? (uint64_t)best * 2 : best;
+            sh.u.a.hx[lane]   = i16(x + sh.u.a.x1o[lane]);
+            sh.u.a.hy[lane]   = i16(y + sh.u.a.y1o[lane]);
+        }
+    }
     HME_STAMP(5);
     BState *b = FP ? &sh.bs : dj.bst + sb_local;
     if (wid == 0) {
         if (lane < 32) {
-            int16_t X = sh.u.a.hx[lane], Y = sh.u.a.hy[lane];
-            uint64_t SD = sh.u.a.hsad[lane];
-            if (SD == ~0ull) { // searched (hme_level_1 result, full-pel x 2)
-                uint32_t best;
-                int x, y;
-                key_result(sh.u.a.key1[lane], &best, &x, &y);
-                SD = hsub ? (uint64_t)best * 2 : best;
-                X  = i16((x + sh.u.a.x1o[lane]) * 2);
-                Y  = i16((y + sh.u.a.y1o[lane]) * 2);
-            }
-            b->hx[0][lane]         = X;
-            b->hy[0][lane]         = Y;
-            b->hsad[0][lane]       = SD;
+            b->hx[0][lane]         = sh.u.a.hx[lane];
+            b->hy[0][lane]         = sh.u.a.hy[lane];
+            b->hsad[0][lane]       = sh.u.a.hsad[lane];
             (&b->lx[0][0])[lane]   = (&d.lx[0][0])[lane];
             (&b->ly[0][0])[lane]   = (&d.ly[0][0])[lane];
             (&b->lsad[0][0])[lane] = (&d.lsad[0][0])[lane];
@@ -2938,10 +3065,10 @@ extern "C" void svtme_hme_prepare(DevJob *dj) {
     }
 }
 
-// k_hme applies: every SB 64 wide, sub-sampled HME rows, level 2 off
+// k_hme applies: every SB 64 wide, sub-sampled HME rows
 extern "C" bool svtme_hme_fused(const svtme_job *job) {
     const svtme_controls &c = job->ctrl;
-    return (job->width % 64) == 0 && c.hme_search_method != SVTME_FULL_SAD_SEARCH && !c.enable_hme_level2_flag &&
+    return (job->width % 64) == 0 && c.hme_search_method != SVTME_FULL_SAD_SEARCH &&
            getenv("SVTME_NO_FUSED_HME") == nullptr;
 }
 
