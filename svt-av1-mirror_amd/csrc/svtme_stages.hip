@@ -2189,11 +2189,11 @@ __device__ __forceinline__ void fp_rows(PuMin<K32> &M, const uint32_t *a, int sd
 // global load per plane row and lane (uniform row base in SGPRs + the lane's
 // dword offset), every bound wave-uniform. Reads up to one dword right of the
 // window (plane margins / allocation slack).
-template <bool SUB>
+template <bool SUB, int TQ = 2> // TQ: position quads per load set (2: one 16-byte load per row, 6: two)
 __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint32_t *a, int sdw, int sh, int w, int nq, int y0,
                                           int y1, uint32_t obase, const uint32_t (&src)[SUB ? 4 : 8][2], int by,
                                           int bx) {
-    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1, NR = 1 + (ROWS - 1) * RSTEP;
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1, NL = (TQ + 2 + 3) / 4;
     a     = uni_ptr(a);
     sdw   = UNI(sdw);
     sh    = UNI(sh);
@@ -2204,29 +2204,38 @@ __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint32_t *a, int
     obase = (uint32_t)UNI(obase);
     const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2);
     for (int ty = y0; ty < y1; ty++) {
-        for (int tq = 0; tq < nq; tq += 2) {
+        for (int tq = 0; tq < nq; tq += TQ) {
             const uint32_t *rb = a + (ptrdiff_t)ty * sdw + tq;
-            u32x4a4 T[NR];
+            uint32_t D[ROWS][4 * NL];
 #pragma unroll
-            for (int i = 0; i < NR; i++) T[i] = ldg4(rb + (ptrdiff_t)i * sdw + lo);
-            unsigned long long a0 = 0, a1 = 0;
+            for (int rr = 0; rr < ROWS; rr++)
 #pragma unroll
-            for (int rr = 0; rr < ROWS; rr++) {
-                const u32x4a4 &R = T[rr * RSTEP];
-                a0 = qsad64(pair(R.x, R.y), src[rr][0], a0);
-                a0 = qsad64(pair(R.y, R.z), src[rr][1], a0);
-                a1 = qsad64(pair(R.y, R.z), src[rr][0], a1);
-                a1 = qsad64(pair(R.z, R.w), src[rr][1], a1);
-            }
-            const int x0 = 4 * tq - sh;
-            uint32_t l0 = (uint32_t)a0, h0 = (uint32_t)(a0 >> 32), l1 = (uint32_t)a1, h1 = (uint32_t)(a1 >> 32);
-            if (SUB) { // raw 8x4 SADs <= 8160: doubling stays inside each u16
-                l0 <<= 1, h0 <<= 1, l1 <<= 1, h1 <<= 1;
-            }
+                for (int v = 0; v < NL; v++) {
+                    const u32x4a4 t = ldg4(rb + (ptrdiff_t)(rr * RSTEP) * sdw + lo + 4 * v);
+                    D[rr][4 * v] = t.x, D[rr][4 * v + 1] = t.y, D[rr][4 * v + 2] = t.z, D[rr][4 * v + 3] = t.w;
+                }
+            unsigned long long acc[TQ];
+#pragma unroll
+            for (int iq = 0; iq < TQ; iq++) acc[iq] = 0;
+#pragma unroll
+            for (int rr = 0; rr < ROWS; rr++)
+#pragma unroll
+                for (int iq = 0; iq < TQ; iq++) {
+                    acc[iq] = qsad64(pair(D[rr][iq], D[rr][iq + 1]), src[rr][0], acc[iq]);
+                    acc[iq] = qsad64(pair(D[rr][iq + 1], D[rr][iq + 2]), src[rr][1], acc[iq]);
+                }
+            const int x0    = 4 * tq - sh;
             const uint32_t ob = obase + (uint32_t)(ty * w + x0);
-            M.add_quad(l0, h0, ob, x0, w);
-            if (tq + 1 < nq)
-                M.add_quad(l1, h1, ob + 4, x0 + 4, w);
+#pragma unroll
+            for (int iq = 0; iq < TQ; iq++) {
+                if (iq > 0 && tq + iq >= nq)
+                    break; // wave-uniform
+                uint32_t l0 = (uint32_t)acc[iq], h0 = (uint32_t)(acc[iq] >> 32);
+                if (SUB) { // raw 8x4 SADs <= 8160: doubling stays inside each u16
+                    l0 <<= 1, h0 <<= 1;
+                }
+                M.add_quad(l0, h0, ob + 4 * iq, x0 + 4 * iq, w);
+            }
         }
     }
 }
@@ -2239,7 +2248,7 @@ __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint32_t *a, int
 // the full-pel search of search rows [h * part / parts, h * (part + 1) / parts);
 // the 85-PU argmin keys go to kp (atomic min when parts > 1), the slot state
 // to cs (part 0). src: this lane's 8x8 source block rows (lane = block by, bx).
-template <bool SUB, bool K32, int TQ = (SUB ? FP_TQ : 2)>
+template <bool SUB, bool K32, int TQ = (SUB ? FP_TQ : 2), bool WIDE = false>
 __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s, const uint32_t (&src)[SUB ? 4 : 8][2],
                                         int by, int bx, uint64_t hme_sad, uint32_t zz, uint32_t rdiv, int16_t sc_x,
                                         int16_t sc_y, uint8_t dref, uint8_t tf_exit, int part, uint32_t parts,
@@ -2352,7 +2361,8 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     const int y0 = (int)(((uint32_t)h * part) / parts), y1 = (int)(((uint32_t)h * (part + 1)) / parts);
     const uint32_t obase = probe ? 1u : 0u; // the centre probe wins ties: order 0
     if constexpr (K32)
-        fp_rows32<SUB>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
+        fp_rows32<SUB, WIDE ? 6 : 2>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by,
+                                     bx);
     else
         fp_rows<SUB, K32, TQ>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
     M.finalize();
@@ -2381,7 +2391,7 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
 
 
 // K32: every order fits 12 bits (the host bounds the area, svtme_fp_k32)
-template <bool SUB, bool K32>
+template <bool SUB, bool K32, bool WIDE = false> // WIDE: 6-quad full-pel load sets (areas >= 24 wide)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 5 : 4, 8))) k_stage_c1(const DevBatch B) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
@@ -2425,7 +2435,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
     const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
     CSlot *cs = dj.cslot + (size_t)sb_local * dj.R + k;
     unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
-    fp_slot<SUB, K32>(dj, G, s, src, by, bx, hme_sad, zz, rdiv, sc_x, sc_y, dref, tf_exit, part, parts, kp, cs);
+    fp_slot<SUB, K32, (SUB ? FP_TQ : 2), WIDE>(dj, G, s, src, by, bx, hme_sad, zz, rdiv, sc_x, sc_y, dref, tf_exit, part,
+                                             parts, kp, cs);
 }
 
 // Per SB: decode the argmin keys kb[k][85] of the R records (slot state cin[k])
@@ -3078,6 +3089,11 @@ extern "C" bool svtme_fp_k32(const svtme_controls *c) {
     return (c->me_8x8_var_enabled ? 1u : 0u) + w * h <= 4096u; // order 0 is the variance probe
 }
 
+// the full-pel area's minimum width reaches 24 positions: 6-quad load sets pay
+extern "C" bool svtme_fp_wide(const svtme_controls *c) {
+    return c->me_sa.sa_min.width >= 24 && c->me_sa.sa_max.width >= 24;
+}
+
 extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {
     if (c->enable_me_sr_adjustment == 2)
         return 0; // slot 0's 64x64 SAD feeds the other slots' areas: per-SB k_stage_c
@@ -3093,7 +3109,7 @@ extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
     const bool full = dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     return (uint32_t)full | (uint32_t)(dj->parts != 0) << 1 | (uint32_t)svtme_fp_k32(&dj->job.ctrl) << 2 |
            (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4 |
-           (uint32_t)(dj->parts == 1) << 5;
+           (uint32_t)(dj->parts == 1) << 5 | (uint32_t)svtme_fp_wide(&dj->job.ctrl) << 6;
 }
 
 static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
@@ -3165,10 +3181,15 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     if (h0.parts) { // wide full-pel stage + per-SB decode
         const DevBatch bc = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.R * j.parts; });
         const dim3 grid((bc.total + 3) / 4);
-        if (full && k32)
+        const bool wide = svtme_fp_wide(&h0.job.ctrl);
+        if (full && k32 && wide)
+            SVTME_LAUNCH((svtme::k_stage_c1<false, true, true>), grid, 3, bc);
+        else if (full && k32)
             SVTME_LAUNCH((svtme::k_stage_c1<false, true>), grid, 3, bc);
         else if (full)
             SVTME_LAUNCH((svtme::k_stage_c1<false, false>), grid, 3, bc);
+        else if (k32 && wide)
+            SVTME_LAUNCH((svtme::k_stage_c1<true, true, true>), grid, 3, bc);
         else if (k32)
             SVTME_LAUNCH((svtme::k_stage_c1<true, true>), grid, 3, bc);
         else
