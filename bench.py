@@ -47,14 +47,17 @@ sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
 
 METRIC = "open-loop ME 64x64 superblocks/sec + achieved HBM GB/s, 4K preset-8"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md, chip-level parameters)
-# v_sad_u8: 4 absdiffs per lane, 64 lanes per CU per clock, 256 CUs, 2.4 GHz
-SAD_PEAK_T = 4 * 64 * 256 * 2.4e9 / 1e12
+# SAD-instruction roof measured on MI355X (scripts/ubench_sad.hip, profiles/r02_ubench_sad.json): v_sad_u8
+# 150.3 T absdiff/s (0.96 wave-instr/clk/CU), v_qsad_pk_u16_u8 142.6 T/s (17.6 clk per wave-instr per SIMD)
+SAD_PEAK_T = 150.3
 STAGES = ("k_stage_a", "k_stage_d", "k_stage_b", "k_stage_c1", "k_stage_e")
-STAGES_FUSED = ("k_hme", "-", "-", "k_stage_c1", "k_stage_e")  # k_hme = stages A + D + B in one launch
+STAGES_FUSED = ("k_hme", "-", "-", "k_stage_c1", "k_stage_e")  # k_hme = stages A + D + B (+ C1 + E) in one launch
 # SURVEY.md 8(d) p8 byte split over the stage kernels: zz 2048 + pre-HME 2645 + 1034 +
 # HME-L0 1081 (+ source 64x32 + 16x8) | HME-L1 5304 (+ source 32x16) | full-pel 4686 + 680 out
 STAGE_BYTES_P8 = {"k_stage_a": (2176, 6808), "k_stage_d": (0, 0), "k_stage_b": (512, 5304),
                   "k_stage_c1": (0, 4686), "k_stage_e": (0, 680), "k_hme": (2688, 12112)}
+# the whole pass in k_hme (fused full-pel + decode): every byte of the pass
+STAGE_BYTES_P8_ALL = (2688, 16798 + 680)
 PICTURE_STRIDE = 32  # picture p of a step pans from t = 8 + 32 p (distinct content per picture)
 
 
@@ -216,7 +219,7 @@ def main():
             continue
         e = {"avg_ms": round(stage_ms[k], 4), "share": round(stage_ms[k] / kern_ms, 3)}
         if wl["windows"] == "p8":
-            src_b, per_ref = STAGE_BYTES_P8[st]
+            src_b, per_ref = STAGE_BYTES_P8_ALL if (fused and stage_ms[3] <= 0) else STAGE_BYTES_P8[st]
             sb_b = (src_b + R * per_ref) * sbs_launch
             if sb_b:
                 e["bytes_per_launch"] = sb_b
@@ -262,7 +265,7 @@ def main():
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "ME pass: " + " -> ".join(n for n in names if n != "-") +
+                         "kernel": "ME pass: " + " -> ".join(n for k, n in enumerate(names) if stage_ms[k] > 0) +
                                    " (one launch each, back to back on the library stream)",
                          "pass_ms": round(device_ms, 4), "kernel_sum_ms": round(kern_ms, 4),
                          "kernel_samples": n_timed,

@@ -2546,6 +2546,8 @@ struct HmeSh {
     BState bs;
     CSlot cin[8]; // by record
     CSlot csl[8]; // by slot (stage_e_body)
+    SlotCentre cen[8]; // final search centre / pruning by slot
+    uint8_t tf_exit;
     union U {
         HmeA a;
         StC st;
@@ -2559,8 +2561,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     __shared__ HmeSh sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = UNI(tid >> 6);
     uint32_t sb_local;
+    // the job in the job table (scalar loads where the reads are wave-uniform: the
+    // full-pel and decode phases) and its LDS copy (per-lane reads of the HME phases)
+    const DevJob &gj = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
     {
-        const DevJob &gj = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
         const uint32_t *js = (const uint32_t *)&gj;
         uint32_t *jd       = (uint32_t *)&sh.dj;
         for (int i = tid; i < (int)(sizeof(DevJob) / 4); i += 256) jd[i] = js[i];
@@ -2946,13 +2950,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         return;
     }
     __syncthreads(); // phase A..B state is dead from here (StC overlays it)
-    // ---- C: integer_search_b64 of every record, one wavefront each (k_stage_c1, one band)
-    {
+    // ---- C: set_final_seach_centre_sb / hme_prune_ref_and_adjust_sr once (wave 0), then
+    // integer_search_b64 of every record, one wavefront each (k_stage_c1, one band)
+    if (wid == 0) {
+        const SlotCentre scv = final_centre(job, &sh.bs, vmask); // lane = slot
+        if (lane < 8)
+            sh.cen[lane] = scv;
+        if (lane == 0)
+            sh.tf_exit = job.me_type == SVTME_ME_MCTF && scv.hme_sad < job.tf_me_exit_th; // :3109-3113
+    }
+    __syncthreads();
+    for (int k = wid; k < (int)dj.R; k += 4) {
         constexpr int ROWS = SUB_ME ? 4 : 8, RSTEP = SUB_ME ? 2 : 1;
         const int z16 = lane >> 2, k4 = lane & 3;
         const int by  = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
         const int bx  = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
-        const DevPlane &C = dj.cur.lv[0];
+        const DevPlane &C = gj.cur.lv[0];
         uint32_t src[ROWS][2];
 #pragma unroll
         for (int rr = 0; rr < ROWS; rr++) {
@@ -2961,21 +2974,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             src[rr][0] = sp[0];
             src[rr][1] = sp[1];
         }
-        const SlotCentre scv = final_centre(job, &sh.bs, vmask); // lane = slot
-        const bool mctf      = job.me_type == SVTME_ME_MCTF;
-        const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
-        for (int k = wid; k < (int)dj.R; k += 4) {
-            const int s = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
-            fp_slot<SUB_ME, K32, 2>(dj, G, s, src, by, bx, rl64(scv.hme_sad, s), rl32(scv.zz, s),
-                                 rl32(scv.reduce_div, s), (int16_t)rl32((uint32_t)(int32_t)scv.sc_x, s),
-                                 (int16_t)rl32((uint32_t)(int32_t)scv.sc_y, s), (uint8_t)rl32(scv.do_ref, s), tf_exit,
-                                 0, 1u, &sh.u.st.keys[k][0], &sh.cin[k]);
-        }
+        const int s         = k < gj.job.num_refs[0] ? k : 4 + (k - gj.job.num_refs[0]);
+        const SlotCentre &v = sh.cen[s];
+        fp_slot<SUB_ME, K32, 2>(gj, G, s, src, by, bx, rl64(v.hme_sad, 0), (uint32_t)UNI(v.zz), (uint32_t)UNI(v.reduce_div),
+                                (int16_t)UNI(v.sc_x), (int16_t)UNI(v.sc_y), (uint8_t)UNI(v.do_ref),
+                                (uint8_t)UNI(sh.tf_exit), 0, 1u, &sh.u.st.keys[k][0], &sh.cin[k]);
     }
     __syncthreads();
     HME_STAMP(6);
     // ---- E: decode, me_prune_ref, records, candidates / distortions / GM detection
-    stage_e_body(sh.u.st, sh.csl, dj, sb_local, G, vmask, sh.cin, &sh.u.st.keys[0][0], false);
+    stage_e_body(sh.u.st, sh.csl, gj, sb_local, G, vmask, sh.cin, &sh.u.st.keys[0][0], false);
     HME_STAMP(7);
 }
 
@@ -3151,7 +3159,8 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     const DevBatch bd = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
     const bool full = h0.job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     const bool k32  = svtme_fp_k32(&h0.job.ctrl);
-    if (svtme_hme_fused(&h0.job) && h0.parts == 1 && getenv("SVTME_FUSED_FP")) { // the whole pass in one launch
+    // the whole pass in one launch; SVTME_SPLIT_PASS=1 keeps k_hme -> k_stage_c1 -> k_stage_e (diagnostics)
+    if (svtme_hme_fused(&h0.job) && h0.parts == 1 && !getenv("SVTME_SPLIT_PASS")) {
         if (full && k32)
             SVTME_LAUNCH((svtme::k_hme<true, false, true>), dim3(bd.total), 0, bd);
         else if (full)
