@@ -1276,7 +1276,7 @@ __device__ __forceinline__ int find_search(const S *t, int n, int it) {
     return lo;
 }
 
-#define HT16 2 // position rows per 1/16 tile
+#define HT16 3 // position rows per 1/16 tile (4K p8: 190 tiles per SB, one pass of the workgroup)
 
 
 // ----------------------------------------------------------------------------
