@@ -6,6 +6,8 @@ non-base layers, 1..4 refs per list, P and B pictures, partial SBs at the
 right/bottom edges, presets 4/6/8/12 (check_00_center, HME-L2, pre-HME with
 line skipping, 8x8-variance resize), flat/saturated/noise content for ties.
 """
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -180,6 +182,32 @@ def test_banded_fullpel_parity(svtme, gpu):
     assert not _controls_case(S, gpu, S.derive_controls(8, 35, S.input_resolution_of(640, 360), 1), 640, 360,
                               (7, 6), (9, 10))
     assert not _controls_case(S, gpu, ctrl, 640, 360, (7,), ())
+
+
+@pytest.mark.parametrize("area,th,k32", [((64, 48), "grow", False), ((80, 64), "shrink", False),
+                                         ((64, 48), "shrink", True), ((32, 24), "grow", True),
+                                         ((48, 32), "shrink", True), ((48, 32), "derived", True)])
+def test_banded_fullpel_variance_parity(svtme, gpu, area, th, k32):
+    """Banded full-pel search WITH the 8x8-variance centre probe: every band
+    re-inserts the probe's key at order 0, which the decode reads as the
+    centre; the area grows (x 3/2) or shrinks (/2, /4) after the probe, with
+    64-bit and 32-bit argmin keys."""
+    S = svtme
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(640, 360), 1)
+    ctrl.me_sa.sa_min.width = ctrl.me_sa.sa_max.width = area[0]
+    ctrl.me_sa.sa_min.height = ctrl.me_sa.sa_max.height = area[1]
+    ctrl.me_8x8_var_enabled = 1
+    ctrl.enable_me_sr_adjustment = 0
+    ctrl.me_early_exit_th = 0  # check_00_center on as well
+    if th == "grow":
+        ctrl.me_sr_div4_th, ctrl.me_sr_div2_th, ctrl.me_sr_mult2_th = 0, 0, 0
+    elif th == "shrink":
+        ctrl.me_sr_div4_th, ctrl.me_sr_div2_th, ctrl.me_sr_mult2_th = 0xFFFFFFF, 0xFFFFFFF, 0xFFFFFFFF
+    lib = S.load_product()
+    lib.svtme_fp_k32.restype = C.c_bool
+    assert lib.svtme_fp_parts(C.byref(ctrl)) > 1, "the case must take the banded path"
+    assert lib.svtme_fp_k32(C.byref(ctrl)) == k32
+    assert not _controls_case(S, gpu, ctrl, 640, 360, (7, 6), (9,))
 
 
 def test_picture_invalidate(svtme, gpu):
