@@ -47,12 +47,16 @@ def main():
     gpu.sync()
     lib = S.load_product()
     nb = n_sb * P
-    st = np.zeros((nb, 8), np.uint64)
+    st = np.zeros((nb, 16), np.uint64)
     fn = lib.svtme_debug_hme_stamps
     fn.argtypes = [C.c_void_p, C.c_uint32]
     fn.restype = C.c_int
     assert fn(st.ctypes.data, nb) == 0
     st = st.astype(np.int64)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{name}_x{P}.npy"), st)
+    rt, ids, st_w = st[:, 8:10], st[:, 10:12], st[:, 12:16]
+    st = st[:, :8]
     if not st[:, 7].any():  # HME-only build: the last stamp is 6
         st = st[:, :7]
     d = np.diff(st, axis=1)
@@ -61,6 +65,26 @@ def main():
     for k, ph in enumerate(PHASES[: d.shape[1]]):
         v = d[:, k]
         print(f"  {ph:14s} mean {v.mean():8.0f}  p50 {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}  max {v.max():8.0f}")
+    # the 100 MHz real-time clock is chip-wide: launch span, start / end spread
+    t0 = rt[:, 0].min()
+    s0, s1 = (rt[:, 0] - t0) * 10.0, (rt[:, 1] - t0) * 10.0  # ns
+    print(f"  real time: span {s1.max():.0f} ns; WG start p50 {np.median(s0):.0f} p90 {np.percentile(s0, 90):.0f} "
+          f"max {s0.max():.0f}; WG end p10 {np.percentile(s1, 10):.0f} p50 {np.median(s1):.0f} max {s1.max():.0f}; "
+          f"WG duration p50 {np.median(s1 - s0):.0f} max {(s1 - s0).max():.0f}")
+    xcc = ids[:, 0] & 0xF
+    for x in range(8):
+        m = xcc == x
+        if m.any():
+            print(f"  XCC {x}: {m.sum():4d} WGs (blockIdx%8 = {sorted(set((np.nonzero(m)[0] % 8).tolist()))[:4]}) "
+                  f"start max {s0[m].max():.0f} end max {s1[m].max():.0f} ns")
+    cu = (ids[:, 1] >> 8) & 0xF
+    se = (ids[:, 1] >> 13) & 0x7
+    key = xcc * 1000 + se * 100 + cu
+    _, cnt = np.unique(key, return_counts=True)
+    simd = (st_w >> 4) & 3
+    print("  SIMD of waves 0-3, share of WGs with wave w on SIMD (w + r) & 3, r = 0..3:",
+          [[round(float(np.mean(simd[:, w] == ((w + r) & 3))), 2) for r in range(4)] for w in range(4)])
+    print(f"  distinct CUs {len(cnt)}; WGs per CU min {cnt.min()} p50 {np.median(cnt):.0f} max {cnt.max()}")
     gpu.close()
 
 

@@ -1033,11 +1033,28 @@ __device__ __forceinline__ SlotCentre final_centre(const svtme_job &job, const B
 // Diagnostic build (-DSVTME_STAMPS, scripts/hme_stamps.py): thread 0 of every
 // k_hme workgroup records the shader clock at each phase boundary.
 #ifdef SVTME_STAMPS
-__device__ unsigned long long g_hme_stamps[1 << 17][8];
+__device__ unsigned long long g_hme_stamps[1 << 17][16];
+// slots 0-7 shader clock per phase; 8 / 9 the 100 MHz real-time clock at the
+// first / latest stamp; 10 XCC_ID, 11 HW_ID (CU, SE) register values; 12-15
+// HW_ID of waves 0-3
 #define HME_STAMP(k)                                                                                                   \
     do {                                                                                                               \
-        if (threadIdx.x == 0 && blockIdx.x < (1u << 17))                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < (1u << 17)) {                                                             \
             g_hme_stamps[blockIdx.x][k] = __builtin_readcyclecounter();                                                \
+            g_hme_stamps[blockIdx.x][(k) == 0 ? 8 : 9] = __builtin_amdgcn_s_memrealtime();                             \
+            if ((k) == 0) {                                                                                            \
+                g_hme_stamps[blockIdx.x][10] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));                   \
+                g_hme_stamps[blockIdx.x][11] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                    \
+            }                                                                                                          \
+        }                                                                                                              \
+        if ((k) == 0 && (threadIdx.x & 63) == 0 && blockIdx.x < (1u << 17))                                            \
+            g_hme_stamps[blockIdx.x][12 + (threadIdx.x >> 6)] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));   \
+    } while (0)
+#elif defined(SVTME_STOP_AFTER) // diagnostic build (scripts/gpu_phase_cost.sh): k_hme ends after that phase
+#define HME_STAMP(k)                                                                                                   \
+    do {                                                                                                               \
+        if ((k) == SVTME_STOP_AFTER)                                                                                   \
+            return;                                                                                                    \
     } while (0)
 #else
 #define HME_STAMP(k)
@@ -1051,6 +1068,18 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ u32x4a4 ldg4(const uint32_t *p) {
     typedef __attribute__((address_space(1))) const u32x4a4 gu4;
     return *(gu4 *)(uintptr_t)p;
+}
+// raw buffer over a plane from a dword-aligned base (gfx9 descriptor word 3),
+// and a 16-byte load at lane offset voff + uniform offset soff (bytes): the
+// address adds go to the load unit, none to the VALU
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, (int)0xFFFFFFFF, 0x00020000);
+}
+__device__ __forceinline__ u32x4a4 bld4(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, (int)soff, 0);
+    u32x4a4 o;
+    o.x = v[0], o.y = v[1], o.z = v[2], o.w = v[3];
+    return o;
 }
 // 16 uniform bytes through the scalar cache (p wave-uniform, 4-byte aligned)
 __device__ __forceinline__ uint4 sld4(const uint8_t *p) {
@@ -2044,13 +2073,6 @@ struct PuMin {
             return (key_t)((sad << 12) | o);
         return (key_t)(((unsigned long long)sad << 32) | o);
     }
-    __device__ __forceinline__ static unsigned long long wide(key_t k) {
-        if (K32) {
-            const uint32_t v = (uint32_t)k;
-            return v == 0xFFFFFFFFu ? ~0ull : (((unsigned long long)(v >> 12) << 32) | (v & 0xFFFu));
-        }
-        return (unsigned long long)k;
-    }
     __device__ __forceinline__ void add(uint32_t s8, uint32_t o) {
         const uint32_t s16 = dpp_add<0x4E>(dpp_add<0xB1>(s8));              // xor 1, xor 2
         const uint32_t s32 = dpp_add<0x128>(dpp_add<0x124>(s16));           // row_ror 4, 8
@@ -2061,55 +2083,99 @@ struct PuMin {
         b32 = k32 < b32 ? k32 : b32;
         b64 = k64 < b64 ? k64 : b64;
     }
-    // K32: the 4 positions x0 + e (orders o0 + e) of an aligned quad, SADs packed
-    // as u16 pairs (lo: e = 0, 1; hi: e = 2, 3; already doubled for SUB). The
-    // 8x8 minima take all 4 positions per lane; the 16x16 / 32x32 / 64x64
-    // minima are lane-specialised: lane g = lane & 3 of each 4-lane group
-    // keeps position g only (16x16 sums on the packed pairs, <= 65280), so b16 /
-    // b32 / b64 hold minima over positions = g (mod 4) until finalize().
-    __device__ __forceinline__ void add_quad(uint32_t lo, uint32_t hi, uint32_t o0, int x0, int w) {
+    // K32 search (fp_rows32): SADs stay raw (SUB: the 8x4 sums, doubled only by
+    // out()); b8 keys are (sad << 16 | order) (an 8x8 SAD < 2^15), b16 / b32 / b64
+    // (sad << 12 | order). Two aligned position quads, a = x0 + e and b = x0 + 4
+    // + e (orders o0 + e, o0 + 4 + e), SADs packed as u16 pairs (l: e = 0, 1;
+    // h: e = 2, 3). The 8x8 minima take all 8 positions per lane; the 16x16 /
+    // 32x32 minima are lane-specialised: lane g = lane & 3 of each 4-lane group
+    // keeps positions = g (mod 4) (16x16 sums on the packed pairs, <= 32640);
+    // the 64x64 minima in addition by row: one permlane16_swap sums the 32x32
+    // quadrant pairs of both quads, rows with qb = 1 keep quad b. finalize()
+    // reduces the classes.
+    // INNER: both quads inside the area (the caller's wave-uniform test).
+    template <bool INNER>
+    __device__ __forceinline__ void add_quads(uint32_t la, uint32_t ha, uint32_t lb, uint32_t hb, uint32_t o0, int x0,
+                                              int w, uint32_t qb) {
         const int g = threadIdx.x & 3;
-        if (x0 >= 0 && x0 + 3 < w) { // wave-uniform: whole quad inside the area
-            const uint32_t k0 = ((lo & 0xFFFFu) << 12) | o0, k1 = ((lo >> 16) << 12) | (o0 + 1);
-            const uint32_t k2 = ((hi & 0xFFFFu) << 12) | (o0 + 2), k3 = ((hi >> 16) << 12) | (o0 + 3);
-            b8 = min_u32(min_u32((uint32_t)b8, min_u32(k0, k1)), min_u32(k2, k3));
+        if (INNER) {
+            b8 = min_u32(min_u32((uint32_t)b8, (la << 16) | o0), (la & 0xFFFF0000u) | (o0 + 1));
+            b8 = min_u32(min_u32((uint32_t)b8, (ha << 16) | (o0 + 2)), (ha & 0xFFFF0000u) | (o0 + 3));
+            b8 = min_u32(min_u32((uint32_t)b8, (lb << 16) | (o0 + 4)), (lb & 0xFFFF0000u) | (o0 + 5));
+            b8 = min_u32(min_u32((uint32_t)b8, (hb << 16) | (o0 + 6)), (hb & 0xFFFF0000u) | (o0 + 7));
         } else {
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
+            for (int e = 0; e < 8; e++) {
                 const int x = x0 + e;
                 if (x < 0 || x >= w)
                     continue; // wave-uniform
-                const uint32_t v = e < 2 ? lo : hi;
-                const uint32_t sd = (e & 1) ? (v >> 16) : (v & 0xFFFFu);
-                b8 = min_u32((uint32_t)b8, (sd << 12) | (o0 + e));
+                const uint32_t v = e < 2 ? la : e < 4 ? ha : e < 6 ? lb : hb;
+                b8 = min_u32((uint32_t)b8, ((e & 1) ? (v & 0xFFFF0000u) : (v << 16)) | (o0 + e));
             }
         }
-        const uint32_t L = dpp_add<0x4E>(dpp_add<0xB1>(lo)), H = dpp_add<0x4E>(dpp_add<0xB1>(hi));
-        const uint32_t v = (g & 2) ? H : L;
-        const uint32_t s16 = (g & 1) ? (v >> 16) : (v & 0xFFFFu);
-        const uint32_t s32 = dpp_add<0x128>(dpp_add<0x124>(s16)); // row_ror 4, 8: same g
-        // 64x64: the 4 rows' s32 of the same g (row_bcast would mix the classes):
-        // permlane16_swap / permlane32_swap of a register with itself leave the two
-        // rows (halves) being summed in the pair of outputs of every lane
-        const auto p16     = __builtin_amdgcn_permlane16_swap(s32, s32, false, false);
+        const uint32_t La = dpp_add<0x4E>(dpp_add<0xB1>(la)), Ha = dpp_add<0x4E>(dpp_add<0xB1>(ha));
+        const uint32_t Lb = dpp_add<0x4E>(dpp_add<0xB1>(lb)), Hb = dpp_add<0x4E>(dpp_add<0xB1>(hb));
+        const uint32_t sel = (uint32_t)(g & 1) * 16;
+        const uint32_t s16a = (((g & 2) ? Ha : La) >> sel) & 0xFFFFu;
+        const uint32_t s16b = (((g & 2) ? Hb : Lb) >> sel) & 0xFFFFu;
+        const uint32_t s32a = dpp_add<0x128>(dpp_add<0x124>(s16a)); // row_ror 4, 8: same g
+        const uint32_t s32b = dpp_add<0x128>(dpp_add<0x124>(s16b));
+        // 64x64: rows 2j, 2j + 1 of the swap hold one quad's quadrants 2j + 1 and
+        // 2j, which quad is qb; the permlane32_swap of the sum with itself adds
+        // the other row pair
+        const auto p16     = __builtin_amdgcn_permlane16_swap(s32a, s32b, false, false);
         const uint32_t t   = p16[0] + p16[1];
         const auto p32     = __builtin_amdgcn_permlane32_swap(t, t, false, false);
         const uint32_t s64 = p32[0] + p32[1];
-        const int x = x0 + g;
-        if (x >= 0 && x < w) {
-            const uint32_t og = o0 + (uint32_t)g;
-            b16 = min_u32((uint32_t)b16, (s16 << 12) | og);
-            b32 = min_u32((uint32_t)b32, (s32 << 12) | og);
-            b64 = min_u32((uint32_t)b64, (s64 << 12) | og);
+        const uint32_t oa = o0 + (uint32_t)g, ob = oa + 4, o64 = oa + 4 * qb;
+        if (INNER) {
+            b16 = min_u32(min_u32((uint32_t)b16, (s16a << 12) | oa), (s16b << 12) | ob);
+            b32 = min_u32(min_u32((uint32_t)b32, (s32a << 12) | oa), (s32b << 12) | ob);
+            b64 = min_u32((uint32_t)b64, (s64 << 12) | o64);
+        } else {
+            const int xa = x0 + g, xb = xa + 4, x64 = xa + 4 * (int)qb;
+            if (xa >= 0 && xa < w) {
+                b16 = min_u32((uint32_t)b16, (s16a << 12) | oa);
+                b32 = min_u32((uint32_t)b32, (s32a << 12) | oa);
+            }
+            if (xb >= 0 && xb < w) {
+                b16 = min_u32((uint32_t)b16, (s16b << 12) | ob);
+                b32 = min_u32((uint32_t)b32, (s32b << 12) | ob);
+            }
+            if (x64 >= 0 && x64 < w)
+                b64 = min_u32((uint32_t)b64, (s64 << 12) | o64);
         }
     }
-    // K32 after add_quad: min of b16 / b32 / b64 over the 4 lanes of each group
+    // the quad of every lane's 64x64 sums in add_quads (the rows permlane16_swap
+    // takes from its second operand)
+    __device__ __forceinline__ static uint32_t quad_b_rows() {
+        return __builtin_amdgcn_permlane16_swap(0u, 1u, false, false)[0];
+    }
+    // K32 after add_quads: b16 / b32 over the 4 lanes of each group, b64 over
+    // the wave (idempotent: the search may go on afterwards)
     __device__ __forceinline__ void finalize() {
         if (K32) {
             b16 = quad_min((uint32_t)b16);
             b32 = quad_min((uint32_t)b32);
-            b64 = quad_min((uint32_t)b64);
+            uint32_t v     = quad_min((uint32_t)b64);
+            const auto p16 = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+            v              = min_u32(p16[0], p16[1]);
+            const auto p32 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            b64            = min_u32(p32[0], p32[1]);
         }
+    }
+    // (sad << 32 | order) of a minimum, ~0 if none: K32 keys converted, SUB
+    // SADs doubled (8x4 sums of every other row)
+    template <bool SUB>
+    __device__ __forceinline__ static unsigned long long out(key_t k, bool is8) {
+        if (K32) {
+            const uint32_t v = (uint32_t)k;
+            if (v == 0xFFFFFFFFu)
+                return ~0ull;
+            const uint32_t sad = (is8 ? v >> 16 : v >> 12) << (SUB ? 1 : 0);
+            return ((unsigned long long)sad << 32) | (is8 ? (v & 0xFFFFu) : (v & 0xFFFu));
+        }
+        return (unsigned long long)k;
     }
     __device__ __forceinline__ static uint32_t quad_min(uint32_t v) {
         v = min_u32(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false));
@@ -2159,15 +2225,8 @@ __device__ __forceinline__ void fp_rows(PuMin<K32> &M, const uint32_t *a, int sd
                         acc = qsad(T[iy + rr * RSTEP][iq + 1], T[iy + rr * RSTEP][iq + 2], src[rr][1], acc);
                     }
                     const int y = ty + iy;
-                    if (K32) {
-                        const int x0   = 4 * (tq + iq) - sh;
-                        uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32);
-                        if (SUB) { // raw 8x4 SADs <= 8160: doubling stays inside each u16
-                            lo <<= 1;
-                            hi <<= 1;
-                        }
-                        M.add_quad(lo, hi, obase + (uint32_t)(y * w + x0), x0, w);
-                    } else {
+                    static_assert(!K32, "K32 keys: fp_rows32");
+                    {
                         uint32_t s4[4] = {0, 0, 0, 0};
                         qsad_unpack(acc, s4);
 #pragma unroll
@@ -2185,58 +2244,66 @@ __device__ __forceinline__ void fp_rows(PuMin<K32> &M, const uint32_t *a, int sd
 
 #define FP_TQ 3 // position quads per full-pel tile (sub-sampled rows; 2 for full rows)
 
-// K32 form of fp_rows: position quads in pairs, one dword-aligned 16-byte
-// global load per plane row and lane (uniform row base in SGPRs + the lane's
-// dword offset), every bound wave-uniform. Reads up to one dword right of the
-// window (plane margins / allocation slack).
+// K32 form of fp_rows: position quads in pairs from position 0 of the window
+// g (any byte alignment: unaligned 16-byte buffer loads), one load per plane
+// row and lane (uniform row offset + the lane's offset), every bound
+// wave-uniform. Reads up to 3 bytes right of the window (plane margins /
+// allocation slack).
 template <bool SUB, int TQ = 2> // TQ: position quads per load set (2: one 16-byte load per row, 6: two)
-__device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint32_t *a, int sdw, int sh, int w, int nq, int y0,
-                                          int y1, uint32_t obase, const uint32_t (&src)[SUB ? 4 : 8][2], int by,
-                                          int bx) {
+__device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint8_t *g, int sdw, int w, int y0, int y1,
+                                          uint32_t obase, const uint32_t (&src)[SUB ? 4 : 8][2], int by, int bx) {
     constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1, NL = (TQ + 2 + 3) / 4;
-    a     = uni_ptr(a);
+    g     = uni_ptr(g);
     sdw   = UNI(sdw);
-    sh    = UNI(sh);
     w     = UNI(w);
-    nq    = UNI(nq);
+    const int nq = (w + 3) >> 2; // the quads start at position 0: loads at any byte alignment
     y0    = UNI(y0);
     y1    = UNI(y1);
     obase = (uint32_t)UNI(obase);
+    static_assert(TQ % 2 == 0, "position quads go in pairs");
+    const uint32_t qb = PuMin<true>::quad_b_rows();
     const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2);
-    for (int ty = y0; ty < y1; ty++) {
-        for (int tq = 0; tq < nq; tq += TQ) {
-            const uint32_t *rb = a + (ptrdiff_t)ty * sdw + tq;
-            uint32_t D[ROWS][4 * NL];
+    // one load set: rows of quads [tq, tq + TQ) of search row ty
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(g);
+    auto set = [&](int ty, int tq, auto inner) {
+        const uint32_t rb = (uint32_t)(ty * sdw + tq) * 4u;
+        uint32_t D[ROWS][4 * NL];
 #pragma unroll
-            for (int rr = 0; rr < ROWS; rr++)
+        for (int rr = 0; rr < ROWS; rr++)
 #pragma unroll
-                for (int v = 0; v < NL; v++) {
-                    const u32x4a4 t = ldg4(rb + (ptrdiff_t)(rr * RSTEP) * sdw + lo + 4 * v);
-                    D[rr][4 * v] = t.x, D[rr][4 * v + 1] = t.y, D[rr][4 * v + 2] = t.z, D[rr][4 * v + 3] = t.w;
-                }
-            unsigned long long acc[TQ];
+            for (int v = 0; v < NL; v++) {
+                const u32x4a4 t = bld4(rs, (lo + 4 * v) * 4u, rb + (uint32_t)(rr * RSTEP * sdw) * 4u);
+                D[rr][4 * v] = t.x, D[rr][4 * v + 1] = t.y, D[rr][4 * v + 2] = t.z, D[rr][4 * v + 3] = t.w;
+            }
+        unsigned long long acc[TQ];
 #pragma unroll
-            for (int iq = 0; iq < TQ; iq++) acc[iq] = 0;
+        for (int iq = 0; iq < TQ; iq++) acc[iq] = 0;
 #pragma unroll
-            for (int rr = 0; rr < ROWS; rr++)
-#pragma unroll
-                for (int iq = 0; iq < TQ; iq++) {
-                    acc[iq] = qsad64(pair(D[rr][iq], D[rr][iq + 1]), src[rr][0], acc[iq]);
-                    acc[iq] = qsad64(pair(D[rr][iq + 1], D[rr][iq + 2]), src[rr][1], acc[iq]);
-                }
-            const int x0    = 4 * tq - sh;
-            const uint32_t ob = obase + (uint32_t)(ty * w + x0);
+        for (int rr = 0; rr < ROWS; rr++)
 #pragma unroll
             for (int iq = 0; iq < TQ; iq++) {
-                if (iq > 0 && tq + iq >= nq)
-                    break; // wave-uniform
-                uint32_t l0 = (uint32_t)acc[iq], h0 = (uint32_t)(acc[iq] >> 32);
-                if (SUB) { // raw 8x4 SADs <= 8160: doubling stays inside each u16
-                    l0 <<= 1, h0 <<= 1;
-                }
-                M.add_quad(l0, h0, ob + 4 * iq, x0 + 4 * iq, w);
+                acc[iq] = qsad64(pair(D[rr][iq], D[rr][iq + 1]), src[rr][0], acc[iq]);
+                acc[iq] = qsad64(pair(D[rr][iq + 1], D[rr][iq + 2]), src[rr][1], acc[iq]);
             }
+        const int x0      = 4 * tq;
+        const uint32_t ob = obase + (uint32_t)(ty * w + x0);
+#pragma unroll
+        for (int iq = 0; iq < TQ; iq += 2) {
+            if (!decltype(inner)::value && iq > 0 && tq + iq >= nq)
+                break; // wave-uniform (a second quad past nq lies right of the area)
+            M.template add_quads<decltype(inner)::value>((uint32_t)acc[iq], (uint32_t)(acc[iq] >> 32),
+                                                         (uint32_t)acc[iq + 1], (uint32_t)(acc[iq + 1] >> 32),
+                                                         ob + 4 * iq, x0 + 4 * iq, w, qb);
         }
+    };
+    // load sets wholly inside the area: tq < t_out (wave-uniform; every set when
+    // w is a multiple of 4 TQ, as the 8-aligned full-pel widths are for TQ = 2)
+    const int t_out = w >= 4 * TQ ? (w - 4 * TQ) / (4 * TQ) * TQ + TQ : 0;
+    for (int ty = y0; ty < y1; ty++) {
+        for (int tq = 0; tq < t_out; tq += TQ)
+            set(ty, tq, std::true_type());
+        for (int tq = t_out; tq < nq; tq += TQ)
+            set(ty, tq, std::false_type()); // the right edge
     }
 }
 
@@ -2317,12 +2384,12 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
         const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc);
         const int sh     = (int)((uintptr_t)g & 3);
         if constexpr (K32)
-            fp_rows32<SUB>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
+            fp_rows32<SUB>(M, g, P.stride >> 2, 1, 0, 1, 0u, src, by, bx);
         else
             fp_rows<SUB, K32, 1>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
         M.finalize();
-        const uint32_t p8   = (uint32_t)(PuMin<K32>::wide(M.b8) >> 32);
-        const uint32_t p64  = rl32((uint32_t)(PuMin<K32>::wide(M.b64) >> 32), 63);
+        const uint32_t p8   = (uint32_t)(PuMin<K32>::template out<SUB>(M.b8, true) >> 32);
+        const uint32_t p64  = rl32((uint32_t)(PuMin<K32>::template out<SUB>(M.b64, false) >> 32), 63);
         const uint32_t mean = p64 / 64;
         const int32_t diff  = (int32_t)p8 - (int32_t)mean;
         const uint32_t var  = wave_sum_u32((uint32_t)(diff * diff)) / 64;
@@ -2361,13 +2428,14 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     const int y0 = (int)(((uint32_t)h * part) / parts), y1 = (int)(((uint32_t)h * (part + 1)) / parts);
     const uint32_t obase = probe ? 1u : 0u; // the centre probe wins ties: order 0
     if constexpr (K32)
-        fp_rows32<SUB, WIDE ? 6 : 2>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by,
-                                     bx);
+        fp_rows32<SUB, WIDE ? 6 : 2>(M, g, P.stride >> 2, w, y0, y1, obase, src, by, bx);
     else
         fp_rows<SUB, K32, TQ>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
     M.finalize();
-    const unsigned long long k8 = PuMin<K32>::wide(M.b8), k16 = PuMin<K32>::wide(M.b16);
-    const unsigned long long k32 = PuMin<K32>::wide(M.b32), k64 = PuMin<K32>::wide(M.b64);
+    const unsigned long long k8  = PuMin<K32>::template out<SUB>(M.b8, true);
+    const unsigned long long k16 = PuMin<K32>::template out<SUB>(M.b16, false);
+    const unsigned long long k32 = PuMin<K32>::template out<SUB>(M.b32, false);
+    const unsigned long long k64 = PuMin<K32>::template out<SUB>(M.b64, false);
     if (parts == 1) {
         kp[21 + lane] = k8;
         if ((lane & 3) == 0)
@@ -2991,7 +3059,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks) {
     if (nblocks > (1u << 17))
         nblocks = 1u << 17;
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 8 * sizeof(unsigned long long));
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 16 * sizeof(unsigned long long));
 }
 #endif
 
