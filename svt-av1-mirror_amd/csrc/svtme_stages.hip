@@ -1203,7 +1203,7 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
     };
     u32x4a4 L[2][3];
     ld(0, L[0]);
-    unsigned long long acc[HQ] = {0, 0, 0};
+    unsigned long long acc[HQ] = {};
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) {
         if (kk + 1 < 4)
@@ -1247,7 +1247,7 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
 __device__ __forceinline__ unsigned long long hme_tile64(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                          int y, int kh2, const uint8_t (*src)[64]) {
     const int g = threadIdx.x & 15;
-    unsigned long long acc[HQ] = {0, 0, 0};
+    unsigned long long acc[HQ] = {};
 #pragma unroll
     for (int kk = 0; kk < 2; kk++) {
         const int k = 2 * g + kk;
@@ -2245,18 +2245,18 @@ __device__ __forceinline__ void fp_rows(PuMin<K32> &M, const uint32_t *a, int sd
 #define FP_TQ 3 // position quads per full-pel tile (sub-sampled rows; 2 for full rows)
 
 // K32 form of fp_rows: position quads in pairs from position 0 of the window
-// g (any byte alignment: unaligned 16-byte buffer loads), one load per plane
-// row and lane (uniform row offset + the lane's offset), every bound
-// wave-uniform. Reads up to 3 bytes right of the window (plane margins /
+// g at any byte alignment: dword-aligned buffer loads (uniform row offset +
+// the lane's offset, no VALU address work) realigned with v_alignbyte, every
+// bound wave-uniform. Reads up to 4 bytes right of the window (plane margins /
 // allocation slack).
 template <bool SUB, int TQ = 2> // TQ: position quads per load set (2: one 16-byte load per row, 6: two)
 __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint8_t *g, int sdw, int w, int y0, int y1,
                                           uint32_t obase, const uint32_t (&src)[SUB ? 4 : 8][2], int by, int bx) {
-    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1, NL = (TQ + 2 + 3) / 4;
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1;
     g     = uni_ptr(g);
     sdw   = UNI(sdw);
     w     = UNI(w);
-    const int nq = (w + 3) >> 2; // the quads start at position 0: loads at any byte alignment
+    const int nq = (w + 3) >> 2; // the quads start at position 0
     y0    = UNI(y0);
     y1    = UNI(y1);
     obase = (uint32_t)UNI(obase);
@@ -2264,17 +2264,27 @@ __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint8_t *g, int 
     const uint32_t qb = PuMin<true>::quad_b_rows();
     const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2);
     // one load set: rows of quads [tq, tq + TQ) of search row ty
-    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(g);
+    const int sh = (int)((uintptr_t)g & 3); // the loads stay dword aligned
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(g - sh);
     auto set = [&](int ty, int tq, auto inner) {
         const uint32_t rb = (uint32_t)(ty * sdw + tq) * 4u;
-        uint32_t D[ROWS][4 * NL];
+        // dword-aligned loads of TQ + 3 dwords, realigned to position 0 (v_alignbyte)
+        constexpr int NX = (TQ + 3) / 4, NR = (TQ + 3) - 4 * NX;
+        uint32_t D[ROWS][TQ + 3];
 #pragma unroll
-        for (int rr = 0; rr < ROWS; rr++)
+        for (int rr = 0; rr < ROWS; rr++) {
+            const uint32_t ro = rb + (uint32_t)(rr * RSTEP * sdw) * 4u;
 #pragma unroll
-            for (int v = 0; v < NL; v++) {
-                const u32x4a4 t = bld4(rs, (lo + 4 * v) * 4u, rb + (uint32_t)(rr * RSTEP * sdw) * 4u);
+            for (int v = 0; v < NX; v++) {
+                const u32x4a4 t = bld4(rs, (lo + 4 * v) * 4u, ro);
                 D[rr][4 * v] = t.x, D[rr][4 * v + 1] = t.y, D[rr][4 * v + 2] = t.z, D[rr][4 * v + 3] = t.w;
             }
+#pragma unroll
+            for (int v = 0; v < NR; v++)
+                D[rr][4 * NX + v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)((lo + 4 * NX + v) * 4u), (int)ro, 0);
+#pragma unroll
+            for (int j = 0; j < TQ + 2; j++) D[rr][j] = __builtin_amdgcn_alignbyte(D[rr][j + 1], D[rr][j], (uint32_t)sh);
+        }
         unsigned long long acc[TQ];
 #pragma unroll
         for (int iq = 0; iq < TQ; iq++) acc[iq] = 0;
