@@ -1060,7 +1060,8 @@ __device__ unsigned long long g_hme_stamps[1 << 17][16];
 #define HME_STAMP(k)
 #endif
 
-#define HQ 3  // position quads per HME-L1 tile (8-wide areas at any alignment: 2 or 3 quads)
+#define HQ 3  // position quads per HME-L2 tile (8-wide areas at any alignment: 2 or 3 quads)
+#define HQ1 2 // position quads per HME-L1 tile (rows realigned to position 0: 8-wide areas = 2 quads)
 #define HQ16 2 // position quads per 1/16 tile (interior windows are dword aligned: 8/16/32 wide = 2/4/8 quads)
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -1189,10 +1190,11 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
 }
 
 // One quarter of the SADs of the 32 x kh1 (sub) quarter-resolution source
-// block (LDS, rows 32 bytes apart) at HQ quads of position row y of a 1/4
-// window: block rows [4g, 4g + 4) of lane g = lane & 3, all loads issued up
-// front; the 4 lanes of a quad then sum their partial SADs (DPP) and every
-// lane returns the row's minimum key.
+// block (LDS, rows 32 bytes apart) at HQ1 quads of position row y of a 1/4
+// window (a0 dword aligned, position 0 at byte sh: the rows are realigned with
+// v_alignbyte): block rows [4g, 4g + 4) of lane g = lane & 3, all loads
+// issued up front; the 4 lanes of a quad then sum their partial SADs (DPP)
+// and every lane returns the row's minimum key.
 __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                           int y, int kh1, const uint8_t (*src)[32]) {
     const int g = threadIdx.x & 3;
@@ -1203,7 +1205,7 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
     };
     u32x4a4 L[2][3];
     ld(0, L[0]);
-    unsigned long long acc[HQ] = {};
+    unsigned long long acc[HQ1] = {};
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) {
         if (kk + 1 < 4)
@@ -1213,24 +1215,26 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
             const u32x4a4 *R = L[kk & 1];
             const uint4 s0 = ((const uint4 *)src[k])[0], s1 = ((const uint4 *)src[k])[1];
             const uint32_t sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-            const uint32_t d[12] = {R[0].x, R[0].y, R[0].z, R[0].w, R[1].x, R[1].y,
-                                    R[1].z, R[1].w, R[2].x, R[2].y, R[2].z, R[2].w};
+            uint32_t d[12] = {R[0].x, R[0].y, R[0].z, R[0].w, R[1].x, R[1].y,
+                              R[1].z, R[1].w, R[2].x, R[2].y, R[2].z, R[2].w};
 #pragma unroll
-            for (int qq = 0; qq < HQ; qq++)
+            for (int j = 0; j < HQ1 + 8; j++) d[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], (uint32_t)sh);
+#pragma unroll
+            for (int qq = 0; qq < HQ1; qq++)
 #pragma unroll
                 for (int j = 0; j < 8; j++) acc[qq] = qsad64(pair(d[qq + j], d[qq + j + 1]), sv[j], acc[qq]);
         }
     }
     uint32_t mt = U32MAX; // sad (< 2^17) << 15 | x (< 2^15)
 #pragma unroll
-    for (int qq = 0; qq < HQ; qq++) {
+    for (int qq = 0; qq < HQ1; qq++) {
         uint32_t a[4] = {0, 0, 0, 0};
         qsad_unpack(acc[qq], a);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             const uint32_t v = dpp_add<0x4E>(dpp_add<0xB1>(a[e])); // the quad's 4 row groups
-            const int x      = 4 * (q0 + qq) - sh + e;
-            if (x >= 0 && x < sa_w)
+            const int x      = 4 * (q0 + qq) + e;
+            if (x < sa_w)
                 mt = min_u32(mt, (v << 15) | (uint32_t)x);
         }
     }
@@ -2890,7 +2894,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
                         e.sh              = (uint8_t)((uintptr_t)w0 & 3);
                         e.a0              = w0 - e.sh;
                         e.sa_w            = sw;
-                        e.ncols           = (int16_t)((((e.sh + sw + 3) >> 2) + HQ - 1) / HQ);
+                        e.ncols           = (int16_t)((((sw + 3) >> 2) + HQ1 - 1) / HQ1); // realigned rows
                         e.id              = (uint8_t)lane;
                         items             = e.ncols * shh;
                         mk                = true;
@@ -2924,7 +2928,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             const HSrch1 &e = sh.u.a.s1[find_search(sh.u.a.s1, nsrch, it)];
             const int local = it - e.item0;
             const int y = local / e.ncols, col = local - y * e.ncols;
-            const unsigned long long kk = hme_tile32q(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh1, sh.u.a.src4);
+            const unsigned long long kk = hme_tile32q(e.a0, pstride, HQ1 * col, e.sh, e.sa_w, y, kh1, sh.u.a.src4);
             if ((it4 & 3) == 0 && kk != ~0ull)
                 atomicMin(&sh.u.a.key1[e.id], kk);
         }
