@@ -7,15 +7,17 @@ svt_aom_sig_deriv_me. Pyramids of the pictures and their references are
 resident in HBM before the timed region (the PA stage builds them once per
 picture). --workload picks another BASELINE config (svt-av1-mirror_amd/workloads.py).
 
-One step, on N GPUs (one process per GPU, torch.distributed over RCCL): N
-pictures, each split into N equal SB chunks (SBs are
-independent given the picture controls); rank r searches chunk r of every
-picture in ONE batched launch per stage (svtme_submit_batch_device), then the
-ranks all-gather their record chunks over RCCL (one all_gather_into_tensor per
-step, device buffers, on a communication stream overlapped with the next
-step's ME). Per-GPU work is one picture's worth of SBs at every N: "scaling"
-is weak; at N = 1 the step is exactly one picture job. value = SBs of all N
-pictures / max-over-ranks time.
+One step, on N GPUs (one process per GPU, torch.distributed over RCCL): 4 N
+pictures (the encoder's look-ahead keeps several pictures' ME in flight; the
+C host batches whole pictures, BASELINE.json north_star), each split into N
+equal SB chunks (SBs are independent given the picture
+controls); rank r searches chunk r of every picture in ONE batched launch
+(svtme_submit_batch_device), then the ranks all-gather their record chunks
+over RCCL (one all_gather_into_tensor per step, device buffers, on a
+communication stream overlapped with the next step's ME). Per-GPU work is four
+pictures' worth of SBs at every N: "scaling" is weak. value = SBs of all
+pictures / max-over-ranks time. "single_picture" reports the latency mode
+(one picture per GPU per launch) on the same jobs.
 
 roofline: the ME pass (the five stage kernels, back to back on the library's
 stream) — algorithmic bytes per pass (bytes/SB x SBs per
@@ -59,6 +61,8 @@ STAGE_BYTES_P8 = {"k_stage_a": (2176, 6808), "k_stage_d": (0, 0), "k_stage_b": (
 # the whole pass in k_hme (fused full-pel + decode): every byte of the pass
 STAGE_BYTES_P8_ALL = (2688, 16798 + 680)
 PICTURE_STRIDE = 32  # picture p of a step pans from t = 8 + 32 p (distinct content per picture)
+PICTURES_PER_GPU = 4  # pictures of one step per GPU (one batched launch); --pictures overrides
+MAX_BATCH = 16  # SVTME_MAX_BATCH_JOBS (include/svtme.h): jobs of one batched launch
 
 
 def host_cores():
@@ -105,7 +109,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="4k_p8", choices=sorted(W.WORKLOADS))
-    ap.add_argument("--pictures", type=int, default=0, help="pictures per step (default: one per GPU)")
+    ap.add_argument("--pictures", type=int, default=0,
+                    help=f"pictures per step (default: {PICTURES_PER_GPU} per GPU, one batched launch)")
     ap.add_argument("--kernel-samples", type=int, default=20, help="steps timed per kernel after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="target CPU-seconds of the baseline sample")
@@ -130,7 +135,7 @@ def main():
     name = args.workload
     wl = W.WORKLOADS[name]
     Wd, Ht = wl["w"], wl["h"]
-    P = args.pictures or world
+    P = args.pictures or PICTURES_PER_GPU * world
     n_sb = S.sb_total(Wd, Ht)
     slots = D.chunk_slots(n_sb, world)
     begin, count = D.sb_chunk(n_sb, rank, world)
@@ -159,11 +164,13 @@ def main():
     g_done = [torch.cuda.Event() for _ in range(2)]
     used = [False, False]
 
-    def step(i):
+    def step(i, n_pic=P):
         b = i & 1
         if used[b] and world > 1:
             ext.wait_event(g_done[b])  # the gather of step i-2 has read local[b]
-        gpu.submit_batch_device(jobs, [local[b].data_ptr() + p * chunk_bytes for p in range(P)])
+        for g0 in range(0, n_pic, MAX_BATCH):  # SVTME_MAX_BATCH_JOBS jobs per launch
+            g1 = min(n_pic, g0 + MAX_BATCH)
+            gpu.submit_batch_device(jobs[g0:g1], [local[b].data_ptr() + p * chunk_bytes for p in range(g0, g1)])
         if world > 1:
             me_done[b].record(ext)
             comm.wait_event(me_done[b])
@@ -198,6 +205,18 @@ def main():
     fence()
     gpu.set_timing(False)
     n_timed, stage_ms = gpu.timing_read()
+    # latency mode: one picture per GPU per launch (the same jobs, P = world)
+    lat_ms = None
+    if P > world:
+        for i in range(args.warmup):
+            step(i, world)
+        fence()
+        ev0.record(ext)
+        for i in range(args.steps):
+            step(args.warmup + i, world)
+        ev1.record(ext)
+        fence()
+        lat_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -220,7 +239,7 @@ def main():
         e = {"avg_ms": round(stage_ms[k], 4), "share": round(stage_ms[k] / kern_ms, 3)}
         if wl["windows"] == "p8":
             src_b, per_ref = STAGE_BYTES_P8_ALL if (fused and stage_ms[3] <= 0) else STAGE_BYTES_P8[st]
-            sb_b = (src_b + R * per_ref) * sbs_launch
+            sb_b = (src_b + R * per_ref) * count * min(P, MAX_BATCH)  # one kernel launch
             if sb_b:
                 e["bytes_per_launch"] = sb_b
                 e["achieved_gbps"] = round(sb_b / (stage_ms[k] * 1e-3) / 1e9, 1)
@@ -261,6 +280,10 @@ def main():
                        "parallelism": f"{world} GPU(s): each picture split in {world} equal SB chunks, "
                                       f"rank r searches chunk r of all {P} pictures in one batched launch per "
                                       f"stage" + (", RCCL all-gather of the record chunks" if world > 1 else "")},
+            "single_picture": None if lat_ms is None else {
+                "pictures_per_step": world, "ms_per_step": round(lat_ms, 4),
+                "value": round(n_sb * world / (lat_ms * 1e-3), 1),
+                "note": "latency mode: one picture per GPU per launch (library-stream HIP events)"},
             "sb_ref_per_s": round(value * R, 1),
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -1059,6 +1059,12 @@ __device__ unsigned long long g_hme_stamps[1 << 17][16];
 #else
 #define HME_STAMP(k)
 #endif
+// extra stop points of the SVTME_STOP_AFTER builds (no stamp slot)
+#if defined(SVTME_STOP_AFTER) && !defined(SVTME_STAMPS)
+#define HME_STOP(k) HME_STAMP(k)
+#else
+#define HME_STOP(k)
+#endif
 
 #define HQ 3  // position quads per HME-L2 tile (8-wide areas at any alignment: 2 or 3 quads)
 #define HQ1 2 // position quads per HME-L1 tile (rows realigned to position 0: 8-wide areas = 2 quads)
@@ -2638,8 +2644,11 @@ struct HmeSh {
 
 // FP: the whole ME pass of the SB in this workgroup (k_stage_c1 with one band
 // per record, then k_stage_e); else the HME state goes to BState for them.
+#ifndef HME_WAVES_PER_EU
+#define HME_WAVES_PER_EU 8 // 64 VGPRs: 8 workgroups per CU
+#endif
 template <bool FP, bool SUB_ME, bool K32>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_hme(const DevBatch B) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WAVES_PER_EU, HME_WAVES_PER_EU))) k_hme(const DevBatch B) {
     __shared__ HmeSh sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = UNI(tid >> 6);
     uint32_t sb_local;
@@ -3042,6 +3051,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             sh.tf_exit = job.me_type == SVTME_ME_MCTF && scv.hme_sad < job.tf_me_exit_th; // :3109-3113
     }
     __syncthreads();
+    HME_STOP(55);
     for (int k = wid; k < (int)dj.R; k += 4) {
         constexpr int ROWS = SUB_ME ? 4 : 8, RSTEP = SUB_ME ? 2 : 1;
         const int z16 = lane >> 2, k4 = lane & 3;
