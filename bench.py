@@ -113,6 +113,7 @@ def main():
                     help=f"pictures per step (default: {PICTURES_PER_GPU} per GPU, one batched launch)")
     ap.add_argument("--kernel-samples", type=int, default=20, help="steps timed per kernel after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-single-picture", action="store_true", help="skip the one-picture latency-mode timing")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="target CPU-seconds of the baseline sample")
     args = ap.parse_args()
 
@@ -207,7 +208,7 @@ def main():
     n_timed, stage_ms = gpu.timing_read()
     # latency mode: one picture per GPU per launch (the same jobs, P = world)
     lat_ms = None
-    if P > world:
+    if P > world and not args.no_single_picture:
         for i in range(args.warmup):
             step(i, world)
         fence()
