@@ -1357,6 +1357,7 @@ struct StC {
     uint32_t me_distortion[SVTME_PU_COUNT];
     uint8_t cand0[SVTME_PU_COUNT + 3];
     uint32_t gm_cnt[2][4][2][2];
+    uint32_t wm[8]; // magic_u32 of each slot's full-pel width (key decode)
 };
 
 // Window of one reference: rows h, positions w, dword-aligned quads
@@ -1694,9 +1695,9 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
         const uint32_t d64 = st.me_distortion[0];
         const uint64_t mean = d8 / 64;
         const int64_t diff  = (int64_t)d8v - (int64_t)mean;
-        uint64_t sq         = (uint64_t)(diff * diff);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) sq += __shfl_xor(sq, off, 64);
+        const uint64_t sq1  = (uint64_t)(diff * diff); // < 2^42: 24-bit limbs sum exactly in 32 bits
+        const uint64_t sq   = ((uint64_t)wave_sum_u32((uint32_t)(sq1 >> 24)) << 24) +
+                            (uint64_t)wave_sum_u32((uint32_t)(sq1 & 0xFFFFFFu));
         if (lane == 0) {
             o->me_8x8_cost_variance = (uint32_t)(sq / 64);
             o->rc_me_distortion     = (job.input_resolution <= 2) ? d8 : d16;
@@ -1707,17 +1708,19 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             o->me_8x8_distortion    = (d8 * 4096u) / pix;
         }
     }
-    // perform_gm_detection (motion_estimation.c:2838-2961)
-    if (job.gm_enabled && tid == 0) {
-        uint64_t stationary = 0, tot = 0;
-        uint32_t(*cnt)[4][2][2] = st.gm_cnt;
-        for (int a2 = 0; a2 < 2; a2++)
-            for (int b2 = 0; b2 < 4; b2++)
-                for (int cc = 0; cc < 2; cc++) cnt[a2][b2][cc][0] = cnt[a2][b2][cc][1] = 0;
+    // perform_gm_detection (motion_estimation.c:2838-2961): wave 0, one lane per
+    // block; the direction counters are LDS adds, the stationary count a ballot
+    if (job.gm_enabled && tid < 64) {
+        const int lane = tid;
+        uint32_t *cntf = &st.gm_cnt[0][0][0][0];
+        if (lane < 32)
+            cntf[lane] = 0;
+        wave_lds_fence();
         const bool low  = job.input_resolution <= 2;
         const int n_blk = low ? 64 : 16;
-        for (int i = 0; i < n_blk; i++) {
-            uint8_t n = (uint8_t)(low ? 21 + i : 5 + i);
+        bool stat       = false;
+        if (lane < n_blk) {
+            uint8_t n = (uint8_t)(low ? 21 + lane : 5 + lane);
             if (low && !job.enable_me_8x8) {
                 if (n >= 21)
                     n = c_8x8_to_16x16[n - 21];
@@ -1741,27 +1744,28 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             }
             const uint32_t mv = st.best_mv[li * 4 + ri][n];
             const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4;
+            uint32_t(*cnt)[4][2][2] = st.gm_cnt;
             if (mx < -active_th)
-                cnt[li][ri][0][0]++;
+                atomicAdd(&cnt[li][ri][0][0], 1u);
             else if (mx > active_th)
-                cnt[li][ri][0][1]++;
+                atomicAdd(&cnt[li][ri][0][1], 1u);
             if (my < -active_th)
-                cnt[li][ri][1][0]++;
+                atomicAdd(&cnt[li][ri][1][0], 1u);
             else if (my > active_th)
-                cnt[li][ri][1][1]++;
+                atomicAdd(&cnt[li][ri][1][1], 1u);
             const int stt = low ? 0 : 4;
-            if (absi(mx) <= stt && absi(my) <= stt)
-                stationary++;
-            tot++;
+            stat          = absi(mx) <= stt && absi(my) <= stt;
         }
-        if (stationary > ((tot * 5) / 100))
-            o->stationary_block_present = 1;
-        for (int a2 = 0; a2 < 2; a2++)
-            for (int b2 = 0; b2 < 4; b2++)
-                for (int cc = 0; cc < 2; cc++)
-                    for (int s2 = 0; s2 < 2; s2++)
-                        if (cnt[a2][b2][cc][s2] > (tot / 2))
-                            o->rc_me_allow_gm = 1;
+        const uint64_t stationary = (uint64_t)__popcll(__ballot(stat)), tot = (uint64_t)n_blk;
+        wave_lds_fence();
+        const bool over = lane < 32 && cntf[lane] > (tot / 2);
+        const bool any  = __ballot(over) != 0ull;
+        if (lane == 0) {
+            if (stationary > ((tot * 5) / 100))
+                o->stationary_block_present = 1;
+            if (any)
+                o->rc_me_allow_gm = 1;
+        }
     }
 }
 
@@ -1776,17 +1780,21 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
     // ---- me_prune_ref (motion_estimation.c:1522-1565)
     if (job.me_type != SVTME_ME_MCTF && c.enable_hme_flag && c.enable_me_hme_ref_pruning && w0) {
         const int s = lane;
+        // the 64 8x8 best SADs of every searched slot, summed across the wave
+        // (searched == do_ref outside MCTF: each SAD < 2^15, the sum fits 32 bits)
+        uint32_t sum8 = 0;
+        for (int k = 0; k < 8; k++) {
+            if (!(slot_valid(vmask, k) && st.do_ref[k]))
+                continue; // wave-uniform
+            const uint32_t t = wave_sum_u32(st.best_sad[k][21 + lane]);
+            if (lane == k)
+                sum8 = t;
+        }
         uint64_t v  = ~0ull;
         if (s < 8) {
             v = st.hme_sad[s];
             if (slot_valid(vmask, s)) {
-                if (!st.do_ref[s])
-                    v = (uint64_t)SVTME_MAX_SAD_VALUE * 64;
-                else {
-                    uint64_t sum = 0;
-                    for (int i = 0; i < 64; i++) sum += st.best_sad[s][21 + i];
-                    v = sum;
-                }
+                v             = st.do_ref[s] ? (uint64_t)sum8 : (uint64_t)SVTME_MAX_SAD_VALUE * 64;
                 st.hme_sad[s] = v;
             }
         }
@@ -2558,6 +2566,7 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
         const int s     = tid < job.num_refs[0] ? tid : 4 + (tid - job.num_refs[0]);
         const CSlot v   = cin[tid];
         csl[s]          = v;
+        st.wm[s]        = v.searched ? magic_u32((uint32_t)max(1, (int)v.w)) : 0u;
         st.hme_sad[s]   = v.hme_sad;
         st.zz[s]        = v.zz;
         st.sc_x[s]      = v.sc_x;
@@ -2583,10 +2592,11 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
             if (v.probe && o == 0) {
                 mx = v.xc;
                 my = v.yc;
-            } else {
+            } else { // p / w by multiply-high (p * w < 2^32)
                 const int p = (int)o - (int)v.probe;
-                my          = i16(v.yo + p / v.w);
-                mx          = i16(v.xo + p % v.w);
+                const int q = mdiv(p, st.wm[s]);
+                my          = i16(v.yo + q);
+                mx          = i16(v.xo + (p - q * v.w));
             }
             mv = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
         }
