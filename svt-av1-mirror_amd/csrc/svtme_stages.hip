@@ -1107,12 +1107,14 @@ struct HSrch {             // one 1/16-resolution search (pre-HME region or HME-
     int16_t sa_w, ncols;   // positions per row; tile columns
     int16_t cnt0, cnt1;    // position rows of each tile-row parity (skip: cnt0 = rows, cnt1 = 0)
     int16_t ylast;         // last plane-row offset a tile of this search may read
+    uint32_t ncm;          // magic_u32(ncols): tile index / ncols by multiply-high
     uint8_t sh, skip, id;  // byte offset of position 0; odd rows only; ARes index
     uint8_t need;          // bit of HmeSh::need (slot * 2 + (L0 ? 1 : 0))
 };
 struct HSrch1 {            // one HME-L1 refinement search
     const uint8_t *a0;
     int32_t item0;
+    uint32_t ncm;          // magic_u32(ncols)
     int16_t sa_w, ncols;
     uint8_t sh, id;        // id = slot * 4 + quadrant
 };
@@ -1132,7 +1134,7 @@ __device__ __forceinline__ Row8 row8(const uint8_t *a0, int stride, int ro, int 
 // position rows yf + 2t (t < tv); plane rows are clamped to ylast. Rows are
 // loaded two ahead of their use. Returns the tile's minimum key
 // (sad << 32 | y << 16 | x), ~0 if no position is valid.
-template <int T>
+template <int T, bool FULLK = false> // FULLK: a full-height SB (kh == 8), no row checks
 __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                          int yf, int tv, int ylast, int kh,
                                                          const uint32_t (&sr)[8][4]) {
@@ -1159,7 +1161,7 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
             const int k = m - t;
             if (k < 0 || k >= 8)
                 continue;
-            if (k >= kh) // wave-uniform (partial-height SB)
+            if (!FULLK && k >= kh) // wave-uniform (partial-height SB)
                 continue;
 #pragma unroll
             for (int qq = 0; qq < HQ16; qq++)
@@ -1201,6 +1203,7 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
 // v_alignbyte): block rows [4g, 4g + 4) of lane g = lane & 3, all loads
 // issued up front; the 4 lanes of a quad then sum their partial SADs (DPP)
 // and every lane returns the row's minimum key.
+template <bool FULLK = false> // FULLK: a full-height SB (kh1 == 16), no row checks
 __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                           int y, int kh1, const uint8_t (*src)[32]) {
     const int g = threadIdx.x & 3;
@@ -1217,7 +1220,7 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
         if (kk + 1 < 4)
             ld(kk + 1, L[(kk + 1) & 1]);
         const int k = 4 * g + kk;
-        if (k < kh1) {
+        if (FULLK || k < kh1) {
             const u32x4a4 *R = L[kk & 1];
             const uint4 s0 = ((const uint4 *)src[k])[0], s1 = ((const uint4 *)src[k])[1];
             const uint32_t sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
@@ -2728,6 +2731,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                 e.skip            = skip;
                 const int nq      = (e.sh + sw + 3) >> 2;
                 e.ncols           = (int16_t)((nq + HQ16 - 1) / HQ16);
+                e.ncm             = magic_u32((uint32_t)e.ncols);
                 if (skip) {
                     e.cnt0  = (int16_t)nrows;
                     e.cnt1  = 0;
@@ -2833,28 +2837,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         const int nitems = sh.u.a.nitems, nsrch = sh.u.a.nsrch;
         const uint32_t need = sh.u.a.need;
         const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
-        for (int it = tid; it < nitems; it += 256) {
-            const HSrch &e = sh.u.a.srch[find_search(sh.u.a.srch, nsrch, it)];
-            if (!((need >> e.need) & 1u))
-                continue;
-            const int local = it - e.item0;
-            const int rt = local / e.ncols, col = local - rt * e.ncols;
-            int yf, tv;
-            if (e.skip) {
-                yf = 2 * HT16 * rt + 1;
-                tv = min(HT16, e.cnt0 - HT16 * rt);
-            } else {
-                const int p = rt & 1, i = rt >> 1;
-                yf = 2 * HT16 * i + p;
-                tv = min(HT16, (p ? e.cnt1 : e.cnt0) - HT16 * i);
+        auto tiles = [&](auto fullk) {
+            for (int it = tid; it < nitems; it += 256) {
+                const HSrch &e = sh.u.a.srch[find_search(sh.u.a.srch, nsrch, it)];
+                if (!((need >> e.need) & 1u))
+                    continue;
+                const int local = it - e.item0;
+                const int rt = mdiv(local, e.ncm), col = local - rt * e.ncols;
+                int yf, tv;
+                if (e.skip) {
+                    yf = 2 * HT16 * rt + 1;
+                    tv = min(HT16, e.cnt0 - HT16 * rt);
+                } else {
+                    const int p = rt & 1, i = rt >> 1;
+                    yf = 2 * HT16 * i + p;
+                    tv = min(HT16, (p ? e.cnt1 : e.cnt0) - HT16 * i);
+                }
+                if (tv <= 0)
+                    continue;
+                const unsigned long long kk = hme_tile16<HT16, decltype(fullk)::value>(
+                    e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
+                if (kk != ~0ull)
+                    atomicMin(&sh.u.a.key[e.id], kk);
             }
-            if (tv <= 0)
-                continue;
-            const unsigned long long kk =
-                hme_tile16<HT16>(e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
-            if (kk != ~0ull)
-                atomicMin(&sh.u.a.key[e.id], kk);
-        }
+        };
+        tiles(std::false_type()); // (a kh == 8 specialisation spills: the scheduler hoists every row)
     }
     __syncthreads();
     HME_STAMP(3);
@@ -2914,6 +2921,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                         e.a0              = w0 - e.sh;
                         e.sa_w            = sw;
                         e.ncols           = (int16_t)((((sw + 3) >> 2) + HQ1 - 1) / HQ1); // realigned rows
+                        e.ncm             = magic_u32((uint32_t)e.ncols);
                         e.id              = (uint8_t)lane;
                         items             = e.ncols * shh;
                         mk                = true;
@@ -2942,15 +2950,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     {
         const int nlanes = 4 * sh.u.a.nitems1, nsrch = sh.u.a.nsrch1;
         const int pstride = dj.cur.lv[1].stride;
-        for (int it4 = tid; it4 < nlanes; it4 += 256) {
-            const int it    = it4 >> 2;
-            const HSrch1 &e = sh.u.a.s1[find_search(sh.u.a.s1, nsrch, it)];
-            const int local = it - e.item0;
-            const int y = local / e.ncols, col = local - y * e.ncols;
-            const unsigned long long kk = hme_tile32q(e.a0, pstride, HQ1 * col, e.sh, e.sa_w, y, kh1, sh.u.a.src4);
-            if ((it4 & 3) == 0 && kk != ~0ull)
-                atomicMin(&sh.u.a.key1[e.id], kk);
-        }
+        auto tiles = [&](auto fullk) {
+            for (int it4 = tid; it4 < nlanes; it4 += 256) {
+                const int it    = it4 >> 2;
+                const HSrch1 &e = sh.u.a.s1[find_search(sh.u.a.s1, nsrch, it)];
+                const int local = it - e.item0;
+                const int y = mdiv(local, e.ncm), col = local - y * e.ncols;
+                const unsigned long long kk = hme_tile32q<decltype(fullk)::value>(e.a0, pstride, HQ1 * col, e.sh,
+                                                                                  e.sa_w, y, kh1, sh.u.a.src4);
+                if ((it4 & 3) == 0 && kk != ~0ull)
+                    atomicMin(&sh.u.a.key1[e.id], kk);
+            }
+        };
+        tiles(std::false_type()); // (a kh1 == 16 specialisation measured slower)
     }
     __syncthreads();
     // resolve the searched level-1 refinements (full-pel units: x 2)
@@ -2987,6 +2999,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                         e.a0              = w0 - e.sh;
                         e.sa_w            = sw;
                         e.ncols           = (int16_t)((((e.sh + sw + 3) >> 2) + HQ - 1) / HQ);
+                        e.ncm             = magic_u32((uint32_t)e.ncols);
                         e.id              = (uint8_t)lane;
                         items             = e.ncols * shh;
                         mk                = true;
@@ -3014,7 +3027,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                 const int it    = it16 >> 4;
                 const HSrch1 &e = sh.u.a.s1[find_search(sh.u.a.s1, nsrch, it)];
                 const int local = it - e.item0;
-                const int y = local / e.ncols, col = local - y * e.ncols;
+                const int y = mdiv(local, e.ncm), col = local - y * e.ncols;
                 const unsigned long long kk = hme_tile64(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh2, sh.u.a.src1);
                 if ((it16 & 15) == 0 && kk != ~0ull)
                     atomicMin(&sh.u.a.key1[e.id], kk);
