@@ -114,6 +114,7 @@ def main():
     ap.add_argument("--kernel-samples", type=int, default=20, help="steps timed per kernel after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-single-picture", action="store_true", help="skip the one-picture latency-mode timing")
+    ap.add_argument("--no-upload", action="store_true", help="skip the host-upload (PCIe-inclusive) timing")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="target CPU-seconds of the baseline sample")
     args = ap.parse_args()
 
@@ -225,6 +226,31 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = n_sb * P * args.steps / elapsed
 
+    # PCIe-inclusive rate (never `value`): one picture's upload from
+    # host memory (pageable numpy, and a pinned buffer) + pyramid build, synchronous
+    upload = None
+    if rank == 0 and not args.no_upload:
+        frame = syn.frame10(8) if wl["ten_bit"] else syn.frame(8)
+        fn = gpu.lib.svtme_picture_upload_10bit if wl["ten_bit"] else gpu.lib.svtme_picture_upload
+
+        def t_up(ptr, reps=10):
+            t = []
+            for k in range(reps + 2):
+                t0u = time.perf_counter()
+                gpu._check(fn(gpu.ctx, 900000 + k, ptr, Wd, Wd, Ht), "upload")
+                t.append(time.perf_counter() - t0u)
+                gpu.release(900000 + k)
+            return float(np.median(t[2:])) * 1e3
+        pageable_ms = t_up(np.ascontiguousarray(frame).ctypes.data)
+        pinned = torch.from_numpy(np.ascontiguousarray(frame)).pin_memory()
+        pinned_ms = t_up(pinned.data_ptr())
+        me_ms = ms_per_step / P * world
+        upload = {"pageable_ms_per_picture": round(pageable_ms, 4), "pinned_ms_per_picture": round(pinned_ms, 4),
+                  "picture_bytes": int(frame.nbytes),
+                  "pcie_inclusive_sb_per_s": round(n_sb / ((pinned_ms + me_ms) * 1e-3), 1),
+                  "note": "upload + pyramid build of one picture, synchronous, from host memory; every picture "
+                          "is uploaded once and then serves as current and reference picture"}
+
     # roofline of the ME pass on this rank (one batched launch per stage)
     sbs_launch = count * P
     bps = W.bytes_per_sb(wl["windows"], R)
@@ -285,6 +311,7 @@ def main():
                 "pictures_per_step": world, "ms_per_step": round(lat_ms, 4),
                 "value": round(n_sb * world / (lat_ms * 1e-3), 1),
                 "note": "latency mode: one picture per GPU per launch (library-stream HIP events)"},
+            "upload": upload,
             "sb_ref_per_s": round(value * R, 1),
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
