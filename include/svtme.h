@@ -234,6 +234,16 @@ svtme_status svtme_picture_upload(svtme_ctx *ctx, uint64_t picture_number, const
  * searched plane is the 8-bit MSB plane p >> 2 (enc_handle.c:4964-4972). */
 svtme_status svtme_picture_upload_10bit(svtme_ctx *ctx, uint64_t picture_number, const uint16_t *y,
                                         uint32_t stride, uint32_t width, uint32_t height);
+/* Asynchronous form of svtme_picture_upload: the rows are copied by DMA into
+ * the resident plane and the pyramid is built on the context's upload stream,
+ * overlapping with jobs already running; the call returns once the copy is
+ * queued (pageable memory: once the driver has staged it). The first job that
+ * reads the picture waits for the upload on the GPU. With pinned host memory
+ * the caller keeps `y` unchanged until svtme_sync() or a job reading the
+ * picture has completed. Jobs queued earlier that read an older version of the
+ * picture finish before it is overwritten. */
+svtme_status svtme_picture_upload_async(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *y, uint32_t stride,
+                                        uint32_t width, uint32_t height);
 /* Same, from a DEVICE pointer already in HBM (no PCIe). */
 svtme_status svtme_picture_upload_device(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *d_y,
                                          uint32_t stride, uint32_t width, uint32_t height);

@@ -26,6 +26,7 @@
 
 extern "C" hipError_t svtme_launch_build_full(const void *src, uint32_t src_stride, int w, int h, int ten_bit,
                                               DevPlane dst, int left, int top, int rows, hipStream_t s);
+extern "C" hipError_t svtme_launch_copy_words(const void *src, void *dst, uint32_t nwords, hipStream_t s);
 extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int left, int top, int rows,
                                               hipStream_t s);
 extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
@@ -76,11 +77,17 @@ struct PicBuf {
     size_t bytes = 0;
     uint32_t W = 0, H = 0;
     DevPyramid pyr{};
+    hipEvent_t ready = nullptr; // end of an asynchronous upload on the upload stream
+    bool pending     = false;   // the job stream has not waited on `ready` yet
+    hipEvent_t used  = nullptr; // after the last launch that reads the picture (job stream)
 };
 
 struct svtme_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t ustream = nullptr; // asynchronous uploads (copy + pyramid build), created on first use
+    void *ustaging = nullptr;      // their device staging plane (reused in upload-stream order)
+    size_t ustaging_cap = 0;
     std::map<uint64_t, PicBuf> pics;
     void *staging      = nullptr;
     size_t staging_cap = 0;
@@ -95,7 +102,7 @@ struct svtme_ctx {
     // after every kernel queued before has read it); a table identical to the
     // last one published is reused without a copy
     static constexpr int kRing = 16;
-    DevJob *d_table = nullptr, *h_table = nullptr;
+    DevJob *d_table = nullptr, *h_table = nullptr, *h_table_dev = nullptr;
     hipEvent_t ring_copied[kRing] = {}; // the copy out of the pinned slot has run
     bool ring_used[kRing] = {};
     uint32_t ring_n[kRing] = {};
@@ -151,9 +158,19 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         return;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    for (auto &kv : c->pics) (void)hipFree(kv.second.mem);
+    if (c->ustream)
+        (void)hipStreamSynchronize(c->ustream);
+    for (auto &kv : c->pics) {
+        (void)hipFree(kv.second.mem);
+        if (kv.second.ready)
+            (void)hipEventDestroy(kv.second.ready);
+        if (kv.second.used)
+            (void)hipEventDestroy(kv.second.used);
+    }
     if (c->staging)
         (void)hipFree(c->staging);
+    if (c->ustaging)
+        (void)hipFree(c->ustaging);
     if (c->d_records)
         (void)hipFree(c->d_records);
     if (c->d_sb)
@@ -178,7 +195,25 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
     if (c->d_cslot)
         (void)hipFree(c->d_cslot);
     (void)hipStreamDestroy(c->stream);
+    if (c->ustream)
+        (void)hipStreamDestroy(c->ustream);
     delete c;
+}
+
+// the job stream waits for a picture's asynchronous upload (once)
+static svtme_status join_upload(svtme_ctx *c, PicBuf &pb) {
+    if (pb.pending) {
+        HIP_TRY(hipStreamWaitEvent(c->stream, pb.ready, 0));
+        pb.pending = false;
+    }
+    return SVTME_OK;
+}
+// no stream still uses the picture's memory
+static svtme_status quiesce(svtme_ctx *c) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->ustream)
+        HIP_TRY(hipStreamSynchronize(c->ustream));
+    return SVTME_OK;
 }
 
 extern "C" void *svtme_stream(svtme_ctx *c) { return c ? (void *)c->stream : nullptr; }
@@ -199,7 +234,14 @@ static svtme_status ensure_buf(void **p, size_t *cap, size_t need) {
 static svtme_status alloc_pic(svtme_ctx *c, uint64_t pn, uint32_t W, uint32_t H, PicBuf **out) {
     auto it = c->pics.find(pn);
     if (it != c->pics.end() && (it->second.W != W || it->second.H != H)) {
+        svtme_status qs = quiesce(c);
+        if (qs)
+            return qs;
         HIP_TRY(hipFree(it->second.mem));
+        if (it->second.ready)
+            HIP_TRY(hipEventDestroy(it->second.ready));
+        if (it->second.used)
+            HIP_TRY(hipEventDestroy(it->second.used));
         c->pics.erase(it);
         it = c->pics.end();
     }
@@ -233,15 +275,16 @@ static svtme_status alloc_pic(svtme_ctx *c, uint64_t pn, uint32_t W, uint32_t H,
 }
 
 static svtme_status build_pyramid(svtme_ctx *c, PicBuf *pb, const void *dsrc, uint32_t src_stride, uint32_t w,
-                                  uint32_t h, int ten_bit) {
+                                  uint32_t h, int ten_bit, hipStream_t st = nullptr) {
+    if (!st)
+        st = c->stream;
     uint32_t pw, ph, left, top, stride, rows, pad;
     svtme_plane_geometry(0, pb->W, pb->H, &pw, &ph, &left, &top, &stride, &rows, &pad);
     HIP_TRY(svtme_launch_build_full(dsrc, src_stride, (int)w, (int)h, ten_bit, pb->pyr.lv[0], (int)left, (int)top,
-                                    (int)rows, c->stream));
+                                    (int)rows, st));
     for (int lv = 1; lv < 3; lv++) {
         svtme_plane_geometry(lv, pb->W, pb->H, &pw, &ph, &left, &top, &stride, &rows, &pad);
-        HIP_TRY(svtme_launch_build_down(pb->pyr.lv[lv - 1], pb->pyr.lv[lv], (int)left, (int)top, (int)rows,
-                                        c->stream));
+        HIP_TRY(svtme_launch_build_down(pb->pyr.lv[lv - 1], pb->pyr.lv[lv], (int)left, (int)top, (int)rows, st));
     }
     return SVTME_OK;
 }
@@ -261,9 +304,59 @@ static svtme_status upload_host(svtme_ctx *c, uint64_t pn, const void *y, uint32
     PicBuf *pb;
     if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
         return st;
+    if ((st = join_upload(c, *pb)))
+        return st;
     if ((st = build_pyramid(c, pb, c->staging, w, w, h, ten_bit)))
         return st;
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return SVTME_OK;
+}
+
+// Asynchronous 8-bit upload: one linear DMA of the rows into a device staging
+// plane on the upload stream (a pitched copy straight into the padded plane
+// runs as a slow blit), which then builds the padded pyramid from it; the
+// first job that reads the picture waits for it on the job stream. Jobs
+// already queued that read an earlier version of the picture finish before
+// its planes are rewritten.
+extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, const uint8_t *y, uint32_t stride,
+                                                   uint32_t w, uint32_t h) {
+    if (!c || !y || w == 0 || h == 0 || stride < w)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_upload_async: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->ustream) { // high priority: its small pyramid kernels go ahead of queued search workgroups
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, hi));
+    }
+    const bool resident = c->pics.count(pn) != 0;
+    PicBuf *pb;
+    svtme_status st;
+    if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
+        return st;
+    if (resident) { // queued jobs may still read the old planes
+        if (!pb->used) { // read before any asynchronous upload: the whole queue so far
+            HIP_TRY(hipEventCreateWithFlags(&pb->used, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(pb->used, c->stream));
+        }
+        HIP_TRY(hipStreamWaitEvent(c->ustream, pb->used, 0));
+    }
+    if (!pb->ready)
+        HIP_TRY(hipEventCreateWithFlags(&pb->ready, hipEventDisableTiming));
+    const size_t need = (size_t)w * h;
+    if (c->ustaging_cap < need) { // only between uploads: nothing queued reads the old buffer
+        HIP_TRY(hipStreamSynchronize(c->ustream));
+        if ((st = ensure_buf(&c->ustaging, &c->ustaging_cap, need)))
+            return st;
+    }
+    if (stride == w)
+        HIP_TRY(hipMemcpyAsync(c->ustaging, y, need, hipMemcpyHostToDevice, c->ustream));
+    else
+        HIP_TRY(hipMemcpy2DAsync(c->ustaging, w, y, stride, w, h, hipMemcpyHostToDevice, c->ustream));
+    if ((st = build_pyramid(c, pb, c->ustaging, w, w, h, 0, c->ustream)))
+        return st;
+    HIP_TRY(hipEventRecord(pb->ready, c->ustream));
+    pb->pending = true;
     return SVTME_OK;
 }
 
@@ -286,6 +379,8 @@ extern "C" svtme_status svtme_picture_upload_device(svtme_ctx *c, uint64_t pn, c
     PicBuf *pb;
     svtme_status st;
     if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
+        return st;
+    if ((st = join_upload(c, *pb)))
         return st;
     if ((st = build_pyramid(c, pb, d_y, stride, w, h, 0)))
         return st;
@@ -319,8 +414,14 @@ extern "C" svtme_status svtme_picture_release(svtme_ctx *c, uint64_t pn) {
     if (it == c->pics.end())
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_release: picture %llu not resident",
                     (unsigned long long)pn);
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    svtme_status qs = quiesce(c);
+    if (qs)
+        return qs;
     HIP_TRY(hipFree(it->second.mem));
+    if (it->second.ready)
+        HIP_TRY(hipEventDestroy(it->second.ready));
+    if (it->second.used)
+        HIP_TRY(hipEventDestroy(it->second.used));
     c->pics.erase(it);
     return SVTME_OK;
 }
@@ -348,7 +449,9 @@ extern "C" svtme_status svtme_picture_download(svtme_ctx *c, uint64_t pn, int le
     if (!dst)
         return SVTME_OK;
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    svtme_status qs = quiesce(c);
+    if (qs)
+        return qs;
     HIP_TRY(hipMemcpy2D(dst, S, p.base - (ptrdiff_t)p.pad * p.stride - p.pad, (size_t)p.stride, S,
                         (size_t)(p.height + 2 * p.pad), hipMemcpyDeviceToHost));
     return SVTME_OK;
@@ -390,6 +493,9 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
         if (it->second.W != job->width || it->second.H != job->height)
             return fail(SVTME_ERR_BAD_PARAMETER, "picture %llu is %ux%u, job is %ux%u", (unsigned long long)pn,
                         it->second.W, it->second.H, job->width, job->height);
+        svtme_status js = join_upload(c, it->second);
+        if (js)
+            return js;
         *out = it->second.pyr;
         return SVTME_OK;
     };
@@ -416,7 +522,8 @@ static svtme_status ensure_ring(svtme_ctx *c) {
         return SVTME_OK;
     const size_t bytes = sizeof(DevJob) * SVTME_MAX_BATCH * svtme_ctx::kRing;
     HIP_TRY(hipMalloc((void **)&c->d_table, bytes));
-    HIP_TRY(hipHostMalloc((void **)&c->h_table, bytes, hipHostMallocDefault));
+    HIP_TRY(hipHostMalloc((void **)&c->h_table, bytes, hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void **)&c->h_table_dev, c->h_table, 0)); // read by k_copy_words
     for (int k = 0; k < svtme_ctx::kRing; k++)
         HIP_TRY(hipEventCreateWithFlags(&c->ring_copied[k], hipEventDisableTiming));
     return SVTME_OK;
@@ -529,8 +636,10 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
         if (c->ring_used[slot])
             HIP_TRY(hipEventSynchronize(c->ring_copied[slot])); // pinned slot no longer being read
         memcpy(h, ordered, sizeof(DevJob) * n);
-        HIP_TRY(hipMemcpyAsync(c->d_table + (size_t)slot * SVTME_MAX_BATCH, h, sizeof(DevJob) * n,
-                               hipMemcpyHostToDevice, c->stream));
+        static_assert(sizeof(DevJob) % 4 == 0, "DevJob copied in dwords");
+        HIP_TRY(svtme_launch_copy_words(c->h_table_dev + (size_t)slot * SVTME_MAX_BATCH,
+                                        c->d_table + (size_t)slot * SVTME_MAX_BATCH,
+                                        (uint32_t)(sizeof(DevJob) * n / 4), c->stream));
         HIP_TRY(hipEventRecord(c->ring_copied[slot], c->stream));
         c->ring_used[slot] = true;
         c->ring_n[slot]    = n;
@@ -546,6 +655,24 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
         HIP_TRY(svtme_launch_stages(d + group_start[g], ordered + group_start[g], group_start[g + 1] - group_start[g],
                                     c->stream, ev, mask));
     }
+    // mark the pictures read (an asynchronous re-upload waits for these launches only)
+    if (c->ustream)
+        for (uint32_t k = 0; k < n; k++) {
+            const svtme_job &j = jobs[k];
+            auto mark          = [&](uint64_t pn) -> svtme_status {
+                PicBuf &pb = c->pics.find(pn)->second; // resident: validate_job checked
+                if (!pb.used)
+                    HIP_TRY(hipEventCreateWithFlags(&pb.used, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(pb.used, c->stream));
+                return SVTME_OK;
+            };
+            if ((st = mark(j.picture_number)))
+                return st;
+            for (int l = 0; l < j.num_lists; l++)
+                for (int r = 0; r < j.num_refs[l]; r++)
+                    if ((st = mark(j.ref_picture_number[l][r])))
+                        return st;
+        }
     c->last_count      = (uint32_t)sbs;
     c->last_R          = n == 1 ? hj[0].R : 0;
     c->last_has_sb     = with_sb && !out;
@@ -619,8 +746,7 @@ extern "C" svtme_status svtme_sync(svtme_ctx *c) {
     if (!c)
         return fail(SVTME_ERR_BAD_PARAMETER, "null ctx");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return SVTME_OK;
+    return quiesce(c);
 }
 
 extern "C" svtme_status svtme_fetch(svtme_ctx *c, svtme_ref_record *recs, svtme_sb_result *sb) {

@@ -82,3 +82,17 @@ extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int l
     hipLaunchKernelGGL(k_build_down, dim3((n + 255) / 256), dim3(256), 0, s, prev, dst, left, top, rows);
     return hipGetLastError();
 }
+
+// The job table from pinned host memory into the device ring: a kernel read over
+// PCIe instead of a DMA, so it never queues behind a picture upload's copy on
+// the DMA engine (svtme_picture_upload_async)
+__global__ void __launch_bounds__(256) k_copy_words(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                                    uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
+extern "C" hipError_t svtme_launch_copy_words(const void *src, void *dst, uint32_t nwords, hipStream_t s) {
+    const uint32_t blocks = (nwords + 255) / 256 < 16 ? (nwords + 255) / 256 : 16;
+    hipLaunchKernelGGL(k_copy_words, dim3(blocks), dim3(256), 0, s, (const uint32_t *)src, (uint32_t *)dst, nwords);
+    return hipGetLastError();
+}

@@ -502,6 +502,8 @@ def load_product():
         lib.svtme_picture_upload.restype = C.c_int32
         lib.svtme_picture_upload_10bit.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
         lib.svtme_picture_upload_10bit.restype = C.c_int32
+        lib.svtme_picture_upload_async.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
+        lib.svtme_picture_upload_async.restype = C.c_int32
         lib.svtme_picture_upload_device.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
         lib.svtme_picture_upload_device.restype = C.c_int32
         lib.svtme_picture_invalidate.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
@@ -578,6 +580,17 @@ class GpuME:
         else:
             self._check(self.lib.svtme_picture_upload(self.ctx, picture_number, y.ctypes.data, w, w, h),
                         "svtme_picture_upload")
+
+    def upload_async(self, picture_number: int, y, w: int = 0, h: int = 0, stride: int = 0):
+        """Asynchronous 8-bit upload (svtme_picture_upload_async): `y` is a uint8
+        array or a host pointer (then w, h, stride); keep it alive until sync."""
+        if isinstance(y, np.ndarray):
+            h, w = y.shape
+            stride, ptr = w, y.ctypes.data
+        else:
+            ptr = y
+        self._check(self.lib.svtme_picture_upload_async(self.ctx, picture_number, ptr, stride or w, w, h),
+                    "svtme_picture_upload_async")
 
     def upload_device(self, picture_number: int, dev_ptr: int, stride: int, w: int, h: int):
         self._check(self.lib.svtme_picture_upload_device(self.ctx, picture_number, dev_ptr, stride, w, h),

@@ -28,6 +28,11 @@ def svtme():
 
 @pytest.fixture(scope="session")
 def gpu(svtme):
+    # torch's HIP runtime first (as bench.py does): tests allocate device and
+    # pinned buffers with torch, whose lazy init fails after the library's
+    import torch
+
+    torch.cuda.set_device(0)
     g = svtme.GpuME(0)
     yield g
     g.close()

@@ -210,6 +210,46 @@ def test_banded_fullpel_variance_parity(svtme, gpu, area, th, k32):
     assert not _controls_case(S, gpu, ctrl, 640, 360, (7, 6), (9,))
 
 
+def test_picture_upload_async(svtme, gpu):
+    """svtme_picture_upload_async: DMA into the resident plane + in-place pyramid
+    build on the upload stream; the planes equal the reference's pyramid, a job
+    queued before a re-upload of one of its references reads the old planes and
+    a job after it the new ones (device outputs, nothing synchronised between),
+    and a pinned source behaves like a pageable one."""
+    import torch
+
+    S = svtme
+    w, h = 328, 200  # not multiples of 64: partial SBs, pad-to-8 columns and rows
+    syn = S.Synth(w, h)
+    old, new = syn.frame(7), syn.frame(12)
+    cur, ref9 = syn.frame(8), syn.frame(9)
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    gpu.upload_async(4108, cur)
+    pinned = torch.from_numpy(np.ascontiguousarray(old)).pin_memory()
+    gpu.upload_async(4107, pinned.data_ptr(), w, h)
+    gpu.upload_async(4109, ref9)
+    W8, H8 = (w + 7) & ~7, (h + 7) & ~7
+    job = S.make_job(W8, H8, ctrl, 4108, (4107,), (4109,), temporal_layer_index=1, ref_count_used=(1, 1))
+    R = S.ref_slots(job)
+    n = S.sb_total(W8, H8)
+    bufs = [torch.zeros(n * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    gpu.submit_batch_device([job], [bufs[0].data_ptr()])
+    gpu.upload_async(4107, new)  # re-upload while the first job may still run
+    gpu.submit_batch_device([job], [bufs[1].data_ptr()])
+    gpu.sync()
+    got = [np.frombuffer(b.cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n, R) for b in bufs]
+    p_new = S.build_host_pyramid(new, "oracle")
+    for lv, name in enumerate(("full", "quarter", "sixteenth")):
+        assert np.array_equal(gpu.download(4107, lv), getattr(p_new, name)), name
+        assert np.array_equal(gpu.download(4108, lv), getattr(S.build_host_pyramid(cur, "oracle"), name)), name
+    pyr = {8: S.build_host_pyramid(cur, "oracle"), 9: S.build_host_pyramid(ref9, "oracle")}
+    for ref7, g in ((S.build_host_pyramid(old, "oracle"), got[0]), (p_new, got[1])):
+        orecs, _ = S.run_checker(job, pyr[8], {(0, 0): ref7, (1, 0): pyr[9]}, "oracle", nthreads=8)
+        assert not S.compare_records(orecs, g)
+    for pn in (4107, 4108, 4109):
+        gpu.release(pn)
+
+
 def test_picture_invalidate(svtme, gpu):
     """svtme_picture_invalidate (TF re-decimation, temporal_filtering.c:3895-3931):
     the resident pyramid is rebuilt from the new planes, jobs queued before it
