@@ -8,16 +8,19 @@ resident in HBM before the timed region (the PA stage builds them once per
 picture). --workload picks another BASELINE config (svt-av1-mirror_amd/workloads.py).
 
 One step, on N GPUs (one process per GPU, torch.distributed over RCCL): 4 N
-pictures (the encoder's look-ahead keeps several pictures' ME in flight; the
-C host batches whole pictures, BASELINE.json north_star), each split into N
-equal SB chunks (SBs are independent given the picture
-controls); rank r searches chunk r of every picture in ONE batched launch
-(svtme_submit_batch_device), then the ranks all-gather their record chunks
-over RCCL (one all_gather_into_tensor per step, device buffers, on a
-communication stream overlapped with the next step's ME). Per-GPU work is four
-pictures' worth of SBs at every N: "scaling" is weak. value = SBs of all
-pictures / max-over-ranks time. "single_picture" reports the latency mode
-(one picture per GPU per launch) on the same jobs.
+pictures (the encoder keeps several look-ahead pictures' ME in flight; the
+north star's C host batches whole pictures), each split into N equal SB
+chunks (SBs are independent given the picture controls); rank
+r searches chunk r of every picture in ONE launch (svtme_submit_batch_device),
+then the ranks all-gather their record chunks over RCCL (one
+all_gather_into_tensor per step, device buffers, on a communication stream
+overlapped with the next step's ME). Per-GPU work is four pictures' worth of
+SBs at every N: "scaling" is weak. value = SBs of all pictures / max-over-ranks
+wall time. "overlapped" reports one picture per GPU per step with consecutive
+steps alternating the library's two submission lanes (own streams and
+scratch: one step's workgroups fill the CUs while the previous one drains, as
+the reference's ME threads work on several pictures at once); its kernels
+overlap, so it is a chip-level rate beside the per-kernel roofline.
 
 roofline: the ME pass (the five stage kernels, back to back on the library's
 stream) — algorithmic bytes per pass (bytes/SB x SBs per
@@ -61,7 +64,7 @@ STAGE_BYTES_P8 = {"k_stage_a": (2176, 6808), "k_stage_d": (0, 0), "k_stage_b": (
 # the whole pass in k_hme (fused full-pel + decode): every byte of the pass
 STAGE_BYTES_P8_ALL = (2688, 16798 + 680)
 PICTURE_STRIDE = 32  # picture p of a step pans from t = 8 + 32 p (distinct content per picture)
-PICTURES_PER_GPU = 4  # pictures of one step per GPU (one batched launch); --pictures overrides
+PICTURES_PER_GPU = 4  # pictures of one step per GPU, one batched launch (--pictures overrides)
 MAX_BATCH = 16  # SVTME_MAX_BATCH_JOBS (include/svtme.h): jobs of one batched launch
 
 
@@ -110,11 +113,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="4k_p8", choices=sorted(W.WORKLOADS))
     ap.add_argument("--pictures", type=int, default=0,
-                    help=f"pictures per step (default: {PICTURES_PER_GPU} per GPU, one batched launch)")
+                    help=f"pictures per step (default: {PICTURES_PER_GPU} per GPU; several go in one batched launch)")
     ap.add_argument("--kernel-samples", type=int, default=20, help="steps timed per kernel after the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-single-picture", action="store_true", help="skip the one-picture latency-mode timing")
+    ap.add_argument("--no-single-picture", "--no-alt-mode", dest="no_alt", action="store_true",
+                    help="skip the timing of the other picture count (batched / single picture)")
     ap.add_argument("--no-upload", action="store_true", help="skip the host-upload (PCIe-inclusive) timing")
+    ap.add_argument("--lanes", type=int, default=1, choices=(1, 2),
+                    help="submission lanes the timed steps alternate over (svtme_submit_batch_device_lane); the "
+                         "overlapped two-lane rate is reported beside the one-lane value")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="target CPU-seconds of the baseline sample")
     args = ap.parse_args()
 
@@ -138,6 +145,7 @@ def main():
     wl = W.WORKLOADS[name]
     Wd, Ht = wl["w"], wl["h"]
     P = args.pictures or PICTURES_PER_GPU * world
+    P_alt = world  # one picture per GPU per step: the "overlapped" mode reported beside the main one
     n_sb = S.sb_total(Wd, Ht)
     slots = D.chunk_slots(n_sb, world)
     begin, count = D.sb_chunk(n_sb, rank, world)
@@ -146,7 +154,7 @@ def main():
     syn = S.Synth(Wd, Ht)
     offs = sorted(set((0,) + tuple(t - 8 for t in wl["l0"]) + tuple(t - 8 for t in wl["l1"])))
     jobs = []
-    for p in range(P):
+    for p in range(max(P, P_alt)):
         t0 = 8 + PICTURE_STRIDE * p
         for o in offs:
             t = t0 + o
@@ -157,24 +165,29 @@ def main():
     rec = S.REF_RECORD_DTYPE.itemsize
     chunk_bytes = slots * R * rec
     dev = torch.device("cuda", local_rank)
-    local = [torch.zeros(P * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-    gathered = [torch.empty(world * P * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)] \
+    PM = max(P, P_alt)
+    local = [torch.zeros(PM * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+    gathered = [torch.empty(world * PM * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)] \
         if world > 1 else None
-    ext = torch.cuda.ExternalStream(gpu.stream(), device=dev)
+    NL = args.lanes
+    exts = [torch.cuda.ExternalStream(gpu.lane_stream(l), device=dev) for l in range(2)]
+    ext = exts[0]
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
     me_done = [torch.cuda.Event() for _ in range(2)]
     g_done = [torch.cuda.Event() for _ in range(2)]
     used = [False, False]
 
-    def step(i, n_pic=P):
+    def step(i, n_pic=P, nl=NL):
         b = i & 1
+        es = exts[b % nl]  # with two lanes, step i on lane i mod 2: consecutive steps overlap on the GPU
         if used[b] and world > 1:
-            ext.wait_event(g_done[b])  # the gather of step i-2 has read local[b]
+            es.wait_event(g_done[b])  # the gather of step i-2 has read local[b]
         for g0 in range(0, n_pic, MAX_BATCH):  # SVTME_MAX_BATCH_JOBS jobs per launch
             g1 = min(n_pic, g0 + MAX_BATCH)
-            gpu.submit_batch_device(jobs[g0:g1], [local[b].data_ptr() + p * chunk_bytes for p in range(g0, g1)])
+            gpu.submit_batch_device(jobs[g0:g1], [local[b].data_ptr() + p * chunk_bytes for p in range(g0, g1)],
+                                    lane=b % nl)
         if world > 1:
-            me_done[b].record(ext)
+            me_done[b].record(es)
             comm.wait_event(me_done[b])
             D.gather_chunks_device(local[b], gathered[b], dist, stream=comm)
             g_done[b].record(comm)
@@ -191,11 +204,17 @@ def main():
         step(i)
     fence()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    join = torch.cuda.Event()
+
+    def end_on_lane0(ev):  # lane 0 waits for the other lane's queue, then records ev
+        join.record(exts[1])
+        ext.wait_event(join)
+        ev.record(ext)
     t0 = time.perf_counter()
     ev0.record(ext)
     for i in range(args.steps):
         step(args.warmup + i)
-    ev1.record(ext)
+    end_on_lane0(ev1)
     fence()
     elapsed = time.perf_counter() - t0
     device_ms = ev0.elapsed_time(ev1) / args.steps  # the library stream's time per step (HIP events)
@@ -207,18 +226,23 @@ def main():
     fence()
     gpu.set_timing(False)
     n_timed, stage_ms = gpu.timing_read()
-    # latency mode: one picture per GPU per launch (the same jobs, P = world)
-    lat_ms = None
-    if P > world and not args.no_single_picture:
+    # overlapped mode: one picture per GPU per step, consecutive steps on the two
+    # submission lanes (the next step's workgroups fill the CUs while the previous
+    # step drains; kernels overlap, so this is a chip-level rate, not a per-kernel one)
+    alt_ms = None
+    if not args.no_alt:
         for i in range(args.warmup):
-            step(i, world)
+            step(i, P_alt, 2)
         fence()
-        ev0.record(ext)
+        t0a = time.perf_counter()
         for i in range(args.steps):
-            step(args.warmup + i, world)
-        ev1.record(ext)
+            step(args.warmup + i, P_alt, 2)
         fence()
-        lat_ms = ev0.elapsed_time(ev1) / args.steps
+        alt_ms = (time.perf_counter() - t0a) / args.steps * 1e3
+        if world > 1:
+            ta = torch.tensor([alt_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(ta, op=dist.ReduceOp.MAX)
+            alt_ms = float(ta.item())
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -338,13 +362,17 @@ def main():
             "data": "synthetic (integer PCG32 panning texture, SURVEY.md 8(d)); pyramids resident in HBM",
             "config": {"workload": wl["desc"], "name": name, "sbs_per_picture": n_sb, "refs": R,
                        "pictures_per_step": P,
+                       "lanes": NL,
                        "parallelism": f"{world} GPU(s): each picture split in {world} equal SB chunks, "
-                                      f"rank r searches chunk r of all {P} pictures in one batched launch per "
-                                      f"stage" + (", RCCL all-gather of the record chunks" if world > 1 else "")},
-            "single_picture": None if lat_ms is None else {
-                "pictures_per_step": world, "ms_per_step": round(lat_ms, 4),
-                "value": round(n_sb * world / (lat_ms * 1e-3), 1),
-                "note": "latency mode: one picture per GPU per launch (library-stream HIP events)"},
+                                      f"rank r searches chunk r of all {P} pictures in one launch per step" +
+                                      (", consecutive steps on alternating submission lanes" if NL > 1 else "") +
+                                      (", RCCL all-gather of the record chunks" if world > 1 else "")},
+            "overlapped": None if alt_ms is None else {
+                "pictures_per_step": P_alt, "lanes": 2, "ms_per_step": round(alt_ms, 4),
+                "value": round(n_sb * P_alt / (alt_ms * 1e-3), 1),
+                "algorithmic_hbm_gbps": round(bps * n_sb * P_alt / (alt_ms * 1e-3) / 1e9, 1),
+                "note": "one picture per GPU per step, consecutive steps alternating the two submission lanes "
+                        "(svtme_submit_batch_device_lane): kernels of consecutive steps overlap, wall clock"},
             "upload": upload,
             "sb_ref_per_s": round(value * R, 1),
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),

@@ -287,6 +287,19 @@ svtme_status svtme_submit_picture_device(svtme_ctx *ctx, const svtme_job *job, s
 #define SVTME_MAX_BATCH_JOBS 16
 svtme_status svtme_submit_batch_device(svtme_ctx *ctx, const svtme_job *jobs, uint32_t n,
                                        svtme_ref_record *const *d_ref_records, svtme_sb_result *const *d_sb_results);
+/* The same on submission lane `lane` (0 .. SVTME_LANES-1): each lane has its own
+ * stream (svtme_lane_stream; lane 0's is svtme_stream) and inter-stage
+ * scratch, so batches on different lanes overlap on the GPU (the next batch's
+ * workgroups fill the CUs while the previous one drains) the way the
+ * reference's ME threads process pictures concurrently. Pictures are shared:
+ * a lane waits for asynchronous uploads, and a re-upload or rebuild waits for
+ * every lane's queued readers. Completion is signalled on the lane's stream. */
+#define SVTME_LANES 2
+svtme_status svtme_submit_batch_device_lane(svtme_ctx *ctx, uint32_t lane, const svtme_job *jobs, uint32_t n,
+                                            svtme_ref_record *const *d_ref_records,
+                                            svtme_sb_result *const *d_sb_results);
+/* The hipStream_t of a lane (created on first use), NULL on a bad lane. */
+void *svtme_lane_stream(svtme_ctx *ctx, uint32_t lane);
 /* Kernel timing with HIP events on the context's stream, recorded around every
  * stage launch of every submission while enabled (enable = 1). svtme_timing_read
  * waits for the recorded submissions and returns, averaged over them, the

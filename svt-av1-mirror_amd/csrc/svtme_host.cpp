@@ -77,9 +77,30 @@ struct PicBuf {
     size_t bytes = 0;
     uint32_t W = 0, H = 0;
     DevPyramid pyr{};
-    hipEvent_t ready = nullptr; // end of an asynchronous upload on the upload stream
-    bool pending     = false;   // the job stream has not waited on `ready` yet
-    hipEvent_t used  = nullptr; // after the last launch that reads the picture (job stream)
+    hipEvent_t ready = nullptr;           // end of an asynchronous upload on the upload stream
+    uint32_t pending = 0;                 // lanes whose stream has not waited on `ready` yet
+    hipEvent_t used[SVTME_LANES] = {};    // end of the last submission of each lane that reads the
+                                          // picture (a lane's submission event, not owned)
+};
+
+// A submission lane: a stream and the inter-stage scratch of the jobs running
+// on it. Submissions on different lanes overlap on the GPU (the next one's
+// workgroups fill the CUs while the previous one drains); lane 0's stream is
+// the context's stream.
+struct Lane {
+    hipStream_t s = nullptr;
+    static constexpr int kEv = 64;  // submission events, recorded round-robin: one per submission
+    hipEvent_t ev[kEv] = {};
+    int ev_next        = 0;
+    ARes *d_ares    = nullptr; // stage-A results [count][SVTME_A_N]
+    size_t ares_cap = 0;
+    BState *d_bst   = nullptr; // stage-B state [count]
+    size_t bst_cap  = 0;
+    unsigned long long *d_keys = nullptr; // wide full-pel argmin keys [count][R][85]
+    size_t keys_cap            = 0;
+    bool keys_rest             = false; // every key is ~0 (banded jobs accumulate with atomic min)
+    CSlot *d_cslot             = nullptr; // [count][R]
+    size_t cslot_cap           = 0;
 };
 
 struct svtme_ctx {
@@ -104,6 +125,7 @@ struct svtme_ctx {
     static constexpr int kRing = 16;
     DevJob *d_table = nullptr, *h_table = nullptr, *h_table_dev = nullptr;
     hipEvent_t ring_copied[kRing] = {}; // the copy out of the pinned slot has run
+    hipEvent_t ring_read[kRing] = {};   // end of the last submission that read the slot (not owned)
     bool ring_used[kRing] = {};
     uint32_t ring_n[kRing] = {};
     int ring_next = 0;
@@ -114,15 +136,7 @@ struct svtme_ctx {
     hipEvent_t tev[kTimeSets][10] = {};
     uint32_t tmask[kTimeSets] = {};
     int t_pending = 0;
-    ARes *d_ares    = nullptr; // stage-A results [count][SVTME_A_N]
-    size_t ares_cap = 0;
-    BState *d_bst   = nullptr; // stage-B state [count]
-    size_t bst_cap  = 0;
-    unsigned long long *d_keys = nullptr; // wide full-pel argmin keys [count][R][85]
-    size_t keys_cap            = 0;
-    bool keys_rest             = false; // every key is ~0 (banded jobs accumulate with atomic min)
-    CSlot *d_cslot             = nullptr; // [count][R]
-    size_t cslot_cap           = 0;
+    Lane lanes[SVTME_LANES]; // lanes[0].s == stream
     std::mutex mu;
 };
 
@@ -149,6 +163,7 @@ extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
         delete c;
         return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "hipStreamCreate: %s", hipGetErrorString(e));
     }
+    c->lanes[0].s = c->stream;
     *out = c;
     return SVTME_OK;
 }
@@ -157,15 +172,15 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
     if (!c)
         return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    for (auto &L : c->lanes)
+        if (L.s)
+            (void)hipStreamSynchronize(L.s);
     if (c->ustream)
         (void)hipStreamSynchronize(c->ustream);
     for (auto &kv : c->pics) {
         (void)hipFree(kv.second.mem);
         if (kv.second.ready)
             (void)hipEventDestroy(kv.second.ready);
-        if (kv.second.used)
-            (void)hipEventDestroy(kv.second.used);
     }
     if (c->staging)
         (void)hipFree(c->staging);
@@ -186,37 +201,73 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         (void)hipFree(c->d_table);
     if (c->h_table)
         (void)hipHostFree(c->h_table);
-    if (c->d_ares)
-        (void)hipFree(c->d_ares);
-    if (c->d_bst)
-        (void)hipFree(c->d_bst);
-    if (c->d_keys)
-        (void)hipFree(c->d_keys);
-    if (c->d_cslot)
-        (void)hipFree(c->d_cslot);
+    for (int l = 0; l < SVTME_LANES; l++) {
+        Lane &L = c->lanes[l];
+        if (L.d_ares)
+            (void)hipFree(L.d_ares);
+        if (L.d_bst)
+            (void)hipFree(L.d_bst);
+        if (L.d_keys)
+            (void)hipFree(L.d_keys);
+        if (L.d_cslot)
+            (void)hipFree(L.d_cslot);
+        for (auto &e : L.ev)
+            if (e)
+                (void)hipEventDestroy(e);
+        if (l > 0 && L.s)
+            (void)hipStreamDestroy(L.s);
+    }
     (void)hipStreamDestroy(c->stream);
     if (c->ustream)
         (void)hipStreamDestroy(c->ustream);
     delete c;
 }
 
-// the job stream waits for a picture's asynchronous upload (once)
-static svtme_status join_upload(svtme_ctx *c, PicBuf &pb) {
-    if (pb.pending) {
-        HIP_TRY(hipStreamWaitEvent(c->stream, pb.ready, 0));
-        pb.pending = false;
+// lane `lane`'s stream waits for a picture's asynchronous upload (once per upload)
+static svtme_status join_upload(svtme_ctx *c, PicBuf &pb, int lane) {
+    if ((pb.pending >> lane) & 1u) {
+        HIP_TRY(hipStreamWaitEvent(c->lanes[lane].s, pb.ready, 0));
+        pb.pending &= ~(1u << lane);
     }
+    return SVTME_OK;
+}
+// `s` waits for every launch of the other lanes already queued that reads the picture
+static svtme_status after_readers(svtme_ctx *c, PicBuf &pb, hipStream_t s) {
+    for (int l = 0; l < SVTME_LANES; l++)
+        if (pb.used[l] && c->lanes[l].s != s)
+            HIP_TRY(hipStreamWaitEvent(s, pb.used[l], 0));
     return SVTME_OK;
 }
 // no stream still uses the picture's memory
 static svtme_status quiesce(svtme_ctx *c) {
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (auto &L : c->lanes)
+        if (L.s)
+            HIP_TRY(hipStreamSynchronize(L.s));
     if (c->ustream)
         HIP_TRY(hipStreamSynchronize(c->ustream));
     return SVTME_OK;
 }
+static svtme_status ensure_lane(svtme_ctx *c, uint32_t lane) {
+    if (lane >= SVTME_LANES)
+        return fail(SVTME_ERR_BAD_PARAMETER, "lane %u (0..%d)", lane, SVTME_LANES - 1);
+    Lane &L = c->lanes[lane];
+    if (!L.s)
+        HIP_TRY(hipStreamCreateWithFlags(&L.s, hipStreamNonBlocking));
+    if (!L.ev[0])
+        for (auto &e : L.ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return SVTME_OK;
+}
 
 extern "C" void *svtme_stream(svtme_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+extern "C" void *svtme_lane_stream(svtme_ctx *c, uint32_t lane) {
+    if (!c)
+        return nullptr;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess || ensure_lane(c, lane))
+        return nullptr;
+    return (void *)c->lanes[lane].s;
+}
 
 static svtme_status ensure_buf(void **p, size_t *cap, size_t need) {
     if (*cap >= need)
@@ -240,8 +291,6 @@ static svtme_status alloc_pic(svtme_ctx *c, uint64_t pn, uint32_t W, uint32_t H,
         HIP_TRY(hipFree(it->second.mem));
         if (it->second.ready)
             HIP_TRY(hipEventDestroy(it->second.ready));
-        if (it->second.used)
-            HIP_TRY(hipEventDestroy(it->second.used));
         c->pics.erase(it);
         it = c->pics.end();
     }
@@ -304,7 +353,7 @@ static svtme_status upload_host(svtme_ctx *c, uint64_t pn, const void *y, uint32
     PicBuf *pb;
     if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
         return st;
-    if ((st = join_upload(c, *pb)))
+    if ((st = join_upload(c, *pb, 0)) || (st = after_readers(c, *pb, c->stream)))
         return st;
     if ((st = build_pyramid(c, pb, c->staging, w, w, h, ten_bit)))
         return st;
@@ -334,13 +383,8 @@ extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, co
     svtme_status st;
     if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
         return st;
-    if (resident) { // queued jobs may still read the old planes
-        if (!pb->used) { // read before any asynchronous upload: the whole queue so far
-            HIP_TRY(hipEventCreateWithFlags(&pb->used, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(pb->used, c->stream));
-        }
-        HIP_TRY(hipStreamWaitEvent(c->ustream, pb->used, 0));
-    }
+    if (resident && (st = after_readers(c, *pb, c->ustream))) // queued jobs may still read the old planes
+        return st;
     if (!pb->ready)
         HIP_TRY(hipEventCreateWithFlags(&pb->ready, hipEventDisableTiming));
     const size_t need = (size_t)w * h;
@@ -356,7 +400,7 @@ extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, co
     if ((st = build_pyramid(c, pb, c->ustaging, w, w, h, 0, c->ustream)))
         return st;
     HIP_TRY(hipEventRecord(pb->ready, c->ustream));
-    pb->pending = true;
+    pb->pending = (1u << SVTME_LANES) - 1u;
     return SVTME_OK;
 }
 
@@ -380,7 +424,7 @@ extern "C" svtme_status svtme_picture_upload_device(svtme_ctx *c, uint64_t pn, c
     svtme_status st;
     if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
         return st;
-    if ((st = join_upload(c, *pb)))
+    if ((st = join_upload(c, *pb, 0)) || (st = after_readers(c, *pb, c->stream)))
         return st;
     if ((st = build_pyramid(c, pb, d_y, stride, w, h, 0)))
         return st;
@@ -420,8 +464,6 @@ extern "C" svtme_status svtme_picture_release(svtme_ctx *c, uint64_t pn) {
     HIP_TRY(hipFree(it->second.mem));
     if (it->second.ready)
         HIP_TRY(hipEventDestroy(it->second.ready));
-    if (it->second.used)
-        HIP_TRY(hipEventDestroy(it->second.used));
     c->pics.erase(it);
     return SVTME_OK;
 }
@@ -460,7 +502,7 @@ extern "C" svtme_status svtme_picture_download(svtme_ctx *c, uint64_t pn, int le
 // ----------------------------------------------------------------------------
 // jobs
 // ----------------------------------------------------------------------------
-static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj, uint32_t *count) {
+static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj, uint32_t *count, int lane) {
     if (!job)
         return fail(SVTME_ERR_BAD_PARAMETER, "null job");
     if ((job->width & 7) || (job->height & 7) || job->width == 0 || job->height == 0)
@@ -493,7 +535,7 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
         if (it->second.W != job->width || it->second.H != job->height)
             return fail(SVTME_ERR_BAD_PARAMETER, "picture %llu is %ux%u, job is %ux%u", (unsigned long long)pn,
                         it->second.W, it->second.H, job->width, job->height);
-        svtme_status js = join_upload(c, it->second);
+        svtme_status js = join_upload(c, it->second, lane);
         if (js)
             return js;
         *out = it->second.pyr;
@@ -533,16 +575,21 @@ static svtme_status ensure_ring(svtme_ctx *c) {
 // job k; null out => the context's own record buffer (single job only).
 static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uint32_t n,
                                         svtme_ref_record *const *out, svtme_sb_result *const *out_sb,
-                                        bool with_sb) {
+                                        bool with_sb, uint32_t lane = 0) {
     HIP_TRY(hipSetDevice(c->device));
+    svtme_status st;
+    if ((st = ensure_lane(c, lane)))
+        return st;
+    Lane &L = c->lanes[lane];
+    if (!out && lane != 0)
+        return fail(SVTME_ERR_BAD_PARAMETER, "context-owned outputs are lane 0's");
     if (n == 0 || n > SVTME_MAX_BATCH)
         return fail(SVTME_ERR_BAD_PARAMETER, "batch of %u jobs (1..%d)", n, SVTME_MAX_BATCH);
     DevJob hj[SVTME_MAX_BATCH];
     uint32_t count[SVTME_MAX_BATCH];
     size_t sbs = 0, slots = 0;
-    svtme_status st;
     for (uint32_t k = 0; k < n; k++) {
-        if ((st = validate_job(c, &jobs[k], &hj[k], &count[k])))
+        if ((st = validate_job(c, &jobs[k], &hj[k], &count[k], (int)lane)))
             return st;
         sbs += count[k];
         slots += (size_t)count[k] * hj[k].R;
@@ -567,9 +614,12 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
         }
     }
     // inter-stage scratch of the whole batch, per-job offsets
-    if ((st = ensure_buf((void **)&c->d_ares, &c->ares_cap, sbs * SVTME_A_N * sizeof(ARes))))
+    // a lane's scratch grows only between its submissions: the old buffers are idle
+    if (L.ares_cap < sbs * SVTME_A_N * sizeof(ARes) || L.bst_cap < sbs * sizeof(BState))
+        HIP_TRY(hipStreamSynchronize(L.s));
+    if ((st = ensure_buf((void **)&L.d_ares, &L.ares_cap, sbs * SVTME_A_N * sizeof(ARes))))
         return st;
-    if ((st = ensure_buf((void **)&c->d_bst, &c->bst_cap, sbs * sizeof(BState))))
+    if ((st = ensure_buf((void **)&L.d_bst, &L.bst_cap, sbs * sizeof(BState))))
         return st;
     bool any_banded = false, any_single = false, any_wide = false;
     for (uint32_t k = 0; k < n; k++) {
@@ -580,25 +630,27 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
     }
     if (any_wide) { // wide full-pel stage (k_stage_c1 + k_stage_e)
         const size_t kb = slots * SVTME_PU_COUNT * sizeof(unsigned long long);
-        if (c->keys_cap < kb) {
-            if ((st = ensure_buf((void **)&c->d_keys, &c->keys_cap, kb)))
+        if (L.keys_cap < kb || L.cslot_cap < slots * sizeof(CSlot))
+            HIP_TRY(hipStreamSynchronize(L.s));
+        if (L.keys_cap < kb) {
+            if ((st = ensure_buf((void **)&L.d_keys, &L.keys_cap, kb)))
                 return st;
-            c->keys_rest = false;
+            L.keys_rest = false;
         }
-        if ((st = ensure_buf((void **)&c->d_cslot, &c->cslot_cap, slots * sizeof(CSlot))))
+        if ((st = ensure_buf((void **)&L.d_cslot, &L.cslot_cap, slots * sizeof(CSlot))))
             return st;
         // banded jobs merge with atomic min into keys that must all be ~0; k_stage_e
         // resets what it consumed, plain-store (single band) jobs leave keys behind
-        if (any_banded && !c->keys_rest)
-            HIP_TRY(hipMemsetAsync(c->d_keys, 0xFF, c->keys_cap, c->stream));
-        c->keys_rest = !any_single;
+        if (any_banded && !L.keys_rest)
+            HIP_TRY(hipMemsetAsync(L.d_keys, 0xFF, L.keys_cap, L.s));
+        L.keys_rest = !any_single;
     }
     size_t sb_off = 0, slot_off = 0;
     for (uint32_t k = 0; k < n; k++) {
-        hj[k].ares  = c->d_ares + sb_off * SVTME_A_N;
-        hj[k].bst   = c->d_bst + sb_off;
-        hj[k].keys  = hj[k].parts ? c->d_keys + slot_off * SVTME_PU_COUNT : nullptr;
-        hj[k].cslot = hj[k].parts ? c->d_cslot + slot_off : nullptr;
+        hj[k].ares  = L.d_ares + sb_off * SVTME_A_N;
+        hj[k].bst   = L.d_bst + sb_off;
+        hj[k].keys  = hj[k].parts ? L.d_keys + slot_off * SVTME_PU_COUNT : nullptr;
+        hj[k].cslot = hj[k].parts ? L.d_cslot + slot_off : nullptr;
         svtme_stage_a_list(&hj[k].job, hj[k].ta_list, &hj[k].ta_count);
         svtme_stage_b_list(&hj[k].job, hj[k].tb_list, &hj[k].tb_count);
         svtme_hme_prepare(&hj[k]);
@@ -633,14 +685,17 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
         slot         = c->ring_next;
         c->ring_next = (slot + 1) % svtme_ctx::kRing;
         DevJob *h    = c->h_table + (size_t)slot * SVTME_MAX_BATCH;
-        if (c->ring_used[slot])
-            HIP_TRY(hipEventSynchronize(c->ring_copied[slot])); // pinned slot no longer being read
+        if (c->ring_used[slot]) { // its pinned copy and the launches that read it (any lane) are done
+            HIP_TRY(hipEventSynchronize(c->ring_copied[slot]));
+            if (c->ring_read[slot])
+                HIP_TRY(hipEventSynchronize(c->ring_read[slot]));
+        }
         memcpy(h, ordered, sizeof(DevJob) * n);
         static_assert(sizeof(DevJob) % 4 == 0, "DevJob copied in dwords");
         HIP_TRY(svtme_launch_copy_words(c->h_table_dev + (size_t)slot * SVTME_MAX_BATCH,
                                         c->d_table + (size_t)slot * SVTME_MAX_BATCH,
-                                        (uint32_t)(sizeof(DevJob) * n / 4), c->stream));
-        HIP_TRY(hipEventRecord(c->ring_copied[slot], c->stream));
+                                        (uint32_t)(sizeof(DevJob) * n / 4), L.s));
+        HIP_TRY(hipEventRecord(c->ring_copied[slot], L.s));
         c->ring_used[slot] = true;
         c->ring_n[slot]    = n;
     }
@@ -653,17 +708,18 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
             mask = &c->tmask[c->t_pending++];
         }
         HIP_TRY(svtme_launch_stages(d + group_start[g], ordered + group_start[g], group_start[g + 1] - group_start[g],
-                                    c->stream, ev, mask));
+                                    L.s, ev, mask));
     }
-    // mark the pictures read (an asynchronous re-upload waits for these launches only)
-    if (c->ustream)
-        for (uint32_t k = 0; k < n; k++) {
+    // one event per submission: the slot and the pictures it read point at it
+    // (a re-upload / rebuild waits for these launches only)
+    hipEvent_t done = L.ev[L.ev_next];
+    L.ev_next       = (L.ev_next + 1) % Lane::kEv;
+    HIP_TRY(hipEventRecord(done, L.s));
+    c->ring_read[slot] = done;
+    for (uint32_t k = 0; k < n; k++) {
             const svtme_job &j = jobs[k];
             auto mark          = [&](uint64_t pn) -> svtme_status {
-                PicBuf &pb = c->pics.find(pn)->second; // resident: validate_job checked
-                if (!pb.used)
-                    HIP_TRY(hipEventCreateWithFlags(&pb.used, hipEventDisableTiming));
-                HIP_TRY(hipEventRecord(pb.used, c->stream));
+                c->pics.find(pn)->second.used[lane] = done; // resident: validate_job checked
                 return SVTME_OK;
             };
             if ((st = mark(j.picture_number)))
@@ -700,6 +756,15 @@ extern "C" svtme_status svtme_submit_batch_device(svtme_ctx *c, const svtme_job 
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_batch_device: null ctx, jobs or outputs");
     std::lock_guard<std::mutex> lk(c->mu);
     return submit_batch_locked(c, jobs, n, d_recs, d_sb, d_sb != nullptr);
+}
+
+extern "C" svtme_status svtme_submit_batch_device_lane(svtme_ctx *c, uint32_t lane, const svtme_job *jobs,
+                                                       uint32_t n, svtme_ref_record *const *d_recs,
+                                                       svtme_sb_result *const *d_sb) {
+    if (!c || !jobs || !d_recs)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_batch_device_lane: null ctx, jobs or outputs");
+    std::lock_guard<std::mutex> lk(c->mu);
+    return submit_batch_locked(c, jobs, n, d_recs, d_sb, d_sb != nullptr, lane);
 }
 
 extern "C" svtme_status svtme_set_timing(svtme_ctx *c, int enable) {

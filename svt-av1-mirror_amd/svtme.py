@@ -529,6 +529,11 @@ def load_product():
         lib.svtme_timing_read.restype = C.c_uint32
         lib.svtme_submit_batch_device.argtypes = [vp, C.POINTER(Job), C.c_uint32, C.POINTER(vp), C.POINTER(vp)]
         lib.svtme_submit_batch_device.restype = C.c_int32
+        lib.svtme_submit_batch_device_lane.argtypes = [vp, C.c_uint32, C.POINTER(Job), C.c_uint32, C.POINTER(vp),
+                                                       C.POINTER(vp)]
+        lib.svtme_submit_batch_device_lane.restype = C.c_int32
+        lib.svtme_lane_stream.argtypes = [vp, C.c_uint32]
+        lib.svtme_lane_stream.restype = vp
         lib.svtme_device_records.argtypes = [vp, C.POINTER(C.c_uint64)]
         lib.svtme_device_records.restype = vp
         lib.svtme_stream.argtypes = [vp]
@@ -643,13 +648,21 @@ class GpuME:
         n = self.lib.svtme_timing_read(self.ctx, ms)
         return int(n), [float(v) for v in ms]
 
-    def submit_batch_device(self, jobs, d_records, d_sb=None):
-        """One launch per stage over several jobs (device outputs, asynchronous)."""
+    def submit_batch_device(self, jobs, d_records, d_sb=None, lane=None):
+        """One launch per stage over several jobs (device outputs, asynchronous);
+        lane: svtme_submit_batch_device_lane (None: the context stream, lane 0)."""
         n = len(jobs)
         arr = (Job * n)(*jobs)
         recs = (C.c_void_p * n)(*d_records)
         sbs = (C.c_void_p * n)(*d_sb) if d_sb is not None else None
-        self._check(self.lib.svtme_submit_batch_device(self.ctx, arr, n, recs, sbs), "svtme_submit_batch_device")
+        if lane is None:
+            self._check(self.lib.svtme_submit_batch_device(self.ctx, arr, n, recs, sbs), "svtme_submit_batch_device")
+        else:
+            self._check(self.lib.svtme_submit_batch_device_lane(self.ctx, lane, arr, n, recs, sbs),
+                        "svtme_submit_batch_device_lane")
+
+    def lane_stream(self, lane: int) -> int:
+        return self.lib.svtme_lane_stream(self.ctx, lane) or 0
 
     def submit_batch(self, jobs, with_sb_results: bool = True):
         """Batch submission with host outputs (tests): device buffers via torch."""

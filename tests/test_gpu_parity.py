@@ -250,6 +250,57 @@ def test_picture_upload_async(svtme, gpu):
         gpu.release(pn)
 
 
+def test_lanes_parity(svtme, gpu):
+    """svtme_submit_batch_device_lane: batches alternating over the two lanes
+    (own streams and scratch, overlapping on the GPU), banded full-pel jobs
+    (per-lane argmin keys) and fused jobs in flight together, equal the
+    single-lane results; a re-upload of a reference waits for both lanes'
+    readers."""
+    import torch
+
+    S = svtme
+    w, h = 640, 360
+    syn = S.Synth(w, h)
+    frames = {t: syn.frame(t) for t in (6, 7, 8, 9, 10, 13)}
+    for t, f in frames.items():
+        gpu.upload(6000 + t, f)
+    base = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    band = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    band.me_sa.sa_min.width = band.me_sa.sa_min.height = 64
+    band.me_sa.sa_max.width = band.me_sa.sa_max.height = 64
+    band.me_8x8_var_enabled = 0
+    band.enable_me_sr_adjustment = 0
+    jobs = [S.make_job(w, h, base, 6008, (6007, 6006), (6009, 6010), temporal_layer_index=1),
+            S.make_job(w, h, band, 6008, (6007,), (), temporal_layer_index=1),
+            S.make_job(w, h, base, 6009, (6008, 6007), (6010,), temporal_layer_index=1, ref_count_used=(2, 1))]
+    n = S.sb_total(w, h)
+    ref = [gpu.submit(j)[0] for j in jobs]  # single lane, synchronous
+
+    def buf(j):
+        return torch.zeros(n * S.ref_slots(j) * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    outs = []
+    for it in range(6):
+        for k, j in enumerate(jobs):
+            b = buf(j)
+            gpu.submit_batch_device([j], [b.data_ptr()], lane=(it + k) & 1)
+            outs.append((k, b))
+    # re-upload ref 6007 asynchronously while both lanes may still read it, then search again
+    gpu.upload_async(6007, frames[13])
+    after = buf(jobs[0])
+    gpu.submit_batch_device([jobs[0]], [after.data_ptr()], lane=1)
+    gpu.sync()
+    for k, b in outs:
+        got = np.frombuffer(b.cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n, -1)
+        assert not S.compare_records(ref[k], got), k
+    gpu.upload(6007, frames[13])
+    want = gpu.submit(jobs[0])[0]
+    got = np.frombuffer(after.cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n, -1)
+    assert not S.compare_records(want, got)
+    assert S.compare_records(ref[0], got)  # the new reference changed the result
+    for t in frames:
+        gpu.release(6000 + t)
+
+
 def test_picture_invalidate(svtme, gpu):
     """svtme_picture_invalidate (TF re-decimation, temporal_filtering.c:3895-3931):
     the resident pyramid is rebuilt from the new planes, jobs queued before it
