@@ -135,6 +135,12 @@ __device__ __forceinline__ uint32_t dpp_add(uint32_t v) {
     return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, false);
 }
 
+// a + DPP-permuted b in one VALU op
+template <int CTRL, int RM = 0xF>
+__device__ __forceinline__ uint32_t dpp_add2(uint32_t a, uint32_t b) {
+    return a + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, CTRL, RM, 0xF, false);
+}
+
 // ----------------------------------------------------------------------------
 // Search-area derivations (restated per reference function; pure)
 // ----------------------------------------------------------------------------

@@ -2134,27 +2134,24 @@ struct PuMin {
                 b8 = min_u32((uint32_t)b8, ((e & 1) ? (v & 0xFFFF0000u) : (v << 16)) | (o0 + e));
             }
         }
-        const uint32_t La = dpp_add<0x4E>(dpp_add<0xB1>(la)), Ha = dpp_add<0x4E>(dpp_add<0xB1>(ha));
-        const uint32_t Lb = dpp_add<0x4E>(dpp_add<0xB1>(lb)), Hb = dpp_add<0x4E>(dpp_add<0xB1>(hb));
-        const uint32_t sel = (uint32_t)(g & 1) * 16;
-        const uint32_t s16a = (((g & 2) ? Ha : La) >> sel) & 0xFFFFu;
-        const uint32_t s16b = (((g & 2) ? Hb : Lb) >> sel) & 0xFFFFu;
+        // 16x16 by reduce-scatter over the 4 lanes of a group: lanes with g & 2 keep
+        // the pair of positions 2, 3 and send 0, 1 (quad_perm xor 2), then both
+        // halves of the pair are summed over xor 1; lane g takes position g
+        const bool hi2 = (g & 2) != 0;
+        const uint32_t A = dpp_add2<0x4E>(hi2 ? ha : la, hi2 ? la : ha);
+        const uint32_t B = dpp_add2<0x4E>(hi2 ? hb : lb, hi2 ? lb : hb);
+        const uint32_t sel  = (uint32_t)(g & 1) * 16;
+        const uint32_t s16a = (dpp_add<0xB1>(A) >> sel) & 0xFFFFu;
+        const uint32_t s16b = (dpp_add<0xB1>(B) >> sel) & 0xFFFFu;
         const uint32_t s32a = dpp_add<0x128>(dpp_add<0x124>(s16a)); // row_ror 4, 8: same g
         const uint32_t s32b = dpp_add<0x128>(dpp_add<0x124>(s16b));
-        // 64x64: rows 2j, 2j + 1 of the swap hold one quad's quadrants 2j + 1 and
-        // 2j, which quad is qb; the permlane32_swap of the sum with itself adds
-        // the other row pair
-        const auto p16     = __builtin_amdgcn_permlane16_swap(s32a, s32b, false, false);
-        const uint32_t t   = p16[0] + p16[1];
-        const auto p32     = __builtin_amdgcn_permlane32_swap(t, t, false, false);
-        const uint32_t s64 = p32[0] + p32[1];
         const uint32_t oa = o0 + (uint32_t)g, ob = oa + 4, o64 = oa + 4 * qb;
+        const int xa = x0 + g, xb = xa + 4;
+        // the 16x16 / 32x32 keys before the swap below consumes s32a / s32b
         if (INNER) {
             b16 = min_u32(min_u32((uint32_t)b16, (s16a << 12) | oa), (s16b << 12) | ob);
             b32 = min_u32(min_u32((uint32_t)b32, (s32a << 12) | oa), (s32b << 12) | ob);
-            b64 = min_u32((uint32_t)b64, (s64 << 12) | o64);
         } else {
-            const int xa = x0 + g, xb = xa + 4, x64 = xa + 4 * (int)qb;
             if (xa >= 0 && xa < w) {
                 b16 = min_u32((uint32_t)b16, (s16a << 12) | oa);
                 b32 = min_u32((uint32_t)b32, (s32a << 12) | oa);
@@ -2163,6 +2160,18 @@ struct PuMin {
                 b16 = min_u32((uint32_t)b16, (s16b << 12) | ob);
                 b32 = min_u32((uint32_t)b32, (s32b << 12) | ob);
             }
+        }
+        // 64x64: rows 2j, 2j + 1 of the swap hold one quad's quadrants 2j + 1 and
+        // 2j, which quad is qb; the permlane32_swap of the sum with itself adds
+        // the other row pair
+        const auto p16     = __builtin_amdgcn_permlane16_swap(s32a, s32b, false, false);
+        const uint32_t t   = p16[0] + p16[1];
+        const auto p32     = __builtin_amdgcn_permlane32_swap(t, t, false, false);
+        const uint32_t s64 = p32[0] + p32[1];
+        if (INNER) {
+            b64 = min_u32((uint32_t)b64, (s64 << 12) | o64);
+        } else {
+            const int x64 = xa + 4 * (int)qb;
             if (x64 >= 0 && x64 < w)
                 b64 = min_u32((uint32_t)b64, (s64 << 12) | o64);
         }
