@@ -1110,6 +1110,7 @@ struct HSrch {             // one 1/16-resolution search (pre-HME region or HME-
     uint32_t ncm;          // magic_u32(ncols): tile index / ncols by multiply-high
     uint8_t sh, skip, id;  // byte offset of position 0; odd rows only; ARes index
     uint8_t need;          // bit of HmeSh::need (slot * 2 + (L0 ? 1 : 0))
+    uint8_t tt;            // position rows per tile: HT16, or 2 (the HME-L0 group, see k_hme A1)
 };
 struct HSrch1 {            // one HME-L1 refinement search
     const uint8_t *a0;
@@ -2638,6 +2639,7 @@ struct HmeA { // state of phases A0 .. B
     uint32_t need;                     // bit slot * 2: pre-HME searched, slot * 2 + 1: HME-L0 searched
     HSrch srch[48];
     int32_t nsrch, nitems;
+    int32_t nitems3, base2; // end of the HT16-row tiles; first item of the 2-row group (64-aligned)
     unsigned long long key1[32];
     int16_t x1o[32], y1o[32];
     HSrch1 s1[32];
@@ -2709,8 +2711,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         const int s = lane / 6, k = lane - 6 * (lane / 6), l = s >> 2;
         const bool on = lane < 48 && slot_valid(vmask, s) && tl_or_l0(job, l) &&
                         (k < 2 ? c.prehme_enable != 0 : (c.enable_hme_flag && c.enable_hme_level0_flag));
-        bool mk   = false;
-        int items = 0;
+        bool mk    = false;
+        int items3 = 0, items2 = 0;
         HSrch e;
         if (on) {
             const DevPlane &P = dj.ref[l][s & 3].lv[2];
@@ -2745,27 +2747,46 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                     e.cnt0  = (int16_t)nrows;
                     e.cnt1  = 0;
                     e.ylast = (int16_t)(2 * nrows - 1 + 2 * (kh - 1));
-                    items   = e.ncols * ((nrows + HT16 - 1) / HT16);
+                    items3  = e.ncols * ((nrows + HT16 - 1) / HT16);
+                    items2  = e.ncols * ((nrows + 1) / 2);
                 } else {
                     e.cnt0  = (int16_t)((nrows + 1) >> 1);
                     e.cnt1  = (int16_t)(nrows >> 1);
                     e.ylast = (int16_t)(nrows - 1 + 2 * (kh - 1));
-                    items   = e.ncols * 2 * ((e.cnt0 + HT16 - 1) / HT16);
+                    items3  = e.ncols * 2 * ((e.cnt0 + HT16 - 1) / HT16);
+                    items2  = e.ncols * 2 * ((e.cnt0 + 1) / 2);
                 }
                 mk = true;
             }
         }
-        int tot;
-        const int kpos = wave_compact(mk, &tot);
-        const int incl = wave_incl_scan(items);
+        // Tile shapes: a wavefront's qsad count is its tiles' row count x 64 lanes, so
+        // the HME-L0 quadrants (few rows per parity, e.g. 2 at p8, wasting a third of
+        // a 3-row tile) take 2-row tiles in wavefronts of their own when that needs
+        // fewer wavefront-rows: the 3-row group first, the 2-row group from the next
+        // multiple of 64 items
+        const bool l0    = k >= 2;
+        const int n3_pre = (int)wave_sum_u32(mk && !l0 ? (uint32_t)items3 : 0u);
+        const int n3_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items3 : 0u);
+        const int n2_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items2 : 0u);
+        const bool split = ((n3_pre + 63) / 64) * HT16 + ((n2_l0 + 63) / 64) * 2 < ((n3_pre + n3_l0 + 63) / 64) * HT16;
+        const bool t2    = mk && split && l0;
+        const int items  = t2 ? items2 : items3;
+        e.tt             = (uint8_t)(t2 ? 2 : HT16);
+        int n3s, n2s;
+        const int k3 = wave_compact(mk && !t2, &n3s), k2 = wave_compact(t2, &n2s);
+        const int i3 = wave_incl_scan(mk && !t2 ? items : 0), i2 = wave_incl_scan(t2 ? items : 0);
+        const int N3 = (int)lane63((uint32_t)i3), N2 = (int)lane63((uint32_t)i2);
+        const int base2 = (N3 + 63) & ~63;
         if (mk) {
-            e.item0       = incl - items;
-            sh.u.a.srch[kpos] = e;
+            e.item0                          = t2 ? base2 + i2 - items : i3 - items;
+            sh.u.a.srch[t2 ? n3s + k2 : k3] = e;
         }
-        if (lane == 63)
-            sh.u.a.nitems = incl;
-        if (lane == 0)
-            sh.u.a.nsrch = tot;
+        if (lane == 0) {
+            sh.u.a.nsrch   = n3s + n2s;
+            sh.u.a.nitems3 = N3;
+            sh.u.a.base2   = base2;
+            sh.u.a.nitems  = N2 ? base2 + N2 : N3;
+        }
     } else {
         if (zz_on) {
             const int r = lane >> 1, h = lane & 1; // sub row r, half row h
@@ -2846,28 +2867,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         const int nitems = sh.u.a.nitems, nsrch = sh.u.a.nsrch;
         const uint32_t need = sh.u.a.need;
         const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
+        const int nitems3 = sh.u.a.nitems3, base2 = sh.u.a.base2;
         auto tiles = [&](auto fullk) {
             for (int it = tid; it < nitems; it += 256) {
+                if (it >= nitems3 && it < base2)
+                    continue; // the padding before the 2-row group
                 const HSrch &e = sh.u.a.srch[find_search(sh.u.a.srch, nsrch, it)];
                 if (!((need >> e.need) & 1u))
                     continue;
                 const int local = it - e.item0;
                 const int rt = mdiv(local, e.ncm), col = local - rt * e.ncols;
-                int yf, tv;
-                if (e.skip) {
-                    yf = 2 * HT16 * rt + 1;
-                    tv = min(HT16, e.cnt0 - HT16 * rt);
-                } else {
-                    const int p = rt & 1, i = rt >> 1;
-                    yf = 2 * HT16 * i + p;
-                    tv = min(HT16, (p ? e.cnt1 : e.cnt0) - HT16 * i);
-                }
-                if (tv <= 0)
-                    continue;
-                const unsigned long long kk = hme_tile16<HT16, decltype(fullk)::value>(
-                    e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
-                if (kk != ~0ull)
-                    atomicMin(&sh.u.a.key[e.id], kk);
+                // the wavefront's tiles all have e.tt rows (the groups are 64-aligned)
+                auto run = [&](auto TT) {
+                    constexpr int T = decltype(TT)::value;
+                    int yf, tv;
+                    if (e.skip) {
+                        yf = 2 * T * rt + 1;
+                        tv = min(T, e.cnt0 - T * rt);
+                    } else {
+                        const int p = rt & 1, i = rt >> 1;
+                        yf = 2 * T * i + p;
+                        tv = min(T, (p ? e.cnt1 : e.cnt0) - T * i);
+                    }
+                    if (tv <= 0)
+                        return;
+                    const unsigned long long kk = hme_tile16<T, decltype(fullk)::value>(
+                        e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
+                    if (kk != ~0ull)
+                        atomicMin(&sh.u.a.key[e.id], kk);
+                };
+                if (UNI(it >= base2))
+                    run(std::integral_constant<int, 2>());
+                else
+                    run(std::integral_constant<int, HT16>());
             }
         };
         tiles(std::false_type()); // (a kh == 8 specialisation spills: the scheduler hoists every row)
