@@ -2177,6 +2177,19 @@ struct PuMin {
                 b64 = min_u32((uint32_t)b64, (s64 << 12) | o64);
         }
     }
+    // K32: the 8x8-variance centre probe (order 0): this lane's raw 8x8 SAD; every
+    // lane class takes the position, so no finalize() is needed before the search
+    __device__ __forceinline__ void add_probe(uint32_t s8) {
+        const uint32_t s16 = dpp_add<0x4E>(dpp_add<0xB1>(s8));
+        const uint32_t s32 = dpp_add<0x128>(dpp_add<0x124>(s16));
+        b8  = min_u32((uint32_t)b8, s8 << 16);
+        b16 = min_u32((uint32_t)b16, s16 << 12);
+        b32 = min_u32((uint32_t)b32, s32 << 12);
+        const auto p16     = __builtin_amdgcn_permlane16_swap(s32, s32, false, false);
+        const uint32_t t   = p16[0] + p16[1];
+        const auto p32     = __builtin_amdgcn_permlane32_swap(t, t, false, false);
+        b64 = min_u32((uint32_t)b64, (p32[0] + p32[1]) << 12);
+    }
     // the quad of every lane's 64x64 sums in add_quads (the rows permlane16_swap
     // takes from its second operand)
     __device__ __forceinline__ static uint32_t quad_b_rows() {
@@ -2351,6 +2364,31 @@ __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint8_t *g, int 
 
 
 
+// The 8x8-variance probe of fp_slot (K32): this lane's raw 8x8 SAD at window
+// position 0 (dword-aligned buffer loads realigned by v_alignbyte) into M;
+// returns it as the reference counts it (SUB: doubled)
+template <bool SUB>
+__device__ __forceinline__ uint32_t fp_probe32(PuMin<true> &M, const uint8_t *g, int sdw,
+                                               const uint32_t (&src)[SUB ? 4 : 8][2], int by, int bx) {
+    constexpr int ROWS = SUB ? 4 : 8, RSTEP = SUB ? 2 : 1;
+    g         = uni_ptr(g);
+    sdw       = UNI(sdw);
+    const int sh = (int)((uintptr_t)g & 3);
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(g - sh);
+    const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2) * 4u;
+    u32x4a4 d[ROWS];
+#pragma unroll
+    for (int rr = 0; rr < ROWS; rr++) d[rr] = bld4(rs, lo, (uint32_t)(rr * RSTEP * sdw) * 4u);
+    uint32_t s8 = 0;
+#pragma unroll
+    for (int rr = 0; rr < ROWS; rr++) {
+        s8 = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d[rr].y, d[rr].x, (uint32_t)sh), src[rr][0], s8);
+        s8 = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d[rr].z, d[rr].y, (uint32_t)sh), src[rr][1], s8);
+    }
+    M.add_probe(s8);
+    return SUB ? s8 << 1 : s8;
+}
+
 // integer_search_b64 of one reference slot s by one wavefront (motion_estimation.c:
 // 1249-1516): search area, check_00_center, the 8x8-variance centre probe and
 // the full-pel search of search rows [h * part / parts, h * (part + 1) / parts);
@@ -2424,13 +2462,16 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     if (probe) {
         const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc);
         const int sh     = (int)((uintptr_t)g & 3);
-        if constexpr (K32)
-            fp_rows32<SUB>(M, g, P.stride >> 2, 1, 0, 1, 0u, src, by, bx);
-        else
+        uint32_t p8, p64;
+        if constexpr (K32) {
+            p8  = fp_probe32<SUB>(M, g, P.stride >> 2, src, by, bx);
+            p64 = wave_sum_u32(p8); // the 64x64 SAD at the centre
+        } else {
             fp_rows<SUB, K32, 1>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
-        M.finalize();
-        const uint32_t p8   = (uint32_t)(PuMin<K32>::template out<SUB>(M.b8, true) >> 32);
-        const uint32_t p64  = rl32((uint32_t)(PuMin<K32>::template out<SUB>(M.b64, false) >> 32), 63);
+            M.finalize();
+            p8  = (uint32_t)(PuMin<K32>::template out<SUB>(M.b8, true) >> 32);
+            p64 = rl32((uint32_t)(PuMin<K32>::template out<SUB>(M.b64, false) >> 32), 63);
+        }
         const uint32_t mean = p64 / 64;
         const int32_t diff  = (int32_t)p8 - (int32_t)mean;
         const uint32_t var  = wave_sum_u32((uint32_t)(diff * diff)) / 64;
