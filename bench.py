@@ -12,9 +12,14 @@ pictures (the encoder keeps several look-ahead pictures' ME in flight; the
 north star's C host batches whole pictures), each split into N equal SB
 chunks (SBs are independent given the picture controls); rank
 r searches chunk r of every picture in ONE launch (svtme_submit_batch_device),
-then the ranks all-gather their record chunks over RCCL (one
-all_gather_into_tensor per step, device buffers, on a communication stream
-overlapped with the next step's ME). Per-GPU work is four pictures' worth of
+then each picture's chunks go to the rank that owns it (rank j owns pictures
+4j..4j+3: the process whose picture-level consumers read every SB of them) in
+one all_to_all_single per step over RCCL (device buffers, on a communication
+stream overlapped with the next step's ME): 4 (N-1)/N pictures' records per
+rank per step. --exchange allgather gives every rank every picture instead
+(SURVEY.md 8(e)'s all_gather_into_tensor; N x the bytes per rank, the 8K
+single-picture band split's exchange, and the fallback when the pictures of
+a step do not divide over the ranks). Per-GPU work is four pictures' worth of
 SBs at every N: "scaling" is weak. value = SBs of all pictures / max-over-ranks
 wall time. "overlapped" reports one picture per GPU per step with consecutive
 steps alternating the library's two submission lanes (own streams and
@@ -122,6 +127,9 @@ def main():
     ap.add_argument("--lanes", type=int, default=1, choices=(1, 2),
                     help="submission lanes the timed steps alternate over (svtme_submit_batch_device_lane); the "
                          "overlapped two-lane rate is reported beside the one-lane value")
+    ap.add_argument("--exchange", default="owner", choices=("owner", "allgather"),
+                    help="N > 1 record exchange: each picture's chunks to its owner rank (all_to_all_single), or "
+                         "every picture to every rank (all_gather_into_tensor)")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="target CPU-seconds of the baseline sample")
     args = ap.parse_args()
 
@@ -167,8 +175,11 @@ def main():
     dev = torch.device("cuda", local_rank)
     PM = max(P, P_alt)
     local = [torch.zeros(PM * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-    gathered = [torch.empty(world * PM * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)] \
-        if world > 1 else None
+    # the owner exchange needs each step's pictures to divide over the ranks
+    owner = world > 1 and args.exchange == "owner" and P % world == 0 and P_alt % world == 0
+    exchange = None if world == 1 else ("owner (all_to_all_single)" if owner else "allgather (all_gather_into_tensor)")
+    gathered = [torch.empty((1 if owner else world) * PM * chunk_bytes, dtype=torch.uint8, device=dev)
+                for _ in range(2)] if world > 1 else None
     NL = args.lanes
     exts = [torch.cuda.ExternalStream(gpu.lane_stream(l), device=dev) for l in range(2)]
     ext = exts[0]
@@ -189,7 +200,11 @@ def main():
         if world > 1:
             me_done[b].record(es)
             comm.wait_event(me_done[b])
-            D.gather_chunks_device(local[b], gathered[b], dist, stream=comm)
+            if owner:  # this step's n_pic chunks: n_pic / world pictures per owner
+                D.exchange_to_owners_device(local[b][:n_pic * chunk_bytes], gathered[b][:n_pic * chunk_bytes], dist,
+                                            stream=comm)
+            else:
+                D.gather_chunks_device(local[b], gathered[b], dist, stream=comm)
             g_done[b].record(comm)
         used[b] = True
 
@@ -366,7 +381,7 @@ def main():
                        "parallelism": f"{world} GPU(s): each picture split in {world} equal SB chunks, "
                                       f"rank r searches chunk r of all {P} pictures in one launch per step" +
                                       (", consecutive steps on alternating submission lanes" if NL > 1 else "") +
-                                      (", RCCL all-gather of the record chunks" if world > 1 else "")},
+                                      (f", record exchange over RCCL: {exchange}" if world > 1 else "")},
             "overlapped": None if alt_ms is None else {
                 "pictures_per_step": P_alt, "lanes": 2, "ms_per_step": round(alt_ms, 4),
                 "value": round(n_sb * P_alt / (alt_ms * 1e-3), 1),

@@ -1,18 +1,17 @@
 """Multi-GPU orchestration of the open-loop ME path (one process per GPU).
 
-Two ways to spread ME over ranks, neither needs a collective on the data path:
+Two ways to spread ME over ranks:
 
-* picture-parallel (weak scaling, what bench.py measures): every rank runs
-  whole pictures of its own; the only exchange is the optional all-gather of
-  the per-SB records (the encoder's picture-level consumers, me_process.c:
-  274-288, read every SB's results).
+* picture-parallel: every rank runs whole pictures of its own; no exchange.
 * band-parallel (one picture split in SB bands): rank k runs
   SBs [begin_k, begin_k + count_k) of the same picture (svtme_job.sb_begin /
   sb_count) against the same resident references; the bands concatenate to
   the whole picture's records, bit-identical to a single-rank run. On GPUs the
   SB count is padded to equal chunks (sb_chunk) so one all_gather_into_tensor
   over RCCL moves every rank's record slice straight between device buffers
-  (gather_chunks_device); this is the analogue of the reference's ME segments
+  (gather_chunks_device), or, with several pictures per step, one
+  all_to_all_single hands each picture's chunks to the rank that owns it
+  (exchange_to_owners_device); this is the analogue of the reference's ME segments
   -> SB ranges (enc_handle.c:393-412, me_process.c:146-157).
 
 `torch.distributed` is plumbing here (RCCL on GPUs, gloo for the CPU tests).
@@ -59,6 +58,40 @@ def gather_chunks_device(d_local, d_out, dist, group=None, stream=None):
     else:
         dist.all_gather_into_tensor(d_out, d_local, group=group)
     return d_out
+
+
+def owner_of(picture: int, pictures_per_rank: int) -> int:
+    """Rank that assembles `picture` (of a step's world x pictures_per_rank
+    pictures, numbered so that each rank's pictures are contiguous)."""
+    return picture // pictures_per_rank
+
+
+def exchange_to_owners_device(d_local, d_out, dist, group=None, stream=None):
+    """Send each picture's record chunk to the rank that owns the picture.
+
+    A step has world x k pictures; rank j owns pictures [j k, (j + 1) k) (the
+    encoder process whose picture-level consumers read every SB's records of
+    that picture, me_process.c:274-288). d_local: uint8 tensor of world x k
+    chunks (this rank's chunk of every picture, picture-major); d_out: the same
+    size, chunk i of owned picture q at d_out[(i k + q) chunk : ...]
+    (owned_picture_records reassembles it). One all_to_all_single over RCCL:
+    each rank moves (world - 1) / world of k pictures' records instead of the
+    (world - 1) x world x k chunks an all-gather moves to every rank."""
+    import torch
+
+    if stream is not None:
+        with torch.cuda.stream(stream):
+            dist.all_to_all_single(d_out, d_local, group=group)
+    else:
+        dist.all_to_all_single(d_out, d_local, group=group)
+    return d_out
+
+
+def owned_picture_records(d_out, world: int, pictures_per_rank: int, q: int, n_bytes: int):
+    """The records (first n_bytes: n_sb x R x record bytes, raster SB order) of
+    this rank's q-th owned picture out of exchange_to_owners_device's buffer."""
+    chunk = d_out.numel() // (world * pictures_per_rank)
+    return d_out.view(world, pictures_per_rank, chunk)[:, q, :].reshape(-1)[:n_bytes]
 
 
 def gather_band_records(local: np.ndarray, n_sb: int, dist, group=None) -> np.ndarray:

@@ -137,3 +137,60 @@ def test_sb_chunk_padding():
                 assert 0 <= c <= slots and b == min(k * slots, n)
                 cov.extend(range(b, b + c))
             assert cov == list(range(n))
+
+
+def _owner_worker(rank, world, port, out_path, k):
+    """bench.py's default N > 1 exchange on CPU: world x k pictures per step,
+    every rank searches its equal SB chunk of each, one all_to_all_single
+    hands each picture's chunks to its owner rank (k pictures per rank)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "svt-av1-mirror_amd"))
+    import torch
+    import torch.distributed as dist
+
+    import svtme as S
+    import svtme_dist as D
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w, h = 200, 136
+    n_sb = S.sb_total(w, h)
+    slots = D.chunk_slots(n_sb, world)
+    R = 3
+    rec_bytes = S.REF_RECORD_DTYPE.itemsize * R
+    chunk = slots * rec_bytes
+    n_pics = world * k
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    begin, count = D.sb_chunk(n_sb, rank, world)
+    local = torch.zeros(n_pics * chunk, dtype=torch.uint8)
+    for p in range(n_pics):
+        if count:
+            recs, _ = S.run_case_checker("pan", w, h, ctrl, 8 + p, (7 + p, 6 + p), (9 + p,), 1, checker="oracle",
+                                         nthreads=1, sb_begin=begin, sb_count=count)
+            local[p * chunk: p * chunk + count * rec_bytes] = torch.from_numpy(recs.view(np.uint8).reshape(-1).copy())
+    out = torch.empty_like(local)
+    D.exchange_to_owners_device(local, out, dist)
+    for q in range(k):
+        p = rank * k + q
+        assert D.owner_of(p, k) == rank
+        got = D.owned_picture_records(out, world, k, q, n_sb * rec_bytes)
+        np.save(f"{out_path}.{p}.npy", got.numpy().copy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,k", [(2, 2), (3, 1)])
+def test_owner_exchange_equals_single_rank(svtme, tmp_path, world, k):
+    S = svtme
+    out = str(tmp_path / "owned")
+    mp.spawn(_owner_worker, args=(world, _free_port(), out, k), nprocs=world, join=True)
+    w, h = 200, 136
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    for p in range(world * k):
+        ref, _ = S.run_case_checker("pan", w, h, ctrl, 8 + p, (7 + p, 6 + p), (9 + p,), 1, checker="oracle",
+                                    nthreads=2)
+        full = np.load(f"{out}.{p}.npy").view(S.REF_RECORD_DTYPE).reshape(ref.shape)
+        assert not S.compare_records(ref, full)
