@@ -1121,13 +1121,17 @@ struct HSrch1 {            // one HME-L1 refinement search
 };
 
 
-// rows of one 1/16 tile row: 8 dwords from quad q0 (two dword-aligned 16-byte loads)
+// rows of one 1/16 tile row: the HQ16 + 4 = 6 dwords from quad q0 its position
+// quads read (dword-aligned 16- and 8-byte loads)
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
 struct Row8 {
-    u32x4a4 lo, hi;
+    u32x4a4 lo;
+    u32x2a4 hi;
 };
 __device__ __forceinline__ Row8 row8(const uint8_t *a0, int stride, int ro, int q0) {
+    typedef __attribute__((address_space(1))) const u32x2a4 gu2;
     const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)ro * stride) + q0;
-    return Row8{ldg4(rp), ldg4(rp + 4)};
+    return Row8{ldg4(rp), *(gu2 *)(uintptr_t)(rp + 4)};
 }
 
 // SADs of the 16 x kh (sub) source block sr at a T x HQ tile of positions of
@@ -1153,7 +1157,8 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
         if (m + 2 < NR)
             buf[(m + 2) % 3] = row8(a0, stride, min(yf + 2 * (m + 2), ylast), q0);
         const Row8 &R = buf[m % 3];
-        const uint32_t d[8] = {R.lo.x, R.lo.y, R.lo.z, R.lo.w, R.hi.x, R.hi.y, R.hi.z, R.hi.w};
+        static_assert(HQ16 + 4 == 6, "Row8 holds 6 dwords");
+        const uint32_t d[6] = {R.lo.x, R.lo.y, R.lo.z, R.lo.w, R.hi.x, R.hi.y};
         unsigned long long P[HQ16 + 3];
 #pragma unroll
         for (int j = 0; j < HQ16 + 3; j++) P[j] = pair(d[j], d[j + 1]);
@@ -1179,6 +1184,10 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
             xo[qq][e]   = (x >= 0 && x < sa_w) ? (uint32_t)x : U32MAX;
         }
     unsigned long long best = ~0ull;
+    // the key rows from a fresh copy of yf: CSE with the row addresses above keeps
+    // yf + 2t live through the loop (a spill at 64 VGPRs)
+    uint32_t yk = (uint32_t)yf;
+    asm volatile("" : "+v"(yk));
 #pragma unroll
     for (int t = 0; t < T; t++) {
         uint32_t mt = U32MAX;
@@ -1191,7 +1200,7 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
         }
         if (t < tv && mt != U32MAX) {
             const unsigned long long kk = ((unsigned long long)(mt >> 16) << 32) |
-                                          ((unsigned long long)(uint32_t)(yf + 2 * t) << 16) | (mt & 0xFFFFu);
+                                          ((unsigned long long)(yk + 2 * t) << 16) | (mt & 0xFFFFu);
             best = kk < best ? kk : best;
         }
     }
