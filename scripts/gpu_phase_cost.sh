@@ -4,7 +4,7 @@
 cd "$GRAFT_REPO_ROOT"
 WL=${WL:-4k_p8}; P=${P:-4}
 mkdir -p gpurun_out
-for k in ${KS:-1 2 3 4 5 6 full}; do
+for k in ${KS:-1 2 3 4 5 55 6 full}; do
   lib=svt-av1-mirror_amd/libsvtme_stop$k.so
   [ "$k" = full ] && lib=svt-av1-mirror_amd/libsvtme.so
   SVTME_LIB=$lib timeout -k 10 120 python3 scripts/phase_cost.py $WL $P stop_after_$k || exit 1

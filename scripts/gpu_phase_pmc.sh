@@ -6,7 +6,7 @@ WL=${WL:-4k_p8}; P=${P:-1}
 O=gpurun_out/phase_pmc
 mkdir -p $O
 export TMPDIR=/tmp
-for k in ${KS:-1 2 3 4 5 6 full}; do
+for k in ${KS:-1 2 3 4 5 55 6 full}; do
   lib=svt-av1-mirror_amd/libsvtme_stop$k.so
   [ "$k" = full ] && lib=svt-av1-mirror_amd/libsvtme.so
   SVTME_LIB=$lib timeout -s KILL 120 rocprofv3 --kernel-trace --kernel-include-regex "k_hme" \
