@@ -339,7 +339,10 @@ __device__ __forceinline__ void key_result(unsigned long long k, uint32_t *best,
 // n x m SAD (compute_sad_c.c:20-37) of a width x rows block, by one wavefront;
 // ref may be unaligned, cur is dword aligned
 __device__ uint32_t wave_nxm(const uint8_t *ref, int rstride, const uint8_t *cur, int cstride, int rows, int width) {
-    const int lane     = threadIdx.x & 63;
+    // an opaque lane index: the per-lane addresses below are not hoisted out of a
+    // caller's loop (live across it, they spill at 64 VGPRs)
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
     const int wd4      = (width + 3) >> 2;
     const uint32_t mwd = magic_u32((uint32_t)wd4);
     const int sh       = (int)((uintptr_t)ref & 3);
@@ -3171,14 +3174,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         const int z16 = lane >> 2, k4 = lane & 3;
         const int by  = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
         const int bx  = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
+        // this lane's 8x8 source block: buffer loads from the SB origin (a 32-bit
+        // lane offset; 64-bit per-lane row pointers hoisted out of this loop spill)
         const DevPlane &C = gj.cur.lv[0];
+        const int cst     = UNI(C.stride);
+        const __amdgpu_buffer_rsrc_t crs = plane_rsrc(uni_ptr(C.base + (ptrdiff_t)G.oy * cst + G.ox));
+        const uint32_t coff = (uint32_t)(by * 8 * cst + bx * 8);
         uint32_t src[ROWS][2];
 #pragma unroll
         for (int rr = 0; rr < ROWS; rr++) {
-            const uint32_t *sp =
-                (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + by * 8 + rr * RSTEP) * C.stride + G.ox + bx * 8);
-            src[rr][0] = sp[0];
-            src[rr][1] = sp[1];
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(crs, (int)coff, rr * RSTEP * cst, 0);
+            src[rr][0] = v[0];
+            src[rr][1] = v[1];
         }
         const int s         = k < gj.job.num_refs[0] ? k : 4 + (k - gj.job.num_refs[0]);
         const SlotCentre &v = sh.cen[s];
