@@ -1220,31 +1220,45 @@ template <bool FULLK = false> // FULLK: a full-height SB (kh1 == 16), no row che
 __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                           int y, int kh1, const uint8_t (*src)[32]) {
     const int g = threadIdx.x & 3;
-    auto ld = [&](int kk, u32x4a4 (&L)[3]) {
+    // the HQ1 + 9 = 11 dwords a row's quads read: 16 + 16 + 12 bytes
+    static_assert(HQ1 + 9 == 11, "L1 rows hold 11 dwords");
+    typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
+    typedef __attribute__((address_space(1))) const u32x3a4 gu3;
+    struct Row11 {
+        u32x4a4 a, b;
+        u32x3a4 c;
+    };
+    auto ld = [&](int kk, Row11 &L) {
         const int k        = min(4 * g + kk, 15);
         const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)(y + 2 * k) * stride) + q0;
-        L[0] = ldg4(rp), L[1] = ldg4(rp + 4), L[2] = ldg4(rp + 8);
+        L.a = ldg4(rp), L.b = ldg4(rp + 4), L.c = *(gu3 *)(uintptr_t)(rp + 8);
     };
-    u32x4a4 L[2][3];
+    Row11 L[2];
     ld(0, L[0]);
     unsigned long long acc[HQ1] = {};
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) {
         if (kk + 1 < 4)
             ld(kk + 1, L[(kk + 1) & 1]);
-        const int k = 4 * g + kk;
-        if (FULLK || k < kh1) {
-            const u32x4a4 *R = L[kk & 1];
+        // every row is summed and rows past the block height (a partial SB, a
+        // per-lane test) are dropped by a select: no divergent branch, whose
+        // join would wait for the row prefetched above
+        const int k = min(4 * g + kk, 15);
+        {
+            const Row11 &R = L[kk & 1];
             const uint4 s0 = ((const uint4 *)src[k])[0], s1 = ((const uint4 *)src[k])[1];
             const uint32_t sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-            uint32_t d[12] = {R[0].x, R[0].y, R[0].z, R[0].w, R[1].x, R[1].y,
-                              R[1].z, R[1].w, R[2].x, R[2].y, R[2].z, R[2].w};
+            uint32_t d[11] = {R.a.x, R.a.y, R.a.z, R.a.w, R.b.x, R.b.y, R.b.z, R.b.w, R.c.x, R.c.y, R.c.z};
 #pragma unroll
             for (int j = 0; j < HQ1 + 8; j++) d[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], (uint32_t)sh);
+            const bool use = FULLK || 4 * g + kk < kh1;
 #pragma unroll
-            for (int qq = 0; qq < HQ1; qq++)
+            for (int qq = 0; qq < HQ1; qq++) {
+                unsigned long long a = acc[qq];
 #pragma unroll
-                for (int j = 0; j < 8; j++) acc[qq] = qsad64(pair(d[qq + j], d[qq + j + 1]), sv[j], acc[qq]);
+                for (int j = 0; j < 8; j++) a = qsad64(pair(d[qq + j], d[qq + j + 1]), sv[j], a);
+                acc[qq] = use ? a : acc[qq];
+            }
         }
     }
     uint32_t mt = U32MAX; // sad (< 2^17) << 15 | x (< 2^15)
