@@ -2340,31 +2340,39 @@ __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint8_t *g, int 
         const uint32_t rb = (uint32_t)(ty * sdw + tq) * 4u;
         // dword-aligned loads of TQ + 3 dwords, realigned to position 0 (v_alignbyte)
         constexpr int NX = (TQ + 3) / 4, NR = (TQ + 3) - 4 * NX;
-        uint32_t D[ROWS][TQ + 3];
-#pragma unroll
-        for (int rr = 0; rr < ROWS; rr++) {
-            const uint32_t ro = rb + (uint32_t)(rr * RSTEP * sdw) * 4u;
-#pragma unroll
-            for (int v = 0; v < NX; v++) {
-                const u32x4a4 t = bld4(rs, (lo + 4 * v) * 4u, ro);
-                D[rr][4 * v] = t.x, D[rr][4 * v + 1] = t.y, D[rr][4 * v + 2] = t.z, D[rr][4 * v + 3] = t.w;
-            }
-#pragma unroll
-            for (int v = 0; v < NR; v++)
-                D[rr][4 * NX + v] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)((lo + 4 * NX + v) * 4u), (int)ro, 0);
-#pragma unroll
-            for (int j = 0; j < TQ + 2; j++) D[rr][j] = __builtin_amdgcn_alignbyte(D[rr][j + 1], D[rr][j], (uint32_t)sh);
-        }
+        // rows in batches (2 full rows): the 8 full rows of a non-sub-sampled set would hold
+        // 8 (TQ + 3) dwords beside the 16 of the source and spill at 64 VGPRs
+        constexpr int RB = SUB ? 4 : 2;
         unsigned long long acc[TQ];
 #pragma unroll
         for (int iq = 0; iq < TQ; iq++) acc[iq] = 0;
 #pragma unroll
-        for (int rr = 0; rr < ROWS; rr++)
+        for (int r0 = 0; r0 < ROWS; r0 += RB) {
+            uint32_t D[RB][TQ + 3];
 #pragma unroll
-            for (int iq = 0; iq < TQ; iq++) {
-                acc[iq] = qsad64(pair(D[rr][iq], D[rr][iq + 1]), src[rr][0], acc[iq]);
-                acc[iq] = qsad64(pair(D[rr][iq + 1], D[rr][iq + 2]), src[rr][1], acc[iq]);
+            for (int rr = 0; rr < RB; rr++) {
+                const uint32_t ro = rb + (uint32_t)((r0 + rr) * RSTEP * sdw) * 4u;
+#pragma unroll
+                for (int v = 0; v < NX; v++) {
+                    const u32x4a4 t = bld4(rs, (lo + 4 * v) * 4u, ro);
+                    D[rr][4 * v] = t.x, D[rr][4 * v + 1] = t.y, D[rr][4 * v + 2] = t.z, D[rr][4 * v + 3] = t.w;
+                }
+#pragma unroll
+                for (int v = 0; v < NR; v++)
+                    D[rr][4 * NX + v] =
+                        (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)((lo + 4 * NX + v) * 4u), (int)ro, 0);
+#pragma unroll
+                for (int j = 0; j < TQ + 2; j++)
+                    D[rr][j] = __builtin_amdgcn_alignbyte(D[rr][j + 1], D[rr][j], (uint32_t)sh);
             }
+#pragma unroll
+            for (int rr = 0; rr < RB; rr++)
+#pragma unroll
+                for (int iq = 0; iq < TQ; iq++) {
+                    acc[iq] = qsad64(pair(D[rr][iq], D[rr][iq + 1]), src[r0 + rr][0], acc[iq]);
+                    acc[iq] = qsad64(pair(D[rr][iq + 1], D[rr][iq + 2]), src[r0 + rr][1], acc[iq]);
+                }
+        }
         const int x0      = 4 * tq;
         const uint32_t ob = obase + (uint32_t)(ty * w + x0);
 #pragma unroll
@@ -2856,32 +2864,48 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         }
     } else {
         if (zz_on) {
+            // the wave's slots are wid - 1, wid + 2, wid + 5: the current rows are
+            // loaded once and every slot's reference rows are issued before the first
+            // SAD, so the wave waits for one load round trip instead of one per slot
             const int r = lane >> 1, h = lane & 1; // sub row r, half row h
-            for (int s = wid - 1; s < 8; s += 3) { // wave-uniform slot
-                if (!(slot_valid(vmask, s) && tl_or_l0(job, s >> 2)))
-                    continue;
-                const DevPlane &F = dj.ref[s >> 2][s & 3].lv[0];
-                const DevPlane &C = dj.cur.lv[0];
-                uint32_t acc      = 0;
-                if (r < (int)(G.bh >> 1)) {
+            const bool row_in = r < (int)(G.bh >> 1);
+            const DevPlane &C = dj.cur.lv[0];
+            u32x4a4 b0{}, b1{}, a[3][2];
+            bool sv[3];
+            if (row_in) {
+                const uint32_t *cr = (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox) + 8 * h;
+                b0 = ldg4(cr), b1 = ldg4(cr + 4);
+            }
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const int s = wid - 1 + 3 * j; // wave-uniform slot
+                sv[j]       = s < 8 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2);
+                a[j][0] = a[j][1] = u32x4a4{};
+                if (sv[j] && row_in) {
+                    const DevPlane &F = dj.ref[s >> 2][s & 3].lv[0];
                     const uint32_t *rr =
                         (const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * r) * F.stride + G.ox) + 8 * h;
-                    const uint32_t *cr =
-                        (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox) + 8 * h;
-                    const u32x4a4 a0 = ldg4(rr), a1 = ldg4(rr + 4);
-                    const u32x4a4 b0 = ldg4(cr), b1 = ldg4(cr + 4);
-                    acc = __builtin_amdgcn_sad_u8(a0.x, b0.x, acc);
-                    acc = __builtin_amdgcn_sad_u8(a0.y, b0.y, acc);
-                    acc = __builtin_amdgcn_sad_u8(a0.z, b0.z, acc);
-                    acc = __builtin_amdgcn_sad_u8(a0.w, b0.w, acc);
-                    acc = __builtin_amdgcn_sad_u8(a1.x, b1.x, acc);
-                    acc = __builtin_amdgcn_sad_u8(a1.y, b1.y, acc);
-                    acc = __builtin_amdgcn_sad_u8(a1.z, b1.z, acc);
-                    acc = __builtin_amdgcn_sad_u8(a1.w, b1.w, acc);
+                    a[j][0] = ldg4(rr), a[j][1] = ldg4(rr + 4);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                if (!sv[j])
+                    continue;
+                uint32_t acc = 0;
+                if (row_in) {
+                    acc = __builtin_amdgcn_sad_u8(a[j][0].x, b0.x, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[j][0].y, b0.y, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[j][0].z, b0.z, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[j][0].w, b0.w, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[j][1].x, b1.x, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[j][1].y, b1.y, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[j][1].z, b1.z, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[j][1].w, b1.w, acc);
                 }
                 acc = wave_sum_u32(acc);
                 if (lane == 0)
-                    sh.u.a.zzacc[s] = acc;
+                    sh.u.a.zzacc[wid - 1 + 3 * j] = acc;
             }
         }
         // full-resolution source block (64 x 64, even rows) for HME-L2
