@@ -2475,15 +2475,10 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
         yc = ((org_y + yc) < -pad) ? i16(-pad - org_y) : yc;
         yc = ((org_y + yc) > ph - 1) ? i16(yc - ((org_y + yc) - (ph - 1))) : yc;
         const uint8_t *cb = C.base + (ptrdiff_t)oy * C.stride + ox;
-        // the zero-MV SAD is init_zz_sad's get_zz_sad (:1667-1689, the same sub-sampled
-        // 64x64 SAD << 1) whenever that ran for this slot and the SB is whole (zz is
-        // then not rescaled): one SB-sized SAD per record fewer
         const uint32_t zero_sad =
-            (zz != U32MAX && G.bw == 64 && G.bh == 64)
-                ? zz
-                : wave_nxm(P.base + (ptrdiff_t)oy * P.stride + ox, 2 * P.stride, cb, 2 * C.stride, (int)(G.bh >> 1),
-                           (int)G.bw)
-                      << 1;
+            wave_nxm(P.base + (ptrdiff_t)oy * P.stride + ox, 2 * P.stride, cb, 2 * C.stride, (int)(G.bh >> 1),
+                     (int)G.bw)
+            << 1;
         const uint32_t hme_mv_sad = wave_nxm(P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc),
                                              2 * P.stride, cb, 2 * C.stride, (int)(G.bh >> 1), (int)G.bw)
             << 1;
