@@ -184,7 +184,7 @@ def main():
     gathered = [torch.empty((1 if owner else world) * PM * chunk_bytes, dtype=torch.uint8, device=dev)
                 for _ in range(2)] if world > 1 else None
     NL = args.lanes
-    exts = [torch.cuda.ExternalStream(gpu.lane_stream(l), device=dev) for l in range(2)]
+    exts = [torch.cuda.ExternalStream(gpu.lane_stream(l), device=dev) for l in range(max(2, NL))]
     ext = exts[0]
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
     me_done = [torch.cuda.Event() for _ in range(2)]
@@ -232,9 +232,10 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     join = torch.cuda.Event()
 
-    def end_on_lane0(ev):  # lane 0 waits for the other lane's queue, then records ev
-        join.record(exts[1])
-        ext.wait_event(join)
+    def end_on_lane0(ev):  # lane 0 waits for the other lanes' queues, then records ev
+        for l in range(1, len(exts)):
+            join.record(exts[l])
+            ext.wait_event(join)
         ev.record(ext)
     t0 = time.perf_counter()
     ev0.record(ext)
