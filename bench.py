@@ -114,8 +114,8 @@ def main():
 
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="4k_p8", choices=sorted(W.WORKLOADS))
     ap.add_argument("--pictures", type=int, default=0,
                     help=f"pictures per step (default: {PICTURES_PER_GPU} per GPU; several go in one batched launch)")
