@@ -2743,6 +2743,18 @@ struct HmeSh {
 
 // FP: the whole ME pass of the SB in this workgroup (k_stage_c1 with one band
 // per record, then k_stage_e); else the HME state goes to BState for them.
+// wave 0's serial phases (decisions, search tables, final centre) run at raised
+// issue priority: the workgroup's other waves wait for them at a barrier
+#ifndef HME_PRIO
+#define HME_PRIO 1
+#endif
+#if HME_PRIO
+#define HME_PRIO_HI() __builtin_amdgcn_s_setprio(2)
+#define HME_PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#else
+#define HME_PRIO_HI()
+#define HME_PRIO_LO()
+#endif
 #ifndef HME_WAVES_PER_EU
 #define HME_WAVES_PER_EU 8 // 64 VGPRs: 8 workgroups per CU
 #endif
@@ -2928,6 +2940,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     HME_STAMP(1);
     // ---- zz decisions; which searches the reference performs (wave 0)
     if (wid == 0) {
+        HME_PRIO_HI();
         if (lane < 8)
             d.a[SVTME_A_ZZ + lane] = ARes{sh.u.a.zzacc[lane], 0, 0};
         wave_lds_fence();
@@ -2941,6 +2954,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             sh.u.a.need = (uint32_t)m;
     }
     __syncthreads();
+    HME_PRIO_LO();
     HME_STAMP(2);
     // ---- A1: pre-HME regions and HME-L0 quadrants, one HT16 x HQ tile per thread
     {
@@ -3000,6 +3014,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     // ---- D: pre-HME and level-0 decisions, then the HME-L1 table (wave 0)
     const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH; // true on this path
     if (wid == 0) {
+        HME_PRIO_HI();
         if (lane < SVTME_A_N && lane >= SVTME_A_PH) {
             uint32_t best;
             int x, y;
@@ -3077,6 +3092,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             sh.u.a.nsrch1 = tot;
     }
     __syncthreads();
+    HME_PRIO_LO();
     HME_STAMP(4);
     // ---- B: HME-L1 tiles, 4 lanes (block-row quarters) per tile
     {
@@ -3199,6 +3215,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     // ---- C: set_final_seach_centre_sb / hme_prune_ref_and_adjust_sr once (wave 0), then
     // integer_search_b64 of every record, one wavefront each (k_stage_c1, one band)
     if (wid == 0) {
+        HME_PRIO_HI();
         const SlotCentre scv = final_centre(job, &sh.bs, vmask); // lane = slot
         if (lane < 8)
             sh.cen[lane] = scv;
@@ -3206,6 +3223,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             sh.tf_exit = job.me_type == SVTME_ME_MCTF && scv.hme_sad < job.tf_me_exit_th; // :3109-3113
     }
     __syncthreads();
+    HME_PRIO_LO();
     HME_STOP(55);
     for (int k = wid; k < (int)dj.R; k += 4) {
         constexpr int ROWS = SUB_ME ? 4 : 8, RSTEP = SUB_ME ? 2 : 1;
