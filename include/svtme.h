@@ -302,11 +302,13 @@ svtme_status svtme_submit_batch_device_lane(svtme_ctx *ctx, uint32_t lane, const
 void *svtme_lane_stream(svtme_ctx *ctx, uint32_t lane);
 /* Kernel timing with HIP events on the context's stream, recorded around every
  * stage launch of every submission while enabled (enable = 1). svtme_timing_read
- * waits for the recorded submissions and returns, averaged over them, the
- * milliseconds of stage 0 (k_stage_a: zz / pre-HME / HME-L0), 1 (k_stage_d:
- * their decisions), 2 (k_stage_b: HME-L1/L2), 3 (k_stage_c1, or the per-SB
- * k_stage_c) and 4 (k_stage_e) in stage_ms[0..4]; returns the number of
- * submissions averaged and clears them. */
+ * waits for the recorded launch groups and returns the milliseconds of stage 0
+ * (k_stage_a: zz / pre-HME / HME-L0, or the fused k_hme), 1 (k_stage_d: their
+ * decisions), 2 (k_stage_b: HME-L1/L2), 3 (k_stage_c1, or the per-SB
+ * k_stage_c) and 4 (k_stage_e) in stage_ms[0..4], each averaged over the
+ * launch groups that ran that stage; returns the number of launch groups read
+ * and clears them. At most 256 groups are kept between reads; later ones are
+ * not recorded and the read sets svtme_last_error(). */
 svtme_status svtme_set_timing(svtme_ctx *ctx, int enable);
 uint32_t svtme_timing_read(svtme_ctx *ctx, float stage_ms[5]);
 /* Device pointer of the last job's record buffer (for RCCL all-gather). */

@@ -1,35 +1,56 @@
 /*
  * svtme_svt_glue.c — the encoder-side binding of libsvtme.so into SVT-AV1.
  *
- * This file is meant to be compiled INSIDE the reference encoder (it includes
- * the reference's own headers: pcs.h, me_context.h, me_sb_results.h,
- * reference_object.h, aom_dsp_rtcd.h) and linked with libsvtme.so. It is what
- * INTEGRATION.md describes; tests/test_integration.py compiles it against
- * /root/reference/Source with gcc in the build container.
+ * Compiled INSIDE the reference encoder (it includes the reference's own
+ * headers: pcs.h, me_context.h, me_sb_results.h, reference_object.h,
+ * aom_dsp_rtcd.h) and linked with libsvtme.so. oracle/encoder.mk links it into
+ * the reference encoder built from its unmodified sources, and
+ * tests/test_encoder.py checks that the encoder's bitstream is byte-identical
+ * with and without it.
  *
- *   svt_aom_setup_rtcd_hip()          register the *_hip rtcd variants over the
- *                                     pointers svt_aom_setup_rtcd_internal set
- *                                     (aom_dsp_rtcd.c:188; called after it from
- *                                     svt_av1_enc_init, enc_handle.c:1445). Each
- *                                     wrapper re-runs a call on the variant it
- *                                     replaced when the HIP call failed
- *                                     (svtme_rtcd_failed), so a kernel never
- *                                     fails visibly (SURVEY.md 8(b) Errors).
- *   svtme_controls_from_me_context()  the per-picture ME controls that
- *                                     svt_aom_sig_deriv_me (enc_mode_config.c:671)
- *                                     wrote into a MeContext, as svtme_controls.
- *   svtme_job_from_pcs()              one PA-ME picture job (me_process.c:217-261).
- *   svtme_scatter_sb()                one SB's outputs into MeSbResults and the
- *                                     pcs per-SB arrays (me_sb_results.h:28-44,
- *                                     pcs.h:871-878), exactly where
- *                                     svt_aom_motion_estimation_b64 leaves them.
- *   svtme_me_picture()                the picture-level replacement of the SB loop
- *                                     of me_process.c:172-290 (segments 1x1).
- *   svtme_picture_redecimated()       re-upload after temporal filtering replaced
- *                                     a picture's planes (temporal_filtering.c:
- *                                     3895-3931 pad_and_decimate_filtered_pic).
+ * Picture-job mode (the performance boundary)
+ *   svtme_motion_estimation_b64()  drop-in for svt_aom_motion_estimation_b64
+ *                                  (motion_estimation.c:3076), same signature.
+ *                                  The first call for a picture (PA-ME,
+ *                                  me_process.c:266) or for a (picture,
+ *                                  reference) pair (TF-ME, temporal_filtering.c:
+ *                                  3169) runs ONE job over every SB of the
+ *                                  picture; every call then scatters its SB's
+ *                                  results exactly where the reference function
+ *                                  leaves them. Pictures are uploaded on first
+ *                                  use and re-uploaded after the encoder rebuilds
+ *                                  their 1/4 and 1/16 planes
+ *                                  (svtme_picture_changed). Pictures the job API
+ *                                  does not cover (super-resolution / resize
+ *                                  scaled references, me_process.c:229-246;
+ *                                  the DG detector's HME, me_process.c:115) and
+ *                                  jobs that fail run on the encoder's own SB
+ *                                  function (the fallback).
+ *   Linking with -Wl,--wrap=svt_aom_motion_estimation_b64
+ *   -Wl,--wrap=svt_aom_downsample_filtering_input_picture and
+ *   -DSVTME_GLUE_WRAP routes both call sites of the SB function and every
+ *   re-decimation outside pic_analysis_process.c through this file without
+ *   editing the encoder's sources.
+ *
+ * Parity / debug mode
+ *   svt_aom_setup_rtcd_hip_parity() registers the per-kernel *_hip rtcd variants
+ *                                  over the pointers svt_aom_setup_rtcd_internal
+ *                                  set (aom_dsp_rtcd.c:188). Each call becomes a
+ *                                  synchronous GPU round trip, so this is for
+ *                                  per-kernel parity runs only; picture-job mode
+ *                                  registers nothing and mode decision keeps its
+ *                                  CPU kernels (svt_pme_sad_loop_kernel,
+ *                                  sad_16b_kernel, ...).
+ *
+ * Environment (read once): SVTME_DEVICE (HIP device, default 0);
+ * SVTME_GLUE_STRICT=1 aborts instead of falling back; SVTME_GLUE_VERIFY=1
+ * compares every uploaded pyramid with the encoder's own planes;
+ * SVTME_GLUE_STATS=<file> appends the counters at exit; SVTME_GLUE_RESIDENT
+ * caps the resident pictures (default 64).
  */
+#include <pthread.h>
 #include <stddef.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -43,9 +64,34 @@
 
 #include "svtme.h"
 
-/* --------------------------------------------------------------------------
- * rtcd registration (aom_dsp_rtcd.h:779, 841, 842, 848, 853-856, 863, 868)
- * ------------------------------------------------------------------------ */
+EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
+                                        uint32_t b64_origin_y, MeContext *me_ctx, EbPictureBufferDesc *input_ptr);
+void svtme_picture_changed(PictureParentControlSet *pcs);
+void svt_aom_setup_rtcd_hip_parity(void);
+void svtme_controls_from_me_context(svtme_controls *c, const MeContext *m);
+void svtme_job_from_pcs(svtme_job *job, const PictureParentControlSet *pcs, const MeContext *me);
+void svtme_job_from_tf(svtme_job *job, const PictureParentControlSet *centre, const MeContext *me,
+                       const EbPictureBufferDesc *input_ptr);
+void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_index, uint32_t b64_origin_x,
+                      uint32_t b64_origin_y, const svtme_job *job, const svtme_ref_record *recs,
+                      const svtme_sb_result *s);
+
+#ifdef SVTME_GLUE_WRAP
+EbErrorType __real_svt_aom_motion_estimation_b64(PictureParentControlSet *, uint32_t, uint32_t, uint32_t,
+                                                 MeContext *, EbPictureBufferDesc *);
+void __real_svt_aom_downsample_filtering_input_picture(PictureParentControlSet *, EbPictureBufferDesc *,
+                                                       EbPictureBufferDesc *, EbPictureBufferDesc *);
+#define SVTME_ENCODER_ME_B64 __real_svt_aom_motion_estimation_b64
+#else
+EbErrorType svt_aom_motion_estimation_b64(PictureParentControlSet *, uint32_t, uint32_t, uint32_t, MeContext *,
+                                          EbPictureBufferDesc *);
+#define SVTME_ENCODER_ME_B64 svt_aom_motion_estimation_b64
+#endif
+
+/* ==========================================================================
+ * rtcd registration, parity / debug mode only
+ * (aom_dsp_rtcd.h:779, 841, 842, 848, 853-856, 863, 868)
+ * ======================================================================== */
 static struct {
     void (*sad_loop)(uint8_t *, uint32_t, uint8_t *, uint32_t, uint32_t, uint32_t, uint64_t *, int16_t *,
                      int16_t *, uint32_t, uint8_t, int16_t, int16_t);
@@ -73,6 +119,9 @@ _Static_assert(offsetof(MV_COST_PARAMS, mvcost) == SVTME_MVCOST_OFF_MVCOST, "MV_
 _Static_assert(offsetof(MV_COST_PARAMS, error_per_bit) == SVTME_MVCOST_OFF_ERROR_PER_BIT,
                "MV_COST_PARAMS.error_per_bit");
 _Static_assert(offsetof(MV, row) == 0 && offsetof(MV, col) == 2, "MV is (row, col) int16");
+/* the MeCandidate bit-field byte the records carry (me_sb_results.h:28-34) */
+_Static_assert(sizeof(MeCandidate) == 1, "MeCandidate is one byte");
+_Static_assert(sizeof(MvCandidate) == 4, "MvCandidate is (x, y) int16");
 
 static void glue_sad_loop(uint8_t *src, uint32_t src_stride, uint8_t *ref, uint32_t ref_stride, uint32_t bh,
                           uint32_t bw, uint64_t *best_sad, int16_t *x, int16_t *y, uint32_t src_stride_raw,
@@ -148,9 +197,10 @@ static void glue_pme(const struct svt_mv_cost_param *p, uint8_t *src, uint32_t s
                    step, mvx, mvy);
 }
 
-/* Call right after svt_aom_setup_rtcd_internal(): the pointers it set become the
- * fallbacks, the HIP variants the active ones. */
-void svt_aom_setup_rtcd_hip(void) {
+/* Parity / debug only: call right after svt_aom_setup_rtcd_internal(); the
+ * pointers it set become the fallbacks, the HIP variants the active ones. Never
+ * call it in picture-job mode: every rtcd call would become a GPU round trip. */
+void svt_aom_setup_rtcd_hip_parity(void) {
     g_prev.sad_loop              = svt_sad_loop_kernel;
     g_prev.nxm                   = svt_nxm_sad_kernel;
     g_prev.ext_8x8_16x16         = svt_ext_sad_calculation_8x8_16x16;
@@ -174,9 +224,9 @@ void svt_aom_setup_rtcd_hip(void) {
     svt_pme_sad_loop_kernel                   = glue_pme;                     /* :868 */
 }
 
-/* --------------------------------------------------------------------------
- * Controls: the MeContext fields svt_aom_sig_deriv_me sets (me_context.h:280-509)
- * ------------------------------------------------------------------------ */
+/* ==========================================================================
+ * Controls: the MeContext fields svt_aom_sig_deriv_me[_tf] set (me_context.h:280-509)
+ * ======================================================================== */
 static svtme_area area_of(SearchArea a) {
     svtme_area r = {a.width, a.height};
     return r;
@@ -249,25 +299,27 @@ void svtme_controls_from_me_context(svtme_controls *c, const MeContext *m) {
     c->prev_me_stage_based_exit_th = m->prev_me_stage_based_exit_th;
 }
 
-/* --------------------------------------------------------------------------
- * One PA-ME picture job (me_process.c:217-261; pictures are uploaded under
- * their picture_number by the PA stage, svtme_picture_upload)
- * ------------------------------------------------------------------------ */
+/* ==========================================================================
+ * Jobs
+ * ======================================================================== */
+static uint32_t align8(uint32_t v) { return (v + 7u) & ~7u; }
+
+/* One PA-ME picture job: the fields me_process.c:217-261 and
+ * svt_aom_motion_estimation_b64 read from the PCS, the ME context and the
+ * reference pictures' PA objects (me_ds_ref_array, set per SB by
+ * me_process.c:248-262 before the call). */
 void svtme_job_from_pcs(svtme_job *job, const PictureParentControlSet *pcs, const MeContext *me) {
     memset(job, 0, sizeof(*job));
     job->picture_number = pcs->picture_number;
     job->width          = pcs->aligned_width;
     job->height         = pcs->aligned_height;
-    job->num_lists      = pcs->slice_type == P_SLICE ? 1 : 2;
-    job->num_refs[0]    = pcs->ref_list0_count_try;
-    job->num_refs[1]    = pcs->slice_type == B_SLICE ? pcs->ref_list1_count_try : 0;
+    job->num_lists      = me->num_of_list_to_search;
+    job->num_refs[0]    = me->num_of_ref_pic_to_search[0];
+    job->num_refs[1]    = job->num_lists == 2 ? me->num_of_ref_pic_to_search[1] : 0;
     for (int l = 0; l < job->num_lists; l++)
-        for (int r = 0; r < job->num_refs[l]; r++) {
-            const EbPaReferenceObject *ro = (const EbPaReferenceObject *)pcs->ref_pa_pic_ptr_array[l][r]->object_ptr;
-            job->ref_picture_number[l][r] = ro->picture_number;
-        }
-    job->temporal_layer_index            = pcs->temporal_layer_index;
-    job->is_ref                          = pcs->is_ref;
+        for (int r = 0; r < job->num_refs[l]; r++) job->ref_picture_number[l][r] = me->me_ds_ref_array[l][r].picture_number;
+    job->temporal_layer_index            = me->temporal_layer_index;
+    job->is_ref                          = me->is_ref;
     job->hierarchical_levels             = pcs->hierarchical_levels;
     job->similar_brightness_refs         = pcs->similar_brightness_refs;
     job->enable_me_8x8                   = pcs->enable_me_8x8;
@@ -276,25 +328,102 @@ void svtme_job_from_pcs(svtme_job *job, const PictureParentControlSet *pcs, cons
     job->max_refs                        = pcs->pa_me_data->max_refs;
     job->max_l0                          = pcs->pa_me_data->max_l0;
     job->only_l_bwd                      = pcs->scs->mrp_ctrls.only_l_bwd;
-    job->input_resolution                = (uint8_t)pcs->input_resolution;
+    job->input_resolution                = (uint8_t)pcs->scs->input_resolution;
     job->gm_enabled                      = pcs->gm_ctrls.enabled;
     job->gm_use_distance_based_active_th = pcs->gm_ctrls.use_distance_based_active_th;
     job->me_type                         = SVTME_ME_OPEN_LOOP;
     svtme_controls_from_me_context(&job->ctrl, me);
 }
 
-/* --------------------------------------------------------------------------
- * Outputs of one SB back into the reference's storage
- * ------------------------------------------------------------------------ */
-void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_index,
-                      const svtme_ref_record *recs, uint32_t R, const svtme_sb_result *s) {
-    MeSbResults *res   = pcs->pa_me_data->me_results[b64_index];
-    const uint32_t mc  = pcs->pa_me_data->max_cand, mr = pcs->pa_me_data->max_refs;
-    memcpy(res->total_me_candidate_index, s->total_me_candidate_index, SVTME_PU_COUNT);
-    for (int pu = 0; pu < SVTME_PU_COUNT; pu++) {
-        memcpy(&res->me_candidate_array[pu * mc], s->me_candidate_array[pu], mc); /* 1-byte MeCandidate */
+/* One TF-ME job: the central picture against the one reference
+ * temporal_filtering.c:3127-3168 set up (list 0, ref 0) with the TF controls of
+ * svt_aom_sig_deriv_me_tf + set_hme_search_params_mctf. */
+void svtme_job_from_tf(svtme_job *job, const PictureParentControlSet *centre, const MeContext *me,
+                       const EbPictureBufferDesc *input_ptr) {
+    memset(job, 0, sizeof(*job));
+    job->picture_number        = centre->picture_number;
+    job->width                 = align8(input_ptr->width); /* motion_estimation.c:3093-3094 */
+    job->height                = align8(input_ptr->height);
+    job->num_lists             = 1;
+    job->num_refs[0]           = 1;
+    job->ref_picture_number[0][0] = me->me_ds_ref_array[0][0].picture_number;
+    job->temporal_layer_index  = me->temporal_layer_index;
+    job->is_ref                = me->is_ref;
+    job->hierarchical_levels   = centre->hierarchical_levels;
+    job->input_resolution      = (uint8_t)centre->scs->input_resolution;
+    job->me_type               = SVTME_ME_MCTF;
+    job->tf_me_exit_th         = me->tf_me_exit_th;
+    svtme_controls_from_me_context(&job->ctrl, me);
+}
+
+/* ==========================================================================
+ * Outputs of one SB back into the reference's storage, exactly where
+ * svt_aom_motion_estimation_b64 leaves them
+ * ======================================================================== */
+void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_index, uint32_t b64_origin_x,
+                      uint32_t b64_origin_y, const svtme_job *job, const svtme_ref_record *recs,
+                      const svtme_sb_result *s) {
+    /* :3093-3100 */
+    me->b64_width  = (job->width - b64_origin_x) < 64 ? job->width - b64_origin_x : 64;
+    me->b64_height = (job->height - b64_origin_y) < 64 ? job->height - b64_origin_y : 64;
+    /* init_me_hme_data (:3047-3069): every (list, ref) slot */
+    memset(me->p_sb_best_mv, 0, sizeof(me->p_sb_best_mv));
+    for (int l = 0; l < MAX_NUM_OF_REF_PIC_LIST; l++)
+        for (int r = 0; r < REF_LIST_MAX_DEPTH; r++) {
+            if (job->me_type != SVTME_ME_MCTF)
+                me->search_results[l][r].list_i = (uint8_t)l;
+            me->search_results[l][r].ref_i  = (uint8_t)r;
+            me->search_results[l][r].do_ref = 1;
+            me->search_results[l][r].hme_sad = MAX_U32;
+            me->reduce_me_sr_divisor[l][r]  = 1;
+            me->zz_sad[l][r]                = (uint32_t)~0;
+        }
+    /* per-reference state after the SB (search_results, me_context.h:459; the
+     * integer-search winners p_sb_best_* and the p_best_* views of the last
+     * searched reference, :1368-1384, which TF reads) */
+    const svtme_ref_record *rec = recs;
+    for (int l = 0; l < job->num_lists; l++)
+        for (int r = 0; r < job->num_refs[l]; r++, rec++) {
+            SearchResults *sr = &me->search_results[l][r];
+            sr->hme_sc_x      = rec->hme_sc_x;
+            sr->hme_sc_y      = rec->hme_sc_y;
+            sr->hme_sad       = rec->hme_sad;
+            sr->do_ref        = rec->do_ref;
+            me->zz_sad[l][r]  = rec->zz_sad;
+            if (!rec->searched)
+                continue; /* the reference leaves p_sb_best_sad untouched and p_sb_best_mv zero */
+            memcpy(me->p_sb_best_sad[l][r], rec->best_sad, sizeof(rec->best_sad));
+            memcpy(me->p_sb_best_mv[l][r], rec->best_mv, sizeof(rec->best_mv));
+            me->p_best_sad_64x64 = &me->p_sb_best_sad[l][r][ME_TIER_ZERO_PU_64x64];
+            me->p_best_sad_32x32 = &me->p_sb_best_sad[l][r][ME_TIER_ZERO_PU_32x32_0];
+            me->p_best_sad_16x16 = &me->p_sb_best_sad[l][r][ME_TIER_ZERO_PU_16x16_0];
+            me->p_best_sad_8x8   = &me->p_sb_best_sad[l][r][ME_TIER_ZERO_PU_8x8_0];
+            me->p_best_mv64x64   = &me->p_sb_best_mv[l][r][ME_TIER_ZERO_PU_64x64];
+            me->p_best_mv32x32   = &me->p_sb_best_mv[l][r][ME_TIER_ZERO_PU_32x32_0];
+            me->p_best_mv16x16   = &me->p_sb_best_mv[l][r][ME_TIER_ZERO_PU_16x16_0];
+            me->p_best_mv8x8     = &me->p_sb_best_mv[l][r][ME_TIER_ZERO_PU_8x8_0];
+        }
+    if (job->me_type == SVTME_ME_MCTF) {
+        if (recs[0].tf_early_exit) /* :3109-3112 */
+            me->tf_use_pred_64x64_only_th = (uint8_t)~0;
+        return;
+    }
+    /* candidates (:2532-2835) into MeSbResults (me_sb_results.h:44), whose arrays
+     * hold only the PUs ME produces candidates for (pcs.c:108-117): 85, 21
+     * without 8x8, 5 without 16x16 (the use_me_pu rule, :2561-2563); the
+     * candidates past total_me_candidate_index are not written */
+    MeSbResults *res  = pcs->pa_me_data->me_results[b64_index];
+    const uint32_t mc = pcs->pa_me_data->max_cand, mr = pcs->pa_me_data->max_refs;
+    const uint32_t n_pus = pcs->enable_me_16x16
+        ? (pcs->enable_me_8x8 ? pcs->max_number_of_pus_per_sb : MAX_SB64_PU_COUNT_NO_8X8)
+        : MAX_SB64_PU_COUNT_WO_16X16;
+    for (uint32_t pu = 0; pu < n_pus; pu++) {
+        const uint32_t n = s->total_me_candidate_index[pu] < mc ? s->total_me_candidate_index[pu] : mc;
+        res->total_me_candidate_index[pu] = s->total_me_candidate_index[pu];
+        memcpy(&res->me_candidate_array[pu * mc], s->me_candidate_array[pu], n);
         for (uint32_t k = 0; k < mr; k++) res->me_mv_array[pu * mr + k].as_int = s->me_mv_array[pu][k];
     }
+    /* compute_distortion (:2964-3007) and perform_gm_detection (:2838-2961) */
     memcpy(me->me_distortion, s->me_distortion, sizeof(me->me_distortion));
     pcs->me_8x8_cost_variance[b64_index]        = s->me_8x8_cost_variance;
     pcs->rc_me_distortion[b64_index]            = s->rc_me_distortion;
@@ -304,54 +433,293 @@ void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_
     pcs->me_8x8_distortion[b64_index]           = s->me_8x8_distortion;
     pcs->stationary_block_present_sb[b64_index] = s->stationary_block_present;
     pcs->rc_me_allow_gm[b64_index]              = s->rc_me_allow_gm;
-    /* per-reference state the ME context keeps after the SB (search_results,
-     * me_context.h:459, read by GM detection and TF) */
-    for (uint32_t k = 0; k < R; k++) {
-        const int l = k < me->num_of_ref_pic_to_search[0] ? 0 : 1;
-        const int r = l ? (int)k - me->num_of_ref_pic_to_search[0] : (int)k;
-        me->search_results[l][r].hme_sc_x = recs[k].hme_sc_x;
-        me->search_results[l][r].hme_sc_y = recs[k].hme_sc_y;
-        me->search_results[l][r].hme_sad  = recs[k].hme_sad;
-        me->search_results[l][r].do_ref   = recs[k].do_ref;
-        memcpy(me->p_sb_best_sad[l][r], recs[k].best_sad, sizeof(recs[k].best_sad));
-        memcpy(me->p_sb_best_mv[l][r], recs[k].best_mv, sizeof(recs[k].best_mv));
-    }
 }
 
-/* --------------------------------------------------------------------------
- * me_process.c:172-290 for task_type TASK_PAME with ME segments 1x1: one job
- * for every SB of the picture, then the host's picture-level consumers (GM,
- * svt_aom_open_loop_intra_search_mb) run as before.
- * ------------------------------------------------------------------------ */
-EbErrorType svtme_me_picture(svtme_ctx *ctx, PictureParentControlSet *pcs, MeContext *me) {
+/* ==========================================================================
+ * Picture-job service of the SB function
+ * ======================================================================== */
+typedef struct GlueJob {
     svtme_job job;
-    svtme_job_from_pcs(&job, pcs, me);
-    me->num_of_list_to_search       = job.num_lists;
-    me->num_of_ref_pic_to_search[0] = job.num_refs[0];
-    me->num_of_ref_pic_to_search[1] = job.num_refs[1];
-    const uint32_t n_sb = svtme_sb_total(job.width, job.height);
-    const uint32_t R    = svtme_job_ref_slots(&job);
-    svtme_ref_record *recs = (svtme_ref_record *)malloc((size_t)n_sb * R * sizeof(*recs));
-    svtme_sb_result *sbr   = (svtme_sb_result *)malloc((size_t)n_sb * sizeof(*sbr));
-    if (!recs || !sbr) {
-        free(recs);
-        free(sbr);
-        return EB_ErrorInsufficientResources;
-    }
-    const svtme_status st = svtme_submit_picture(ctx, &job, recs, sbr);
-    if (st == SVTME_OK)
-        for (uint32_t sb = 0; sb < n_sb; sb++) svtme_scatter_sb(pcs, me, sb, &recs[(size_t)sb * R], R, &sbr[sb]);
-    free(recs);
-    free(sbr);
-    return (EbErrorType)st;
+    uint32_t n_sb, R;
+    svtme_ref_record *recs;
+    svtme_sb_result *sbr;
+    uint32_t served;
+    int state; /* 0 running, 1 done, -1 failed (its SBs run on the encoder's function) */
+    struct GlueJob *next;
+} GlueJob;
+
+typedef struct GluePic {
+    uint64_t pn;
+    uint32_t w, h;
+    uint64_t last_use;
+} GluePic;
+
+static struct {
+    pthread_once_t once;
+    pthread_mutex_t mu;  /* job list, residency table, counters */
+    pthread_cond_t cv;   /* a job finished */
+    pthread_mutex_t gpu; /* one thread drives the backend at a time */
+    svtme_ctx *ctx;
+    int strict, verify, max_resident;
+    const char *stats_path;
+    GlueJob *jobs;
+    GluePic *pics;
+    uint32_t n_pics, cap_pics;
+    uint64_t tick;
+    struct {
+        unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified;
+    } n;
+} G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER};
+
+static void glue_stats_at_exit(void) {
+    FILE *f = fopen(G.stats_path, "a");
+    if (!f)
+        return;
+    fprintf(f,
+            "{\"backend\": %d, \"pa_jobs\": %llu, \"tf_jobs\": %llu, \"sbs\": %llu, \"fallback_sbs\": %llu, "
+            "\"uploads\": %llu, \"invalidations\": %llu, \"evictions\": %llu, \"verified_planes\": %llu}\n",
+            G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
+            G.n.evictions, G.n.verified);
+    fclose(f);
 }
 
-/* Temporal filtering replaced the picture's padded planes
- * (temporal_filtering.c:3895-3931): re-upload so later PA-ME / TF-ME jobs read
- * the filtered pyramid, never the stale one. */
-EbErrorType svtme_picture_redecimated(svtme_ctx *ctx, const PictureParentControlSet *pcs,
-                                      const EbPictureBufferDesc *filtered) {
-    const uint8_t *y = filtered->buffer_y + (size_t)filtered->org_y * filtered->stride_y + filtered->org_x;
-    return (EbErrorType)svtme_picture_invalidate(ctx, pcs->picture_number, y, filtered->stride_y,
-                                                 pcs->aligned_width, pcs->aligned_height);
+static void glue_init(void) {
+    const char *e;
+    G.strict       = (e = getenv("SVTME_GLUE_STRICT")) && atoi(e);
+    G.verify       = (e = getenv("SVTME_GLUE_VERIFY")) && atoi(e);
+    G.max_resident = (e = getenv("SVTME_GLUE_RESIDENT")) ? atoi(e) : 64;
+    if (G.max_resident < 9)
+        G.max_resident = 9; /* a job names at most 1 + 8 pictures */
+    G.stats_path = getenv("SVTME_GLUE_STATS");
+    if (G.stats_path)
+        atexit(glue_stats_at_exit);
+    const int dev = (e = getenv("SVTME_DEVICE")) ? atoi(e) : 0;
+    if (svtme_ctx_create(dev, &G.ctx) != SVTME_OK) {
+        fprintf(stderr, "svtme glue: no ME device (%s); motion estimation runs on the CPU\n", svtme_last_error());
+        G.ctx = NULL;
+        if (G.strict)
+            abort();
+    }
 }
+
+static void glue_fallback(const char *what) {
+    fprintf(stderr, "svtme glue: %s (%s); the SB runs on the encoder's ME\n", what, svtme_last_error());
+    if (G.strict)
+        abort();
+}
+
+/* ---- residency (G.gpu held) */
+static GluePic *pic_find(uint64_t pn) {
+    for (uint32_t i = 0; i < G.n_pics; i++)
+        if (G.pics[i].pn == pn)
+            return &G.pics[i];
+    return NULL;
+}
+
+static int verify_level(uint64_t pn, int level, const EbPictureBufferDesc *d) {
+    uint32_t S, w, h, pad;
+    if (svtme_picture_download(G.ctx, pn, level, NULL, &S, &w, &h, &pad) != SVTME_OK)
+        return -1;
+    uint8_t *buf = (uint8_t *)malloc((size_t)S * (h + 2 * pad));
+    if (!buf || svtme_picture_download(G.ctx, pn, level, buf, &S, &w, &h, &pad) != SVTME_OK) {
+        free(buf);
+        return -1;
+    }
+    /* compare the searchable extent: the picture and the padding both sides keep */
+    const int px = (int)pad < d->org_x ? (int)pad : d->org_x, py = (int)pad < d->org_y ? (int)pad : d->org_y;
+    int bad = 0;
+    for (int y = -py; y < (int)h + py && !bad; y++) {
+        const uint8_t *a = buf + (size_t)(y + (int)pad) * S + pad - px;
+        const uint8_t *b = d->buffer_y + (ptrdiff_t)(y + d->org_y) * d->stride_y + d->org_x - px;
+        bad = memcmp(a, b, w + 2 * px) != 0;
+    }
+    free(buf);
+    return bad;
+}
+
+/* Make picture pn resident with the encoder's current planes of it. */
+static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPictureBufferDesc *quarter,
+                      const EbPictureBufferDesc *sixteenth, uint32_t w, uint32_t h, uint64_t pin[9], int npin) {
+    GluePic *p = pic_find(pn);
+    if (p && p->w == w && p->h == h) {
+        p->last_use = ++G.tick;
+        return 0;
+    }
+    if (!p && G.n_pics >= (uint32_t)G.max_resident) { /* evict the least recently used picture this job does not name */
+        GluePic *lru = NULL;
+        for (uint32_t i = 0; i < G.n_pics; i++) {
+            int pinned = 0;
+            for (int k = 0; k < npin; k++) pinned |= G.pics[i].pn == pin[k];
+            if (!pinned && (!lru || G.pics[i].last_use < lru->last_use))
+                lru = &G.pics[i];
+        }
+        if (lru) {
+            svtme_picture_release(G.ctx, lru->pn);
+            *lru = G.pics[--G.n_pics];
+            G.n.evictions++;
+        }
+    }
+    const uint8_t *y = full->buffer_y + (size_t)full->org_y * full->stride_y + full->org_x;
+    if (svtme_picture_upload(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
+        return -1;
+    if (G.verify && (verify_level(pn, 0, full) || (quarter && verify_level(pn, 1, quarter)) ||
+                     (sixteenth && verify_level(pn, 2, sixteenth)))) {
+        fprintf(stderr, "svtme glue: picture %llu: the ME pyramid differs from the encoder's planes\n",
+                (unsigned long long)pn);
+        abort();
+    }
+    G.n.verified += G.verify ? 3 : 0;
+    if (!p) {
+        if (G.n_pics == G.cap_pics) {
+            G.cap_pics = G.cap_pics ? 2 * G.cap_pics : 16;
+            G.pics     = (GluePic *)realloc(G.pics, G.cap_pics * sizeof(GluePic));
+            if (!G.pics)
+                abort();
+        }
+        p = &G.pics[G.n_pics++];
+    }
+    p->pn = pn, p->w = w, p->h = h, p->last_use = ++G.tick;
+    G.n.uploads++;
+    return 0;
+}
+
+/* The encoder rebuilt a picture's 1/4 and 1/16 planes from its (possibly
+ * replaced) full-resolution plane: temporal filtering's
+ * pad_and_decimate_filtered_pic (temporal_filtering.c:3895-3931), or picture
+ * decision (pd_process.c:2720-2739). Jobs read it again from the new planes;
+ * jobs already computed read the old ones, as the encoder's SB calls made
+ * before the rebuild did. */
+void svtme_picture_changed(PictureParentControlSet *pcs) {
+    pthread_once(&G.once, glue_init);
+    if (!G.ctx)
+        return;
+    pthread_mutex_lock(&G.gpu);
+    GluePic *p = pic_find(pcs->picture_number);
+    if (p) {
+        svtme_picture_release(G.ctx, p->pn);
+        *p = G.pics[--G.n_pics];
+        G.n.invalidations++;
+    }
+    pthread_mutex_unlock(&G.gpu);
+}
+
+static EbPaReferenceObject *pa_object(const PictureParentControlSet *pcs) {
+    return (EbPaReferenceObject *)pcs->pa_ref_pic_wrapper->object_ptr;
+}
+
+/* run one job (G.gpu held): make its pictures resident, submit, keep the results */
+static int run_job(GlueJob *j, const PictureParentControlSet *pcs, const MeContext *me) {
+    const svtme_job *job = &j->job;
+    uint64_t pin[9];
+    int npin = 0;
+    pin[npin++] = job->picture_number;
+    for (int l = 0; l < job->num_lists; l++)
+        for (int r = 0; r < job->num_refs[l]; r++) pin[npin++] = job->ref_picture_number[l][r];
+    const EbPaReferenceObject *cur = pa_object(pcs);
+    if (pic_ensure(job->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
+                   cur->sixteenth_downsampled_picture_ptr, job->width, job->height, pin, npin))
+        return -1;
+    for (int l = 0; l < job->num_lists; l++)
+        for (int r = 0; r < job->num_refs[l]; r++) {
+            const EbDownScaledBufDescPtrArray *d = &me->me_ds_ref_array[l][r];
+            if (pic_ensure(d->picture_number, d->picture_ptr, d->quarter_picture_ptr, d->sixteenth_picture_ptr,
+                           job->width, job->height, pin, npin))
+                return -1;
+        }
+    j->recs = (svtme_ref_record *)malloc((size_t)j->n_sb * j->R * sizeof(svtme_ref_record));
+    j->sbr  = job->me_type == SVTME_ME_MCTF ? NULL : (svtme_sb_result *)malloc((size_t)j->n_sb * sizeof(svtme_sb_result));
+    if (!j->recs || (job->me_type != SVTME_ME_MCTF && !j->sbr))
+        return -1;
+    return svtme_submit_picture(G.ctx, job, j->recs, j->sbr) == SVTME_OK ? 0 : -1;
+}
+
+static void job_free(GlueJob *j) {
+    free(j->recs);
+    free(j->sbr);
+    free(j);
+}
+
+EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
+                                        uint32_t b64_origin_y, MeContext *me_ctx, EbPictureBufferDesc *input_ptr) {
+    pthread_once(&G.once, glue_init);
+    svtme_job job;
+    if (me_ctx->me_type == ME_OPEN_LOOP && !pcs->frame_superres_enabled && !pcs->frame_resize_enabled)
+        svtme_job_from_pcs(&job, pcs, me_ctx);
+    else if (me_ctx->me_type == ME_MCTF)
+        svtme_job_from_tf(&job, pcs, me_ctx, input_ptr);
+    else /* scaled references (me_process.c:229-246), DG detector: the encoder's own search */
+        return SVTME_ENCODER_ME_B64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
+    if (!G.ctx) {
+        pthread_mutex_lock(&G.mu);
+        G.n.fallback_sbs++;
+        pthread_mutex_unlock(&G.mu);
+        return SVTME_ENCODER_ME_B64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
+    }
+
+    /* find or start the picture's job (one per picture, or per TF reference) */
+    pthread_mutex_lock(&G.mu);
+    GlueJob *j = G.jobs;
+    while (j && memcmp(&j->job, &job, sizeof(job)) != 0) j = j->next;
+    if (!j) {
+        j = (GlueJob *)calloc(1, sizeof(GlueJob));
+        if (!j)
+            abort();
+        j->job  = job;
+        j->n_sb = svtme_sb_total(job.width, job.height);
+        j->R    = svtme_job_ref_slots(&job);
+        j->next = G.jobs;
+        G.jobs  = j;
+        if (job.me_type == SVTME_ME_MCTF)
+            G.n.tf_jobs++;
+        else
+            G.n.pa_jobs++;
+        pthread_mutex_unlock(&G.mu);
+        pthread_mutex_lock(&G.gpu);
+        const int rc = run_job(j, pcs, me_ctx);
+        pthread_mutex_unlock(&G.gpu);
+        pthread_mutex_lock(&G.mu);
+        j->state = rc ? -1 : 1;
+        if (rc)
+            glue_fallback("picture job failed");
+        pthread_cond_broadcast(&G.cv);
+    }
+    while (j->state == 0) pthread_cond_wait(&G.cv, &G.mu);
+    const int ok = j->state == 1 && b64_index < j->n_sb;
+    if (ok)
+        G.n.sbs++;
+    else
+        G.n.fallback_sbs++;
+    pthread_mutex_unlock(&G.mu);
+
+    EbErrorType ret = EB_ErrorNone;
+    if (ok)
+        svtme_scatter_sb(pcs, me_ctx, b64_index, b64_origin_x, b64_origin_y, &j->job,
+                         &j->recs[(size_t)b64_index * j->R], j->sbr ? &j->sbr[b64_index] : NULL);
+    else
+        ret = SVTME_ENCODER_ME_B64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
+
+    /* the job is dropped once every SB of the picture has been served */
+    pthread_mutex_lock(&G.mu);
+    if (++j->served == j->n_sb) {
+        GlueJob **pp = &G.jobs;
+        while (*pp != j) pp = &(*pp)->next;
+        *pp = j->next;
+        job_free(j);
+    }
+    pthread_mutex_unlock(&G.mu);
+    return ret;
+}
+
+#ifdef SVTME_GLUE_WRAP
+EbErrorType __wrap_svt_aom_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index,
+                                                 uint32_t b64_origin_x, uint32_t b64_origin_y, MeContext *me_ctx,
+                                                 EbPictureBufferDesc *input_ptr) {
+    return svtme_motion_estimation_b64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
+}
+
+void __wrap_svt_aom_downsample_filtering_input_picture(PictureParentControlSet *pcs, EbPictureBufferDesc *full,
+                                                       EbPictureBufferDesc *quarter, EbPictureBufferDesc *sixteenth) {
+    __real_svt_aom_downsample_filtering_input_picture(pcs, full, quarter, sixteenth);
+    svtme_picture_changed(pcs);
+}
+#endif

@@ -1,0 +1,86 @@
+# oracle/encoder.mk — TEST INFRASTRUCTURE ONLY (container build; outputs in oracle/_ref/enc/).
+#
+#   make -C oracle -f encoder.mk -j8
+#
+# Builds the reference SVT-AV1 encoder, C-only (the reference's COMPILE_C_ONLY
+# configuration: no x86 SIMD, which needs NASM, absent here), with gcc directly
+# on its own unmodified sources under $(REF). The reference's cmake is never
+# run. The one generated file the sources include, EbVersion.h, is instantiated
+# from the reference's own template Source/Lib/Codec/EbVersion.h.in with the
+# substitution its CMake rule performs (Source/Lib/Codec/CMakeLists.txt:15-17,
+# EXCLUDE_HASH: @PACKAGE_VERSION_STRING@ -> the project version, CMakeLists.txt:19).
+#
+# Three executables, all from the same objects:
+#   svtav1enc            the unmodified encoder app (Source/App)
+#   svtav1enc_ora        + integration/svtme_svt_glue.c with
+#                        -Wl,--wrap=svt_aom_motion_estimation_b64 (PA-ME and
+#                        TF-ME served from picture jobs) and
+#                        -Wl,--wrap=svt_aom_downsample_filtering_input_picture
+#                        (re-decimated pictures are re-uploaded), backed by
+#                        liboraclejob.so: the svtme job API over the oracle (CPU)
+#   svtav1enc_gpu        the same glue backed by the product, libsvtme.so (HIP)
+# tests/test_encoder.py encodes with them and compares the bitstreams byte for byte.
+
+REF ?= /root/reference
+CC ?= gcc
+O = _ref/enc
+RS = $(REF)/Source
+VERSION = 3.0.2
+
+INC = -I$(REF) -I$(RS)/API -I$(RS)/Lib/Codec -I$(RS)/Lib/C_DEFAULT -I$(RS)/Lib/Globals \
+      -I$(REF)/third_party/fastfeat -I$(O)/gen
+# the definitions the reference's C-only build passes (CMakeLists.txt:296-305, :466; cpuinfo.cmake:101)
+DEFS = -DEXCLUDE_HASH=0 -DREPRODUCIBLE_BUILDS=0 -DEN_AVX512_SUPPORT=0 -DHAVE_CPUINFO=0 -DNDEBUG \
+       -D_FORTIFY_SOURCE=2
+CFLAGS = -O2 -std=gnu99 -fPIC -w -fno-strict-aliasing -mno-avx $(EXTRA_CFLAGS)
+
+LIB_SRC = $(wildcard $(RS)/Lib/Codec/*.c) $(wildcard $(RS)/Lib/C_DEFAULT/*.c) \
+          $(wildcard $(RS)/Lib/Globals/*.c) $(wildcard $(REF)/third_party/fastfeat/*.c)
+APP_SRC = $(wildcard $(RS)/App/*.c) $(wildcard $(REF)/third_party/safestringlib/*.c)
+LIB_OBJ = $(patsubst $(REF)/%.c,$(O)/obj/%.o,$(LIB_SRC))
+APP_OBJ = $(patsubst $(REF)/%.c,$(O)/obj/%.o,$(APP_SRC))
+
+all: $(O)/svtav1enc $(O)/svtav1enc_ora $(O)/svtav1enc_gpu
+
+$(O)/gen/EbVersion.h: $(RS)/Lib/Codec/EbVersion.h.in
+	@mkdir -p $(dir $@)
+	sed 's/@PACKAGE_VERSION_STRING@/v$(VERSION)/' $< > $@
+
+$(O)/obj/%.o: $(REF)/%.c $(O)/gen/EbVersion.h
+	@mkdir -p $(dir $@)
+	$(CC) $(CFLAGS) $(DEFS) $(INC) -c -o $@ $<
+
+$(O)/libsvtenc.a: $(LIB_OBJ)
+	rm -f $@ && ar rcs $@ $^
+
+$(O)/svtav1enc: $(APP_OBJ) $(O)/libsvtenc.a
+	$(CC) -o $@ $(APP_OBJ) $(O)/libsvtenc.a -lpthread -lm
+
+# ---- glue (product integration code) compiled against the reference headers
+$(O)/obj/glue.o: ../integration/svtme_svt_glue.c ../include/svtme.h $(O)/gen/EbVersion.h
+	@mkdir -p $(dir $@)
+	$(CC) $(filter-out -w,$(CFLAGS)) -Wall -Wextra -Werror -Wno-unused-parameter -Wno-missing-field-initializers \
+	    -DSVTME_GLUE_WRAP -ffunction-sections $(DEFS) $(INC) -I../include -c -o $@ $<
+
+# ---- test-only backend: the rtcd variants (parity mode) are not part of it, so
+# the oracle-backed link drops the glue's unused registration code (--gc-sections)
+# ---- test-only backend: the svtme job API over the oracle (never shipped)
+liboraclejob.so: svtme_oraclejob.c svtme_oracle.c svtme_oracle_kernels.c svtme_oracle.h ../include/svtme.h
+	$(CC) -O3 -fPIC -std=gnu11 -Wall -Wextra -Wno-unused-parameter -shared -o $@ svtme_oraclejob.c \
+	    svtme_oracle.c svtme_oracle_kernels.c -lpthread
+
+WRAP = -Wl,--wrap=svt_aom_motion_estimation_b64 -Wl,--wrap=svt_aom_downsample_filtering_input_picture
+
+$(O)/svtav1enc_ora: $(APP_OBJ) $(O)/obj/glue.o $(O)/libsvtenc.a liboraclejob.so
+	$(CC) -o $@ $(APP_OBJ) $(O)/obj/glue.o $(O)/libsvtenc.a $(WRAP) -L. -loraclejob \
+	    -Wl,--gc-sections \
+	    -Wl,-rpath,'$$ORIGIN/../..' -lpthread -lm
+
+$(O)/svtav1enc_gpu: $(APP_OBJ) $(O)/obj/glue.o $(O)/libsvtenc.a
+	$(CC) -o $@ $(APP_OBJ) $(O)/obj/glue.o $(O)/libsvtenc.a $(WRAP) -L../svt-av1-mirror_amd -lsvtme \
+	    -Wl,-rpath,'$$ORIGIN/../../../svt-av1-mirror_amd' -lpthread -lm
+
+clean:
+	rm -rf $(O) liboraclejob.so
+
+.PHONY: all clean

@@ -185,7 +185,8 @@ typedef struct {
  * AV1_PROB_COST_SHIFT 9 - RD_EPB_SHIFT 6 + PIXEL_TRANSFORM_ERROR_SCALE 4 */
 static int ora_mv_err_cost(int16_t row, int16_t col, const ora_mv_cost_params *p) {
     const int dr = (int16_t)(row - p->ref_mv[0]), dc = (int16_t)(col - p->ref_mv[1]);
-    const int ar = dr < 0 ? -dr : dr, ac = dc < 0 ? -dc : dc;
+    /* diff and abs_diff are int16 MVs (mcomp.c:46-47): |-32768| wraps back to -32768 */
+    const int ar = (int16_t)(dr < 0 ? -dr : dr), ac = (int16_t)(dc < 0 ? -dc : dc);
     const int sh = 14;
     switch (p->mv_cost_type) {
     case 0: { /* the reference's `if (mvcost)` tests the array parameter: always taken */

@@ -136,6 +136,7 @@ struct svtme_ctx {
     hipEvent_t tev[kTimeSets][10] = {};
     uint32_t tmask[kTimeSets] = {};
     int t_pending = 0;
+    uint32_t t_dropped = 0;
     Lane lanes[SVTME_LANES]; // lanes[0].s == stream
     std::mutex mu;
 };
@@ -706,6 +707,8 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
         if (c->timing && c->t_pending < svtme_ctx::kTimeSets) {
             ev   = c->tev[c->t_pending];
             mask = &c->tmask[c->t_pending++];
+        } else if (c->timing) {
+            c->t_dropped++;
         }
         HIP_TRY(svtme_launch_stages(d + group_start[g], ordered + group_start[g], group_start[g + 1] - group_start[g],
                                     L.s, ev, mask));
@@ -729,9 +732,13 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
                     if ((st = mark(j.ref_picture_number[l][r])))
                         return st;
         }
-    c->last_count      = (uint32_t)sbs;
-    c->last_R          = n == 1 ? hj[0].R : 0;
-    c->last_has_sb     = with_sb && !out;
+    // svtme_fetch / svtme_device_records describe the context-owned buffers only:
+    // a submission into caller buffers leaves them as they were
+    if (!out) {
+        c->last_count  = (uint32_t)sbs;
+        c->last_R      = hj[0].R;
+        c->last_has_sb = with_sb;
+    }
     return SVTME_OK;
 }
 
@@ -784,6 +791,7 @@ extern "C" uint32_t svtme_timing_read(svtme_ctx *c, float stage_ms[5]) {
         return 0;
     std::lock_guard<std::mutex> lk(c->mu);
     double sum[5] = {0, 0, 0, 0, 0};
+    uint32_t launches[5] = {0, 0, 0, 0, 0};
     const int n = c->t_pending;
     for (int i = 0; i < n; i++)
         for (int k = 0; k < 5; k++) {
@@ -794,9 +802,14 @@ extern "C" uint32_t svtme_timing_read(svtme_ctx *c, float stage_ms[5]) {
                 hipEventElapsedTime(&ms, c->tev[i][2 * k], c->tev[i][2 * k + 1]) != hipSuccess)
                 return 0;
             sum[k] += ms;
+            launches[k]++;
         }
-    for (int k = 0; k < 5; k++) stage_ms[k] = n ? (float)(sum[k] / n) : 0.0f;
+    // each stage is averaged over the launch groups that ran it
+    for (int k = 0; k < 5; k++) stage_ms[k] = launches[k] ? (float)(sum[k] / launches[k]) : 0.0f;
+    if (c->t_dropped)
+        svtme_set_error_internal("svtme_timing_read: launch groups beyond the timing capacity were not recorded");
     c->t_pending = 0;
+    c->t_dropped = 0;
     return (uint32_t)n;
 }
 
@@ -814,10 +827,7 @@ extern "C" svtme_status svtme_sync(svtme_ctx *c) {
     return quiesce(c);
 }
 
-extern "C" svtme_status svtme_fetch(svtme_ctx *c, svtme_ref_record *recs, svtme_sb_result *sb) {
-    if (!c)
-        return fail(SVTME_ERR_BAD_PARAMETER, "null ctx");
-    std::lock_guard<std::mutex> lk(c->mu);
+static svtme_status fetch_locked(svtme_ctx *c, svtme_ref_record *recs, svtme_sb_result *sb) {
     HIP_TRY(hipSetDevice(c->device));
     if (recs)
         HIP_TRY(hipMemcpyAsync(recs, c->d_records, (size_t)c->last_count * c->last_R * sizeof(svtme_ref_record),
@@ -832,17 +842,25 @@ extern "C" svtme_status svtme_fetch(svtme_ctx *c, svtme_ref_record *recs, svtme_
     return SVTME_OK;
 }
 
+extern "C" svtme_status svtme_fetch(svtme_ctx *c, svtme_ref_record *recs, svtme_sb_result *sb) {
+    if (!c)
+        return fail(SVTME_ERR_BAD_PARAMETER, "null ctx");
+    std::lock_guard<std::mutex> lk(c->mu);
+    return fetch_locked(c, recs, sb);
+}
+
+// Submit and fetch under one hold of the context lock: the encoder's ME threads
+// call this concurrently, and another thread's submission must not replace the
+// context-owned records between this job's launch and its copy-out.
 extern "C" svtme_status svtme_submit_picture(svtme_ctx *c, const svtme_job *job, svtme_ref_record *recs,
                                              svtme_sb_result *sb) {
     if (!c)
         return fail(SVTME_ERR_BAD_PARAMETER, "null ctx");
-    {
-        std::lock_guard<std::mutex> lk(c->mu);
-        svtme_status st = submit_locked(c, job, sb != nullptr, nullptr, nullptr);
-        if (st)
-            return st;
-    }
-    return svtme_fetch(c, recs, sb);
+    std::lock_guard<std::mutex> lk(c->mu);
+    svtme_status st = submit_locked(c, job, sb != nullptr, nullptr, nullptr);
+    if (st)
+        return st;
+    return fetch_locked(c, recs, sb);
 }
 
 extern "C" void *svtme_device_records(svtme_ctx *c, uint64_t *bytes) {

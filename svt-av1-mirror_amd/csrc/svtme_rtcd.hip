@@ -530,8 +530,9 @@ extern "C" void svt_aom_downsample_2d_hip(uint8_t *input_samples, uint32_t input
 // MV_COST_PARAMS layout of include/svtme.h
 static uint32_t pme_rate(const uint8_t *p, int16_t row, int16_t col) {
     const int16_t *ref_mv = *(const int16_t *const *)(p + SVTME_MVCOST_OFF_REF_MV);
-    const int dr = row - ref_mv[0], dc = col - ref_mv[1];
-    const int ar = dr < 0 ? -dr : dr, ac = dc < 0 ? -dc : dc;
+    // diff and abs_diff are int16 MVs in the reference (mcomp.c:46-47)
+    const int dr = (int16_t)(row - ref_mv[0]), dc = (int16_t)(col - ref_mv[1]);
+    const int ar = (int16_t)(dr < 0 ? -dr : dr), ac = (int16_t)(dc < 0 ? -dc : dc);
     const int epb = *(const int *)(p + SVTME_MVCOST_OFF_ERROR_PER_BIT);
     const int shift = 7 + 9 - 6 + 4; // RDDIV_BITS + AV1_PROB_COST_SHIFT - RD_EPB_SHIFT + PIXEL_TRANSFORM_ERROR_SCALE
     switch (p[SVTME_MVCOST_OFF_TYPE]) {

@@ -24,8 +24,8 @@ stores inputs-as-parameters plus expected outputs:
                      access) as per-picture checksums and full records
 
 Run from the repo root in the build container (needs /root/reference for the
-library build only): python tests/golden/make_golden.py [tf|configs]
-(tf / configs: only those fixtures)
+library build only): python tests/golden/make_golden.py [tf|configs|rtcd]
+(tf / configs / rtcd: only those fixtures)
 """
 import hashlib
 import json
@@ -235,6 +235,8 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["configs"]:
         configs_golden()
+    elif sys.argv[1:] == ["rtcd"]:
+        rtcd_golden()
     else:
         if sys.argv[1:] != ["tf"]:
             main()

@@ -81,6 +81,11 @@ PME = [
     (128, 64, 12, 4, 1, -6, -2, -8, 24, 2, 128, 160, "rand", 70, 0xFFFFFFFF),  # mid-res lambda 0
     (16, 8, 33, 17, 2, -16, -8, 40, -8, 0, 32, 80, "sat", 200, 0xFFFFFFFF),    # saturated, entropy
     (8, 8, 24, 8, 1, -12, -4, 0, 0, 0, 64, 64, "flat", 50, 1),                  # initial best beats all
+    # far reference MVs (ref_mv row, col): the MV difference wraps in the int16 MV of
+    # mcomp.c:46 and |-32768| stays -32768 in abs_diff (mcomp.c:47)
+    (8, 8, 16, 6, 1, -8, 0, 20000, -2768, 3, 64, 160, "rand", 80, 0xFFFFFFFF, (30000, -30000)),  # L1 HD
+    (8, 8, 16, 6, 1, -8, 0, 20000, -2768, 0, 64, 160, "rand", 80, 0xFFFFFFFF, (30000, -30000)),  # entropy
+    (16, 8, 20, 5, 2, -10, -2, -16000, 16000, 4, 64, 160, "rand", 40, 0xFFFFFFFF, (17000, -17000)),  # OPT
 ]
 
 
@@ -233,11 +238,13 @@ class MvCostParams(C.Structure):
 
 
 def run_pme(lib, prefix, case, seed):
-    bw, bh, sa_w, sa_h, step, sx, sy, mvx, mvy, ctype, ss, rs, kind, epb, best0 = case
+    bw, bh, sa_w, sa_h, step, sx, sy, mvx, mvy, ctype, ss, rs, kind, epb, best0 = case[:15]
     rng = np.random.default_rng(seed)
     src = _content(rng, ss * bh + bw + 16, kind)
     ref = _content(rng, rs * (sa_h + bh + 1) + sa_w + bw + 16, kind)
     ref_mv = np.array([int(rng.integers(-64, 64)), int(rng.integers(-64, 64))], np.int16)
+    if len(case) > 15:
+        ref_mv = np.array(case[15], np.int16)
     jc = rng.integers(100, 2000, 4).astype(np.int32)
     tabs = [rng.integers(0, 4000, 2 * 16384 + 1).astype(np.int32) for _ in range(2)]
     p = MvCostParams()
