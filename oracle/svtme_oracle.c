@@ -1039,7 +1039,7 @@ static void ora_gm_detection(OraCtx *x, svtme_sb_result *o) {
             active_th     = job->gm_use_distance_based_active_th ? MAX(dist * 16, 32) : 32;
         }
         const uint32_t mv = x->best_mv[li][ri][n];
-        const int mx = (int)(int16_t)(mv & 0xFFFF) << 2, my = (int)(int16_t)(mv >> 16) << 2;
+        const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4; /* full-pel -> 1/4 pel */
         if (mx < -active_th)
             cnt[li][ri][0][0]++;
         else if (mx > active_th)

@@ -237,7 +237,8 @@ def _proto_common(lib, prefix):
 
 
 def load_oracle():
-    lib = _load(os.path.join(REPO_DIR, "oracle", "liboracle.so"), "CPU oracle")
+    # SVTME_ORACLE_LIB: a sanitizer build of the same sources (scripts/sanitize_cpu.sh)
+    lib = _load(os.environ.get("SVTME_ORACLE_LIB") or os.path.join(REPO_DIR, "oracle", "liboracle.so"), "CPU oracle")
     if not hasattr(lib, "_svtme_protos"):
         _proto_common(lib, "svtora")
         lib._svtme_protos = True
@@ -256,7 +257,7 @@ def load_ref():
 
 
 def load_synth():
-    lib = _load(os.path.join(PKG_DIR, "libsvtme_synth.so"), "synthetic generator")
+    lib = _load(os.environ.get("SVTME_SYNTH_LIB") or os.path.join(PKG_DIR, "libsvtme_synth.so"), "synthetic generator")
     if not hasattr(lib, "_svtme_protos"):
         lib.svtme_synth_texture_size.argtypes = [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
         lib.svtme_synth_texture.argtypes = [C.c_uint32, C.c_uint32, C.c_void_p]

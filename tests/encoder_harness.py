@@ -1,0 +1,137 @@
+"""End-to-end encoder parity: the reference SVT-AV1 encoder with and without
+this library's ME.
+
+oracle/encoder.mk builds, from the reference's unmodified sources (build
+container only), three encoder executables under oracle/_ref/enc/:
+
+  svtav1enc      the reference encoder app, C-only (as the reference's
+                 COMPILE_C_ONLY build)
+  svtav1enc_ora  + integration/svtme_svt_glue.c: PA-ME and TF-ME served from
+                 picture jobs of the job API, here backed by the CPU oracle
+                 (oracle/liboraclejob.so) -- pins the glue's field mapping
+  svtav1enc_gpu  the same glue backed by the product, libsvtme.so (HIP)
+
+The reference's CI pins its encoder the same way: bitstreams compared byte for
+byte (.gitlab/workflows/linux/.gitlab-ci.yml:354-370). Inputs are the PCG32
+panning texture of SURVEY.md 8(d) (svtme.Synth) written as y4m, chroma flat.
+Usable as a CLI: python tests/encoder_harness.py <case> [ora|gpu] [workdir]
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
+# SVTME_ENC_DIR: encoders of a sanitizer build (scripts/sanitize_cpu.sh)
+ENC_DIR = os.environ.get("SVTME_ENC_DIR") or os.path.join(ROOT, "oracle", "_ref", "enc")
+
+# name: (width, height, frames, preset, ten_bit, extra encoder options, expect_jobs)
+CASES = {
+    # BASELINE configs[0]: 640x360 8-bit, 30 frames random access, preset 12 (the app maps it to M10)
+    "ra360_p12": (640, 360, 30, 12, False, [], True),
+    # width and height not multiples of 64 (426 -> aligned 432): partial SBs, split GPU path
+    "240p_p8_ragged": (426, 240, 12, 8, False, [], True),
+    # more references, HME level 2, pre-HME variants
+    "360p_p4": (640, 360, 12, 4, False, [], True),
+    "360p_p0": (640, 360, 8, 0, False, [], True),
+    # TF off: PA-ME only
+    "360p_p8_notf": (640, 360, 12, 8, False, ["--enable-tf", "0"], True),
+    # super-resolution: scaled references stay on the encoder's own ME (me_process.c:229-246)
+    "360p_superres": (640, 360, 12, 8, False,
+                      ["--superres-mode", "1", "--superres-denom", "12", "--superres-kf-denom", "12"], True),
+    # BASELINE configs[1] resolution and configs[2] / configs[3] as whole encodes
+    "1080p_p8": (1920, 1080, 8, 8, False, [], True),
+    "4k_p8": (3840, 2160, 8, 8, False, [], True),
+    "4k10_p6": (3840, 2160, 4, 6, True, [], True),
+}
+
+
+def encoder(kind: str) -> str:
+    d = ENC_DIR if kind == "ora" else os.path.join(ROOT, "oracle", "_ref", "enc")
+    return os.path.join(d, {"ref": "svtav1enc", "ora": "svtav1enc_ora", "gpu": "svtav1enc_gpu"}[kind])
+
+
+def available(kind: str) -> bool:
+    return os.path.exists(encoder(kind))
+
+
+def write_y4m(path: str, w: int, h: int, frames: int, ten_bit: bool) -> None:
+    import svtme as S
+
+    if os.path.exists(path):
+        return
+    syn = S.Synth(w, h)
+    cw, ch = (w + 1) // 2, (h + 1) // 2
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(b"YUV4MPEG2 W%d H%d F30:1 Ip A1:1 C420%s\n" % (w, h, b"p10" if ten_bit else b"jpeg"))
+        chroma = (np.full(cw * ch, 512, "<u2") if ten_bit else np.full(cw * ch, 128, np.uint8)).tobytes()
+        for t in range(frames):
+            f.write(b"FRAME\n")
+            y = syn.frame10(t).astype("<u2") if ten_bit else syn.frame(t)
+            f.write(np.ascontiguousarray(y).tobytes())
+            f.write(chroma)
+            f.write(chroma)
+    os.replace(tmp, path)
+
+
+def _md5(path: str) -> str:
+    with open(path, "rb") as f:
+        return hashlib.md5(f.read()).hexdigest()
+
+
+def encode(kind: str, case: str, workdir: str, env_extra=None, timeout: int = 600) -> dict:
+    """Encode `case` with encoder `kind`; returns md5, seconds, glue counters."""
+    w, h, frames, preset, ten_bit, extra, _ = CASES[case]
+    os.makedirs(workdir, exist_ok=True)
+    y4m = os.path.join(workdir, f"{case}.y4m")
+    write_y4m(y4m, w, h, frames, ten_bit)
+    out = os.path.join(workdir, f"{case}.{kind}.ivf")
+    stats = os.path.join(workdir, f"{case}.{kind}.stats.json")
+    if os.path.exists(stats):
+        os.remove(stats)
+    env = dict(os.environ)
+    if kind != "ref":
+        env.update({"SVTME_GLUE_STRICT": "1", "SVTME_GLUE_VERIFY": "1", "SVTME_GLUE_STATS": stats})
+    env.update(env_extra or {})
+    cmd = [encoder(kind), "-i", y4m, "--preset", str(preset), "-b", out] + list(extra)
+    t0 = time.time()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    dt = time.time() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"{kind} encoder failed (rc {r.returncode}): {r.stderr[-2000:]}")
+    res = {"kind": kind, "case": case, "md5": _md5(out), "bytes": os.path.getsize(out), "seconds": round(dt, 3)}
+    if kind != "ref":
+        with open(stats) as f:
+            res["glue"] = json.loads(f.read().strip().splitlines()[-1])
+    return res
+
+
+def check(case: str, kind: str, workdir: str) -> dict:
+    """Reference encode and glue encode of one case; raises on any difference."""
+    ref = encode("ref", case, workdir)
+    got = encode(kind, case, workdir)
+    g = got["glue"]
+    if got["md5"] != ref["md5"]:
+        raise AssertionError(f"{case}: bitstream with {kind} ME differs from the reference encoder "
+                             f"({got['md5']} != {ref['md5']})")
+    if g["fallback_sbs"]:
+        raise AssertionError(f"{case}: {g['fallback_sbs']} SBs fell back to the encoder's ME")
+    if CASES[case][6] and not g["sbs"]:
+        raise AssertionError(f"{case}: no SB was served from a picture job")
+    return {"case": case, "md5": ref["md5"], "ref_seconds": ref["seconds"], "glue_seconds": got["seconds"], **g}
+
+
+if __name__ == "__main__":
+    case = sys.argv[1]
+    kind = sys.argv[2] if len(sys.argv) > 2 else "ora"
+    wd = sys.argv[3] if len(sys.argv) > 3 else os.path.join("/tmp", "svtme_enc")
+    print(json.dumps(check(case, kind, wd)))

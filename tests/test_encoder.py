@@ -1,0 +1,52 @@
+"""End-to-end: the reference encoder's bitstream is byte-identical with this
+library's ME in place of its own (the reference's CI
+checks its encoder the same way, .gitlab/workflows/linux/.gitlab-ci.yml:354-370).
+
+CPU: svtav1enc_ora -- integration/svtme_svt_glue.c over the oracle-backed job
+API -- against the unmodified encoder; pins every field the glue reads from
+and writes into the encoder (PA-ME and TF-ME, GM inputs, candidate arrays),
+the upload / re-decimation ordering and the pyramid (SVTME_GLUE_VERIFY compares
+every uploaded pyramid with the encoder's own planes).
+GPU: svtav1enc_gpu -- the same glue over libsvtme.so on the MI355X.
+The encoders are built in the build container by oracle/encoder.mk from the
+reference's sources; without them the tests skip.
+"""
+import os
+
+import pytest
+
+import encoder_harness as E
+
+CPU_CASES = ["ra360_p12", "240p_p8_ragged", "360p_p4", "360p_p8_notf", "360p_superres", "1080p_p8", "4k_p8"]
+GPU_CASES = list(E.CASES)
+
+
+@pytest.fixture(scope="module")
+def workdir(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("enc"))
+
+
+@pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
+@pytest.mark.parametrize("case", CPU_CASES)
+def test_bitstream_identical_oracle_backend(case, workdir):
+    r = E.check(case, "ora", workdir)
+    assert r["sbs"] > 0 and r["fallback_sbs"] == 0
+    assert r["verified_planes"] == 3 * r["uploads"]
+
+
+@pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
+def test_tf_jobs_and_redecimation_exercised(workdir):
+    """At preset 8 temporal filtering runs: TF-ME jobs are served and the
+    filtered pictures' pyramids are re-uploaded (svtme_picture_changed)."""
+    r = E.check("ra360_p12", "ora", workdir)
+    assert r["tf_jobs"] > 0 and r["pa_jobs"] > 0 and r["invalidations"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not (E.available("ref") and E.available("gpu")), reason="encoders built by oracle/encoder.mk")
+@pytest.mark.parametrize("case", GPU_CASES)
+def test_bitstream_identical_gpu(case, workdir):
+    r = E.check(case, "gpu", workdir)
+    assert r["backend"] == 1 and r["sbs"] > 0 and r["fallback_sbs"] == 0
+    print(f"\n{case}: ref {r['ref_seconds']} s, GPU-ME encoder {r['glue_seconds']} s, {r['pa_jobs']} PA + "
+          f"{r['tf_jobs']} TF jobs, {r['sbs']} SBs, md5 {r['md5']}")

@@ -29,16 +29,45 @@ def test_glue_compiles_against_reference_headers(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     syms = subprocess.run(["nm", obj], capture_output=True, text=True).stdout
     # defines the glue, binds the reference's rtcd pointers and the library's C ABI
-    for s in ("T svt_aom_setup_rtcd_hip", "T svtme_controls_from_me_context", "T svtme_job_from_pcs",
-              "T svtme_scatter_sb", "T svtme_me_picture", "T svtme_picture_redecimated",
+    for s in ("T svt_aom_setup_rtcd_hip_parity", "T svtme_controls_from_me_context", "T svtme_job_from_pcs",
+              "T svtme_job_from_tf", "T svtme_scatter_sb", "T svtme_motion_estimation_b64", "T svtme_picture_changed",
               "U svt_sad_loop_kernel_hip", "U svt_pme_sad_loop_kernel_hip", "U svtme_rtcd_failed", "U svtme_submit_picture",
-              "U svtme_picture_invalidate"):
+              "U svtme_picture_upload", "U svtme_picture_release", "U svt_aom_motion_estimation_b64"):
         assert s in syms, s
     for ptr in ("svt_sad_loop_kernel", "svt_nxm_sad_kernel", "downsample_2d", "sad_16b_kernel",
                 "svt_ext_all_sad_calculation_8x8_16x16", "svt_ext_eight_sad_calculation_32x32_64x64",
                 "svt_initialize_buffer_32bits", "svt_ext_sad_calculation_8x8_16x16",
                 "svt_ext_sad_calculation_32x32_64x64", "svt_pme_sad_loop_kernel"):
         assert f" {ptr}\n" in syms, ptr  # the RTCD_EXTERN pointer itself (aom_dsp_rtcd.h)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference headers only in the build container")
+def test_glue_wrap_build_exports_wrappers(tmp_path):
+    """-DSVTME_GLUE_WRAP (the --wrap link of oracle/encoder.mk) defines the two
+    wrappers and calls through to the encoder's own functions."""
+    obj = str(tmp_path / "glue_wrap.o")
+    r = subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-DSVTME_GLUE_WRAP", "-DARCH_X86_64=1",
+                        "-DEN_AVX512_SUPPORT=0", "-c", "-o", obj, GLUE] + _incs(), capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
+    syms = subprocess.run(["nm", obj], capture_output=True, text=True).stdout
+    for s in ("T __wrap_svt_aom_motion_estimation_b64", "T __wrap_svt_aom_downsample_filtering_input_picture",
+              "U __real_svt_aom_motion_estimation_b64", "U __real_svt_aom_downsample_filtering_input_picture"):
+        assert s in syms, s
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference headers only in the build container")
+def test_picture_job_mode_registers_no_rtcd_pointer():
+    """Picture-job mode leaves every rtcd pointer to the encoder (mode decision
+    keeps its CPU svt_pme_sad_loop_kernel / sad_16b_kernel, aom_dsp_rtcd.c:501-528):
+    only svt_aom_setup_rtcd_hip_parity assigns them, and nothing in the job path
+    calls it."""
+    src = open(GLUE).read()
+    body = src[src.index("void svt_aom_setup_rtcd_hip_parity(void) {"):]
+    body = body[:body.index("\n}\n")]
+    job_path = src[src.index("Picture-job service of the SB function"):]
+    for ptr in ("svt_pme_sad_loop_kernel", "sad_16b_kernel", "svt_sad_loop_kernel ", "svt_nxm_sad_kernel "):
+        assert f"{ptr.strip()} " in body
+        assert f"{ptr.strip()} =" not in job_path and "svt_aom_setup_rtcd_hip_parity(" not in job_path
 
 
 def test_integration_doc_names_real_pointers():
