@@ -134,6 +134,9 @@ def main():
                     help="N > 1 record exchange: each picture's chunks to its owner rank (all_to_all_single), or "
                          "every picture to every rank (all_gather_into_tensor)")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="target CPU-seconds of the baseline sample")
+    ap.add_argument("--band-steps", type=int, default=30,
+                    help="steps of the band_8k sub-measurement (one 8K p8 picture split over the N GPUs, SURVEY.md "
+                         "8(e)); 0 skips it")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -169,7 +172,7 @@ def main():
         t0 = 8 + PICTURE_STRIDE * p
         for o in offs:
             t = t0 + o
-            gpu.upload(t, syn.frame10(t) if wl["ten_bit"] else syn.frame(t))
+            gpu.upload(t, W.workload_frame(name, syn, t))
         job = W.workload_job(name, base=PICTURE_STRIDE * p, sb_begin=begin, sb_count=count)
         jobs.append(job)
     R = S.ref_slots(jobs[0])
@@ -281,7 +284,7 @@ def main():
     # host memory (pageable numpy, and a pinned buffer) + pyramid build, synchronous
     upload = None
     if rank == 0 and not args.no_upload:
-        frame = syn.frame10(8) if wl["ten_bit"] else syn.frame(8)
+        frame = W.workload_frame(name, syn, 8)
         fn = gpu.lib.svtme_picture_upload_10bit if wl["ten_bit"] else gpu.lib.svtme_picture_upload
 
         def t_up(ptr, reps=10):
@@ -367,6 +370,18 @@ def main():
         traffic = int(prof["hbm_bytes_per_launch"])
     absdiff = W.ABSDIFF_PER_SB_REF[wl["windows"]] * R * sbs_launch
     sad_rate = absdiff / (device_ms * 1e-3) / 1e12
+    # measured DRAM rate of the dominant kernel: rocprofv3 HBM bytes per launch (same code) / its duration
+    dram = None
+    if traffic and dom:
+        dram_gbps = traffic / (stages[dom]["avg_ms"] * 1e-3) / 1e9
+        dram = {"gbps": round(dram_gbps, 1), "frac": round(dram_gbps / HBM_PEAK_GBPS, 4),
+                "note": "measured HBM bytes per launch (traffic) / the kernel's average duration: the share of "
+                        "the 8 TB/s the kernel really draws; the algorithmic frac counts every search window "
+                        "as read from HBM, most of which neighbouring SBs' workgroups find in L2 / MALL"}
+
+    band = None
+    if args.band_steps > 0:
+        band = band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, args.band_steps, fence)
 
     recs = None
     if world == 1:
@@ -389,7 +404,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (integer PCG32 panning texture, SURVEY.md 8(d)); pyramids resident in HBM",
+            "data": ("synthetic (integer PCG32 texture, SURVEY.md 8(d); " +
+                     ("per-region motion and noise" if wl.get("content") == "mixed" else "global pan") +
+                     "); pyramids resident in HBM"),
             "config": {"workload": wl["desc"], "name": name, "sbs_per_picture": n_sb, "refs": R,
                        "pictures_per_step": P,
                        "lanes": NL,
@@ -420,7 +437,12 @@ def main():
                          "bytes_per_launch": bytes_launch, "sbs_per_launch": sbs_launch,
                          "dominant": dom, "stages": stages, "traffic_source": prof_path,
                          "valu_sad": {"achieved_T_absdiff_s": round(sad_rate, 2), "peak": SAD_PEAK_T,
-                                      "frac": round(sad_rate / SAD_PEAK_T, 4)}},
+                                      "frac": round(sad_rate / SAD_PEAK_T, 4)},
+                         "algorithmic_frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "dram": dram,
+                         "limiter": "issue / latency: neither HBM (dram.frac) nor the SAD units (valu_sad.frac) "
+                                    "are saturated; frac is the SURVEY.md 8(d) algorithmic-bytes rate"},
+            "band_8k": band,
             "cpu_baseline": cpu_baseline,
             "parity_vs_cpu": parity,
         }
@@ -428,6 +450,70 @@ def main():
     gpu.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, steps, fence):
+    """SURVEY.md 8(e) / BASELINE configs[4]: ONE 7680x4320 p8 picture, its SBs
+    split in N equal chunks (D.BandSplit), rank r searches chunk r in one launch
+    and one all_gather_into_tensor over RCCL gives every rank the picture's
+    records. Timed separately: the search alone, the all-gather alone, and the
+    dependent pair (gather after the search, next search after the gather has
+    read the chunk); strong scaling: SBs of the picture / the pair's time."""
+    import torch
+
+    name = "8k_p8"
+    wl = W.WORKLOADS[name]
+    base = 800000
+    frames = W.workload_frames(name)
+    for t, f in frames.items():  # every rank holds the full pyramids (pre-HME reaches ~1400 rows)
+        gpu.upload(base + t, f)
+    n_sb = S.sb_total(wl["w"], wl["h"])
+    R = len(wl["l0"]) + len(wl["l1"])
+    split = D.BandSplit(n_sb, R, S.REF_RECORD_DTYPE.itemsize, world, rank)
+    job = W.workload_job(name, base=base, sb_begin=split.begin, sb_count=split.count)
+    local = torch.zeros(split.chunk_bytes, dtype=torch.uint8, device=dev)
+    out = torch.empty(world * split.chunk_bytes, dtype=torch.uint8, device=dev) if world > 1 else None
+    searched, gathered = torch.cuda.Event(), torch.cuda.Event()
+
+    def search():
+        gpu.submit_batch_device([job], [local.data_ptr()], lane=0)
+
+    def gather():
+        searched.record(ext)
+        comm.wait_event(searched)
+        split.exchange(local, out, dist, stream=comm)
+        gathered.record(comm)
+        ext.wait_event(gathered)  # the next search rewrites the chunk the gather reads
+
+    def timed(fn):
+        fence()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        fence()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        if world > 1:
+            t = torch.tensor([ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            ms = float(t.item())
+        return ms
+
+    for _ in range(3):
+        search()
+        if world > 1:
+            gather()
+    search_ms = timed(search)
+    gather_ms = timed(lambda: split.exchange(local, out, dist, stream=comm)) if world > 1 else 0.0
+    pair_ms = timed(lambda: (search(), gather())) if world > 1 else search_ms
+    for t in frames:
+        gpu.release(base + t)
+    return {"workload": wl["desc"] + ", one picture per step split over the GPUs", "sbs_per_picture": n_sb,
+            "sbs_per_rank": split.slots, "refs": R, "steps": steps,
+            "search_ms": round(search_ms, 4), "allgather_ms": round(gather_ms, 4), "step_ms": round(pair_ms, 4),
+            "value": round(n_sb / (pair_ms * 1e-3), 1), "unit": "SB/s", "scaling": "strong",
+            "allgather_bytes_per_rank": split.gather_bytes_in,
+            "note": "value = SBs of the picture / (search + dependent all_gather_into_tensor), max over ranks; "
+                    "search_ms and allgather_ms timed alone"}
 
 
 def cpu_leg(S, W, name, gpu_recs, cpu_seconds):

@@ -10,6 +10,12 @@
  *            (pcg() % 9) - 4 from PCG32(seed 0x5EED0001 + t + 1, stream 2) in
  *            raster order, clamped to [0, 255];
  *   10-bit : p10 = (y8 << 2) | ((x + y) & 3), so the MSB plane equals y8.
+ *   mixed  : (svtme_synth_frame_mixed_from_texture) the picture is tiled in
+ *            256x256 regions, each with its own motion of the same texture
+ *            (static, slow, the global pan, other directions, fast, beyond the
+ *            search range) or fresh noise every frame, so early exits, pruning
+ *            and search centres vary across the picture (bench --workload
+ *            4k_p8_mixed); the +-4 noise as above.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -108,4 +114,41 @@ void svtme_synth_frame10_from_texture(const uint8_t *tex, uint32_t w, uint32_t h
         for (uint32_t x = 0; x < w; x++)
             out[(size_t)y * stride + x] = (uint16_t)((y8[(size_t)y * w + x] << 2) | ((x + y) & 3));
     free(y8);
+}
+
+/* region motion classes of the mixed content: (vx, vy) per frame; 0x7FFF = noise */
+static const int16_t k_mixed_motion[8][2] = {{0, 0}, {1, 1}, {5, 3}, {-6, 2}, {14, -8}, {36, 20}, {-72, 40},
+                                             {0x7FFF, 0}};
+
+static uint32_t mix32(uint32_t v) { /* integer hash of a region index */
+    v ^= v >> 16;
+    v *= 0x7FEB352Du;
+    v ^= v >> 15;
+    v *= 0x846CA68Bu;
+    v ^= v >> 16;
+    return v;
+}
+
+static uint32_t wrap(int64_t v, uint32_t n) { return (uint32_t)(((v % (int64_t)n) + (int64_t)n) % (int64_t)n); }
+
+/* frame t of the mixed-motion content, 8-bit */
+void svtme_synth_frame_mixed_from_texture(const uint8_t *tex, uint32_t w, uint32_t h, uint32_t t, uint8_t *out,
+                                          uint32_t stride) {
+    uint32_t tw, th;
+    svtme_synth_texture_size(w, h, &tw, &th);
+    pcg32 rng, nrng;
+    pcg32_seed(&rng, SYNTH_SEED + t + 1, 2);
+    pcg32_seed(&nrng, SYNTH_SEED ^ (0x9E3779B9u * (t + 1)), 3);
+    for (uint32_t y = 0; y < h; y++)
+        for (uint32_t x = 0; x < w; x++) {
+            const uint32_t k = mix32((x >> 8) * 131u + (y >> 8) * 7919u + 17u) & 7u;
+            const uint32_t n = pcg32_next(&rng) % 9, z = pcg32_next(&nrng) >> 24;
+            int v;
+            if (k_mixed_motion[k][0] == 0x7FFF)
+                v = (int)z;
+            else
+                v = tex[(size_t)wrap((int64_t)y + (int64_t)k_mixed_motion[k][1] * t, th) * tw +
+                        wrap((int64_t)x + (int64_t)k_mixed_motion[k][0] * t, tw)] + (int)n - 4;
+            out[(size_t)y * stride + x] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+        }
 }

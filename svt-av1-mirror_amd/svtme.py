@@ -265,6 +265,8 @@ def load_synth():
                                                        C.c_uint32]
         lib.svtme_synth_frame10_from_texture.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
                                                          C.c_uint32]
+        lib.svtme_synth_frame_mixed_from_texture.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                                             C.c_void_p, C.c_uint32]
         lib._svtme_protos = True
     return lib
 
@@ -286,6 +288,13 @@ class Synth:
     def frame(self, t: int) -> np.ndarray:
         out = np.empty((self.h, self.w), np.uint8)
         load_synth().svtme_synth_frame_from_texture(self.tex.ctypes.data, self.w, self.h, t, out.ctypes.data, self.w)
+        return out
+
+    def frame_mixed(self, t: int) -> np.ndarray:
+        """Per-region motion (static .. beyond the search range) and noise regions."""
+        out = np.empty((self.h, self.w), np.uint8)
+        load_synth().svtme_synth_frame_mixed_from_texture(self.tex.ctypes.data, self.w, self.h, t, out.ctypes.data,
+                                                          self.w)
         return out
 
     def frame10(self, t: int) -> np.ndarray:

@@ -41,6 +41,30 @@ def chunk_slots(n_sb: int, world: int) -> int:
     return -(-n_sb // world)
 
 
+class BandSplit:
+    """One picture's SBs over the ranks: rank r searches the
+    equal chunk r (sb_chunk) into a local buffer of `chunk_bytes`; one
+    all_gather_into_tensor assembles the picture's records, in raster SB
+    order, in the first `picture_bytes` of every rank's gathered buffer."""
+
+    def __init__(self, n_sb: int, refs: int, record_bytes: int, world: int, rank: int):
+        self.n_sb, self.world, self.rank = n_sb, world, rank
+        self.slots = chunk_slots(n_sb, world)
+        self.begin, self.count = sb_chunk(n_sb, rank, world)
+        self.chunk_bytes = self.slots * refs * record_bytes
+        self.picture_bytes = n_sb * refs * record_bytes
+        # bytes each rank receives per picture (its own chunk is already local)
+        self.gather_bytes_in = (world - 1) * self.chunk_bytes
+
+    def exchange(self, d_local, d_out, dist, stream=None):
+        if self.world == 1:
+            return d_local
+        return gather_chunks_device(d_local, d_out, dist, stream=stream)
+
+    def picture(self, d_out):
+        return d_out[: self.picture_bytes]
+
+
 def gather_chunks_device(d_local, d_out, dist, group=None, stream=None):
     """All-gather the ranks' record chunks between device buffers.
 

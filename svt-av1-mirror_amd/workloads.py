@@ -8,6 +8,7 @@ exactly the one whose records are pinned against the reference.
   4k_p8       configs[2]: 3840x2160 p8, 4 refs (L0 d=1,2; L1 d=1,2) -- the headline
   4k10_p6     configs[3]: 3840x2160 10-bit p6 (MSB plane), refs as the encoder (1+1)
   8k_p8       configs[4]: 7680x4320 p8, 4 refs (sharded over GPUs in bench --mode band)
+  4k_p8_mixed configs[2] on mixed-motion content (per-region motion and noise)
   ra360_p12   configs[0]: 640x360 p12, 30 pictures random access (ra_sequence)
 
 Inputs are the integer PCG32 panning texture of SURVEY.md 8(d): current picture
@@ -27,6 +28,12 @@ WORKLOADS = {
                     desc="3840x2160 10-bit preset 6 (8-bit MSB search), 2 refs, open-loop ME"),
     "8k_p8": dict(w=7680, h=4320, mode=8, tl=1, l0=(7, 6), l1=(9, 10), windows="p8", ten_bit=False,
                   desc="7680x4320 8-bit preset 8, 4 refs, open-loop ME"),
+    # configs[2] on content whose motion varies across the picture (static regions take the zz early
+    # exits, fast / out-of-range / noise regions the pruning and the worst-case windows)
+    "4k_p8_mixed": dict(w=3840, h=2160, mode=8, tl=1, l0=(7, 6), l1=(9, 10), windows="p8", ten_bit=False,
+                        content="mixed",
+                        desc="3840x2160 8-bit preset 8, 4 refs (L0 d=1,2; L1 d=1,2), open-loop ME, mixed-motion "
+                             "content (256x256 regions: static / slow / pan / fast / beyond range / noise)"),
 }
 # the bench accepted "1080p_p8" in round 1
 WORKLOADS["1080p_p8"] = WORKLOADS["1080p_sa64"]
@@ -41,12 +48,20 @@ def bytes_per_sb(windows: str, refs: int) -> int:
     return 2688 + refs * (WINDOW_BYTES[windows] + 680)
 
 
+def workload_frame(name: str, syn: "S.Synth", t: int):
+    """Picture t of the workload's content (uint16 plane for 10-bit)."""
+    wl = WORKLOADS[name]
+    if wl.get("content") == "mixed":
+        return syn.frame_mixed(t)
+    return syn.frame10(t) if wl["ten_bit"] else syn.frame(t)
+
+
 def workload_frames(name: str) -> dict:
     """{t: luma plane} of the workload (uint16 planes for 10-bit)."""
     wl = WORKLOADS[name]
     syn = S.Synth(wl["w"], wl["h"])
     ts = sorted(set((8,) + tuple(wl["l0"]) + tuple(wl["l1"])))
-    return {t: (syn.frame10(t) if wl["ten_bit"] else syn.frame(t)) for t in ts}
+    return {t: workload_frame(name, syn, t) for t in ts}
 
 
 def workload_controls(name: str) -> S.Controls:

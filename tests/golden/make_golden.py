@@ -24,8 +24,8 @@ stores inputs-as-parameters plus expected outputs:
                      access) as per-picture checksums and full records
 
 Run from the repo root in the build container (needs /root/reference for the
-library build only): python tests/golden/make_golden.py [tf|configs|rtcd]
-(tf / configs / rtcd: only those fixtures)
+library build only): python tests/golden/make_golden.py [tf|configs [name ...]|rtcd]
+(tf / configs / rtcd: only those fixtures; configs name ...: only those configurations)
 """
 import hashlib
 import json
@@ -152,15 +152,22 @@ def tf_golden():
 CFG_STRIDE = 7  # sampled SBs of the full-size configurations (every 7th SB: all rows and columns)
 
 
-def configs_golden():
+CFG_NAMES = ("1080p_sa64", "4k_p8", "4k10_p6", "8k_p8", "4k_p8_mixed")
+
+
+def configs_golden(only=None):
     """Full-size BASELINE.json configurations through the reference's own ME
     (AVX2 kernels, as the encoder runs at --asm avx2; the C kernels must agree
-    on the sampled SBs of every configuration)."""
+    on the sampled SBs of every configuration). only: regenerate just these
+    configurations and keep the others' entries of configs.json."""
     import workloads as W
 
     ref = S.load_ref()
     meta = {"stride": CFG_STRIDE, "configs": {}, "ra360_p12": []}
-    for name in ("1080p_sa64", "4k_p8", "4k10_p6", "8k_p8"):
+    if only:
+        with open(os.path.join(HERE, "configs.json")) as fh:
+            meta = json.load(fh)
+    for name in (only or CFG_NAMES):
         wl = W.WORKLOADS[name]
         frames = W.workload_frames(name)
         pyr = {t: S.build_host_pyramid(f, "ref") for t, f in frames.items()}
@@ -184,6 +191,10 @@ def configs_golden():
                                  "searched": int(recs["searched"].sum()), "desc": wl["desc"],
                                  "pyramid_sha256": digest(pyr[8].full)}
         print(name, recs.shape, meta["configs"][name]["checksum"][:16], flush=True)
+    if only:
+        with open(os.path.join(HERE, "configs.json"), "w") as fh:
+            json.dump(meta, fh, indent=1)
+        return
     # configs[0]: 640x360 preset 12, 30 pictures random access
     w, h = 640, 360
     syn = S.Synth(w, h)
@@ -235,6 +246,8 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["configs"]:
         configs_golden()
+    elif sys.argv[1:2] == ["configs"]:
+        configs_golden(sys.argv[2:])
     elif sys.argv[1:] == ["rtcd"]:
         rtcd_golden()
     else:

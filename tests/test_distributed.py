@@ -89,21 +89,22 @@ def _chunk_worker(rank, world, port, out_path, n_pics):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     w, h = 200, 136  # 4 x 3 = 12 SBs: chunks of 6 at world 2 (5 + pad at world 3 would be short)
     n_sb = S.sb_total(w, h)
-    slots = D.chunk_slots(n_sb, world)
+    R = 3
+    # the split bench.py's band_8k leg uses (D.BandSplit: equal chunks, one all-gather)
+    split = D.BandSplit(n_sb, R, S.REF_RECORD_DTYPE.itemsize, world, rank)
     outs = []
     for p in range(n_pics):
         ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
-        begin, count = D.sb_chunk(n_sb, rank, world)
-        R = 3
         rec_bytes = S.REF_RECORD_DTYPE.itemsize * R
-        local = torch.zeros(slots * rec_bytes, dtype=torch.uint8)
-        if count:
+        local = torch.zeros(split.chunk_bytes, dtype=torch.uint8)
+        if split.count:
             recs, _ = S.run_case_checker("pan", w, h, ctrl, 8 + p, (7 + p, 6 + p), (9 + p,), 1, checker="oracle",
-                                         nthreads=1, sb_begin=begin, sb_count=count)
-            local[: count * rec_bytes] = torch.from_numpy(recs.view(np.uint8).reshape(-1).copy())
-        out = torch.empty(world * slots * rec_bytes, dtype=torch.uint8)
-        D.gather_chunks_device(local, out, dist)
-        outs.append(out[: n_sb * rec_bytes].numpy().copy())
+                                         nthreads=1, sb_begin=split.begin, sb_count=split.count)
+            local[: split.count * rec_bytes] = torch.from_numpy(recs.view(np.uint8).reshape(-1).copy())
+        out = torch.empty(world * split.chunk_bytes, dtype=torch.uint8)
+        split.exchange(local, out, dist)
+        assert split.picture_bytes == n_sb * rec_bytes
+        outs.append(split.picture(out).numpy().copy())
     if rank == 0:
         np.save(out_path, np.stack(outs))
     dist.barrier()
