@@ -27,7 +27,7 @@ def main():
     jobs = []
     for p in range(P):
         for t in sorted(set((8,) + tuple(wl["l0"]) + tuple(wl["l1"]))):
-            gpu.upload(t + 32 * p, syn.frame10(t) if wl["ten_bit"] else syn.frame(t))
+            gpu.upload(t + 32 * p, W.workload_frame(name, syn, t))
         jobs.append(W.workload_job(name, base=32 * p))
     n_sb = S.sb_total(wl["w"], wl["h"])
     R = S.ref_slots(jobs[0])
