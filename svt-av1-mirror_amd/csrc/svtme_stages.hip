@@ -663,113 +663,68 @@ __device__ __forceinline__ void dec_zz(Dec &d, const svtme_job &job, const SbGeo
     }
 }
 
-// pre-HME decisions of list l (check_prehme_early_exit :1693-1719, the list-1
-// mirror :1740-1760, prehme_b64 :1722-1796), one wavefront; lane = ref * 2 + region
-__device__ __forceinline__ void dec_prehme_list(Dec &d, const svtme_job &job, uint32_t vmask, int l) {
-    const svtme_controls &c = job.ctrl;
-    const int lane          = threadIdx.x & 63;
-    const int r = lane >> 1, sr = lane & 1, s = l * 4 + r;
-    if (lane < 8 && slot_valid(vmask, s) && tl_or_l0(job, l)) {
-        PreHme &p = d.ph[s][sr];
-        bool done = false;
-        if (c.me_early_exit_th && d.zz[s] < c.me_early_exit_th) { // check_prehme_early_exit
-            p.col = p.row = 0;
-            p.sad   = 0;
-            p.valid = 1;
-            done    = true;
-        }
-        if (!done && c.prehme_l1_early_exit && l == 1) {
-            const PreHme &z = d.ph[r][sr];
-            if (z.valid && ((z.sad < (32 * 32)) || ((absi(z.col) < 16) && (absi(z.row) < 16)))) {
-                p.col   = (int16_t)-z.col;
-                p.row   = (int16_t)-z.row;
-                p.sad   = z.sad;
-                p.valid = 1;
-                done    = true;
-            }
-        }
-        if (!done && !d.do_ref[s]) {
-            p.col = p.row = 0;
-            p.sad = U32MAX;
-            done  = true;
-        }
-        if (!done) { // searched in stage A
-            const ARes &a = d.a[SVTME_A_PH + s * 2 + sr];
-            p.sad         = a.sad;
-            p.col         = a.x;
-            p.row         = a.y;
-            p.valid       = 1;
-            p.performed   = 1;
-        }
-    }
-    wave_lds_fence();
-}
-
-// which list-1 pre-HME regions dec_prehme_list(1) will take from a search (the
-// others exit early or mirror list 0): lane = ref * 2 + region; list 0 decided
-__device__ __forceinline__ bool prehme_l1_searched(const Dec &d, const svtme_job &job, uint32_t vmask) {
-    const svtme_controls &c = job.ctrl;
-    const int lane          = threadIdx.x & 63;
-    const int r = lane >> 1, sr = lane & 1, s = 4 + r;
-    if (!(lane < 8 && slot_valid(vmask, s) && tl_or_l0(job, 1)))
-        return false;
-    if (c.me_early_exit_th && d.zz[s] < c.me_early_exit_th)
-        return false;
-    if (c.prehme_l1_early_exit) {
-        const PreHme &z = d.ph[r][sr];
-        if (z.valid && ((z.sad < (32 * 32)) || ((absi(z.col) < 16) && (absi(z.row) < 16))))
-            return false;
-    }
-    return d.do_ref[s] != 0;
-}
-
-// pre-HME based reference pruning after both lists (prehme_b64 :1772-1796), one wavefront
-__device__ __forceinline__ void dec_prehme_prune(Dec &d, const svtme_job &job, uint32_t vmask) {
-    const svtme_controls &c = job.ctrl;
-    const int lane          = threadIdx.x & 63;
-    uint32_t m  = U32MAX;
-    const int s = lane;
-    if (slot_valid(vmask, s)) {
-        if (tl_or_l0(job, s >> 2)) {
-            m = (uint32_t)min_u64(d.ph[s][0].sad, d.ph[s][1].sad);
-        } else { // list 1 at the base layer mirrors list 0
-            for (int k = 0; k < 2; k++) {
-                d.ph[s][k].col = (int16_t)-d.ph[s & 3][k].col;
-                d.ph[s][k].row = (int16_t)-d.ph[s & 3][k].row;
-                d.ph[s][k].sad = d.ph[s & 3][k].sad;
-            }
-        }
-    }
-    const uint32_t best = wave_min_u32(m);
-    if (job.temporal_layer_index > 0 && best < c.phme_sad_th && slot_valid(vmask, s) && (s & 3) > 0 &&
-        d.do_ref[s] && (uint32_t)((m - best) * 100u) > (uint32_t)(c.phme_sad_pct * best))
-        d.do_ref[s] = 0;
-    wave_lds_fence();
-}
-
 // pre-HME decisions (motion_estimation.c:1693-1796), list 0 then list 1, one wavefront
 __device__ __forceinline__ void dec_prehme(Dec &d, const svtme_job &job, uint32_t vmask) {
-    if (job.ctrl.prehme_enable) {
-        for (int l = 0; l < job.num_lists; l++) dec_prehme_list(d, job, vmask, l);
-        dec_prehme_prune(d, job, vmask);
-    }
-}
-
-// whether dec_l0 takes slot s's level-0 result from a search (the reference runs
-// hme_level_0 for it, :1922-1977); lane = slot; zz / pre-HME decided
-__device__ __forceinline__ bool l0_searched(const Dec &d, const svtme_job &job, uint32_t vmask) {
     const svtme_controls &c = job.ctrl;
-    const int s             = threadIdx.x & 63;
-    if (!(slot_valid(vmask, s) && tl_or_l0(job, s >> 2)))
-        return false;
-    if (c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2))
-        return false;
-    if (c.prev_me_stage_based_exit_th) {
-        const int k = d.ph[s][0].sad <= d.ph[s][1].sad ? 0 : 1;
-        if (d.ph[s][k].performed && d.ph[s][k].sad < (c.prev_me_stage_based_exit_th >> 4))
-            return false;
+    const int lane          = threadIdx.x & 63;
+    const int nl            = job.num_lists;
+    if (c.prehme_enable) {
+        for (int l = 0; l < nl; l++) {
+            const int r = lane >> 1, sr = lane & 1, s = l * 4 + r;
+            if (lane < 8 && slot_valid(vmask, s) && tl_or_l0(job, l)) {
+                PreHme &p = d.ph[s][sr];
+                bool done = false;
+                if (c.me_early_exit_th && d.zz[s] < c.me_early_exit_th) { // check_prehme_early_exit
+                    p.col = p.row = 0;
+                    p.sad   = 0;
+                    p.valid = 1;
+                    done    = true;
+                }
+                if (!done && c.prehme_l1_early_exit && l == 1) {
+                    const PreHme &z = d.ph[r][sr];
+                    if (z.valid && ((z.sad < (32 * 32)) || ((absi(z.col) < 16) && (absi(z.row) < 16)))) {
+                        p.col   = (int16_t)-z.col;
+                        p.row   = (int16_t)-z.row;
+                        p.sad   = z.sad;
+                        p.valid = 1;
+                        done    = true;
+                    }
+                }
+                if (!done && !d.do_ref[s]) {
+                    p.col = p.row = 0;
+                    p.sad = U32MAX;
+                    done  = true;
+                }
+                if (!done) { // searched in stage A
+                    const ARes &a = d.a[SVTME_A_PH + s * 2 + sr];
+                    p.sad         = a.sad;
+                    p.col         = a.x;
+                    p.row         = a.y;
+                    p.valid       = 1;
+                    p.performed   = 1;
+                }
+            }
+            wave_lds_fence();
+        }
+        uint32_t m  = U32MAX;
+        const int s = lane;
+        if (slot_valid(vmask, s)) {
+            if (tl_or_l0(job, s >> 2)) {
+                m = (uint32_t)min_u64(d.ph[s][0].sad, d.ph[s][1].sad);
+            } else { // list 1 at the base layer mirrors list 0
+                for (int k = 0; k < 2; k++) {
+                    d.ph[s][k].col = (int16_t)-d.ph[s & 3][k].col;
+                    d.ph[s][k].row = (int16_t)-d.ph[s & 3][k].row;
+                    d.ph[s][k].sad = d.ph[s & 3][k].sad;
+                }
+            }
+        }
+        const uint32_t best = wave_min_u32(m);
+        if (job.temporal_layer_index > 0 && best < c.phme_sad_th && slot_valid(vmask, s) && (s & 3) > 0 &&
+            d.do_ref[s] && (uint32_t)((m - best) * 100u) > (uint32_t)(c.phme_sad_pct * best))
+            d.do_ref[s] = 0;
+        wave_lds_fence();
     }
-    return d.do_ref[s] != 0;
 }
 
 // HME level 0 decisions (motion_estimation.c:1906-2036), one wavefront
@@ -1157,8 +1112,8 @@ struct HSrch {             // one 1/16-resolution search (pre-HME region or HME-
     int16_t ylast;         // last plane-row offset a tile of this search may read
     uint32_t ncm;          // magic_u32(ncols): tile index / ncols by multiply-high
     uint8_t sh, skip, id;  // byte offset of position 0; odd rows only; ARes index
-    uint8_t need;          // bit of HmeA::need: pre-HME slot * 2 + region, HME-L0 16 + slot
-    uint8_t tt;            // position rows per tile: HT16, or 2 (the HME-L0 round, see k_hme A1)
+    uint8_t need;          // bit of HmeSh::need (slot * 2 + (L0 ? 1 : 0))
+    uint8_t tt;            // position rows per tile: HT16, or 2 (the HME-L0 group, see k_hme A1)
 };
 struct HSrch1 {            // one HME-L1 refinement search
     const uint8_t *a0;
@@ -2756,13 +2711,10 @@ struct HmeA { // state of phases A0 .. B
     unsigned long long key[SVTME_A_N]; // search minima by ARes index
     int16_t kxo[SVTME_A_N], kyo[SVTME_A_N];
     uint32_t zzacc[8];
-    uint32_t need;                     // bit slot * 2 + region: pre-HME searched, 16 + slot: HME-L0 searched
+    uint32_t need;                     // bit slot * 2: pre-HME searched, slot * 2 + 1: HME-L0 searched
     HSrch srch[48];
-    int32_t nsrch;
-    // the A1 rounds (pre-HME list 0, pre-HME list 1, HME-L0): tile ranges [rb, re)
-    // (64-aligned starts), and whether the HME-L0 round takes 2-row tiles
-    int32_t rb[3], re[3];
-    int32_t l0_t2;
+    int32_t nsrch, nitems;
+    int32_t nitems3, base2; // end of the HT16-row tiles; first item of the 2-row group (64-aligned)
     unsigned long long key1[32];
     int16_t x1o[32], y1o[32];
     HSrch1 s1[32];
@@ -2832,7 +2784,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     const int kh  = (int)(G.bh >> 2) >> 1; // 1/16 block rows (sub)
     const int kh1 = (int)(G.bh >> 2);      // 1/4 block rows (sub): (bh / 2) / 2
     const bool zz_on = c.me_early_exit_th || c.me_safe_limit_zz_th;
-    const bool hsub  = c.hme_search_method != SVTME_FULL_SAD_SEARCH; // true on this path
     HME_STAMP(0);
 
     // ---- phase 0 (independent work of all waves):
@@ -2860,12 +2811,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                 prehme_area(P, sox, soy, aw, ah, &xo, &yo, &sw, &shh);
                 skip   = c.prehme_skip_search_line != 0; // compute_sad_c.c:74 (16 wide, <= 16 rows)
                 e.id   = (uint8_t)(SVTME_A_PH + s * 2 + k);
-                e.need = (uint8_t)(s * 2 + k);
+                e.need = (uint8_t)(s * 2);
             } else { // hme_level_0 (motion_estimation.c:835-889)
                 hme_l0_rect(c, P, sox, soy, aw, ah, (k - 2) >> 1, (k - 2) & 1, &xo, &yo, &sw, &shh);
                 skip   = false;
                 e.id   = (uint8_t)(SVTME_A_L0 + s * 4 + (k - 2));
-                e.need = (uint8_t)(16 + s);
+                e.need = (uint8_t)(s * 2 + 1);
             }
             sh.u.a.kxo[e.id]    = xo;
             sh.u.a.kyo[e.id]    = yo;
@@ -2895,38 +2846,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                 mk = true;
             }
         }
-        // Three rounds of tiles, each a contiguous 64-aligned item range: the
-        // pre-HME regions of list 0, those of list 1 (run only where list 1 does
-        // not take list 0's result, check_prehme_early_exit :1740-1760), and the
-        // HME-L0 quadrants of the references the pre-HME pruning keeps (:1772-1796).
-        // The reference never searches what these decisions skip, so neither does
-        // the GPU. Tile shapes: a wavefront's qsad count is its tiles' row count x
-        // 64 lanes, so the HME-L0 round (few rows per parity, e.g. 2 at p8, wasting a
-        // third of a 3-row tile) takes 2-row tiles when that needs fewer wavefront-rows
-        const int cls   = k < 2 ? l : 2;
-        const int n3_l0 = (int)wave_sum_u32(mk && cls == 2 ? (uint32_t)items3 : 0u);
-        const int n2_l0 = (int)wave_sum_u32(mk && cls == 2 ? (uint32_t)items2 : 0u);
-        const bool l0t2 = ((n2_l0 + 63) / 64) * 2 < ((n3_l0 + 63) / 64) * HT16;
-        const bool t2   = mk && cls == 2 && l0t2;
-        const int items = t2 ? items2 : items3;
-        e.tt            = (uint8_t)(t2 ? 2 : HT16);
-        int tot0, tot1, tot2;
-        const int k0 = wave_compact(mk && cls == 0, &tot0), k1 = wave_compact(mk && cls == 1, &tot1),
-                  k2 = wave_compact(mk && cls == 2, &tot2);
-        const int i0 = wave_incl_scan(mk && cls == 0 ? items : 0), i1 = wave_incl_scan(mk && cls == 1 ? items : 0),
-                  i2 = wave_incl_scan(mk && cls == 2 ? items : 0);
-        const int N0 = (int)lane63((uint32_t)i0), N1 = (int)lane63((uint32_t)i1), N2 = (int)lane63((uint32_t)i2);
-        const int b1 = (N0 + 63) & ~63, b2 = b1 + ((N1 + 63) & ~63);
+        // Tile shapes: a wavefront's qsad count is its tiles' row count x 64 lanes, so
+        // the HME-L0 quadrants (few rows per parity, e.g. 2 at p8, wasting a third of
+        // a 3-row tile) take 2-row tiles in wavefronts of their own when that needs
+        // fewer wavefront-rows: the 3-row group first, the 2-row group from the next
+        // multiple of 64 items
+        const bool l0    = k >= 2;
+        const int n3_pre = (int)wave_sum_u32(mk && !l0 ? (uint32_t)items3 : 0u);
+        const int n3_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items3 : 0u);
+        const int n2_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items2 : 0u);
+        const bool split = ((n3_pre + 63) / 64) * HT16 + ((n2_l0 + 63) / 64) * 2 < ((n3_pre + n3_l0 + 63) / 64) * HT16;
+        const bool t2    = mk && split && l0;
+        const int items  = t2 ? items2 : items3;
+        e.tt             = (uint8_t)(t2 ? 2 : HT16);
+        int n3s, n2s;
+        const int k3 = wave_compact(mk && !t2, &n3s), k2 = wave_compact(t2, &n2s);
+        const int i3 = wave_incl_scan(mk && !t2 ? items : 0), i2 = wave_incl_scan(t2 ? items : 0);
+        const int N3 = (int)lane63((uint32_t)i3), N2 = (int)lane63((uint32_t)i2);
+        const int base2 = (N3 + 63) & ~63;
         if (mk) {
-            e.item0 = cls == 0 ? i0 - items : cls == 1 ? b1 + i1 - items : b2 + i2 - items;
-            sh.u.a.srch[cls == 0 ? k0 : cls == 1 ? tot0 + k1 : tot0 + tot1 + k2] = e;
+            e.item0                          = t2 ? base2 + i2 - items : i3 - items;
+            sh.u.a.srch[t2 ? n3s + k2 : k3] = e;
         }
         if (lane == 0) {
-            sh.u.a.nsrch = tot0 + tot1 + tot2;
-            sh.u.a.rb[0] = 0, sh.u.a.re[0] = N0;
-            sh.u.a.rb[1] = b1, sh.u.a.re[1] = b1 + N1;
-            sh.u.a.rb[2] = b2, sh.u.a.re[2] = b2 + N2;
-            sh.u.a.l0_t2 = l0t2;
+            sh.u.a.nsrch   = n3s + n2s;
+            sh.u.a.nitems3 = N3;
+            sh.u.a.base2   = base2;
+            sh.u.a.nitems  = N2 ? base2 + N2 : N3;
         }
     } else {
         if (zz_on) {
@@ -2999,11 +2945,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             d.a[SVTME_A_ZZ + lane] = ARes{sh.u.a.zzacc[lane], 0, 0};
         wave_lds_fence();
         dec_zz(d, job, G, vmask);
-        // round 0 runs the pre-HME regions of list 0 the reference searches
-        // (lane = slot * 2 + region): not exited early on the zz SAD, not pruned
         const int s    = lane >> 1;
-        const bool nd  = lane < 8 && slot_valid(vmask, s) && d.do_ref[s] &&
-                        !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th);
+        const bool act = lane < 16 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && d.do_ref[s];
+        const bool nd  = act && ((lane & 1) ? !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2))
+                                            : !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th));
         const unsigned long long m = __ballot(nd);
         if (lane == 0)
             sh.u.a.need = (uint32_t)m;
@@ -3011,36 +2956,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     __syncthreads();
     HME_PRIO_LO();
     HME_STAMP(2);
-    // ---- A1: pre-HME regions and HME-L0 quadrants in three rounds, one HT16 x HQ
-    // tile per thread; between the rounds wave 0 takes the decisions that say
-    // which searches of the next round the reference performs
-    // (straight-line rounds: a loop over them keeps the decisions' values live
-    // through the tiles and spills)
-    auto a1_tiles = [&](const int rnd) {
+    // ---- A1: pre-HME regions and HME-L0 quadrants, one HT16 x HQ tile per thread
+    {
+        // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs (live in A1 only)
+        uint32_t sr[8][4];
         {
-            // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs (live in the round only)
-            uint32_t sr[8][4];
-            {
-                const uint8_t *sp = uni_ptr(dj.cur.lv[2].base + (ptrdiff_t)soy * dj.cur.lv[2].stride + sox);
-                const int sst     = UNI(dj.cur.lv[2].stride);
+            const uint8_t *sp = uni_ptr(dj.cur.lv[2].base + (ptrdiff_t)soy * dj.cur.lv[2].stride + sox);
+            const int sst     = UNI(dj.cur.lv[2].stride);
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * sst);
-                    sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
-                }
+            for (int k = 0; k < 8; k++) {
+                const uint4 v = sld4(sp + (ptrdiff_t)(2 * k) * sst);
+                sr[k][0] = v.x, sr[k][1] = v.y, sr[k][2] = v.z, sr[k][3] = v.w;
             }
-            const int nsrch = sh.u.a.nsrch;
-            const uint32_t need = sh.u.a.need;
-            const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
-            const int rb = sh.u.a.rb[rnd], re = sh.u.a.re[rnd];
-            const bool two = rnd == 2 && sh.u.a.l0_t2;
-            for (int it = rb + tid; it < re; it += 256) {
+        }
+        const int nitems = sh.u.a.nitems, nsrch = sh.u.a.nsrch;
+        const uint32_t need = sh.u.a.need;
+        const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
+        const int nitems3 = sh.u.a.nitems3, base2 = sh.u.a.base2;
+        auto tiles = [&](auto fullk) {
+            for (int it = tid; it < nitems; it += 256) {
+                if (it >= nitems3 && it < base2)
+                    continue; // the padding before the 2-row group
                 const HSrch &e = sh.u.a.srch[find_search(sh.u.a.srch, nsrch, it)];
                 if (!((need >> e.need) & 1u))
                     continue;
                 const int local = it - e.item0;
                 const int rt = mdiv(local, e.ncm), col = local - rt * e.ncols;
-                // the wavefront's tiles all have the round's row count (64-aligned ranges)
+                // the wavefront's tiles all have e.tt rows (the groups are 64-aligned)
                 auto run = [&](auto TT) {
                     constexpr int T = decltype(TT)::value;
                     int yf, tv;
@@ -3054,75 +2996,34 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                     }
                     if (tv <= 0)
                         return;
-                    const unsigned long long kk =
-                        hme_tile16<T, false>(e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
+                    const unsigned long long kk = hme_tile16<T, decltype(fullk)::value>(
+                        e.a0, pstride, HQ16 * col, e.sh, e.sa_w, yf, tv, e.ylast, kh, sr);
                     if (kk != ~0ull)
                         atomicMin(&sh.u.a.key[e.id], kk);
                 };
-                // (a kh == 8 specialisation spills: the scheduler hoists every row)
-                if (UNI(two))
+                if (UNI(it >= base2))
                     run(std::integral_constant<int, 2>());
                 else
                     run(std::integral_constant<int, HT16>());
             }
-        }
-    };
-    auto a1_decide = [&](const int rnd) {
-        if (wid == 0) {
-            HME_PRIO_HI();
-            const bool two_lists = c.prehme_enable && job.num_lists == 2;
-            if (rnd == 0 || two_lists) { // else the need of round 2 set after round 0 stands
-                if (c.prehme_enable) { // the pre-HME results of this round's list, then its decisions
-                    const int id = SVTME_A_PH + rnd * 8 + lane;
-                    if (lane < 8) {
-                        uint32_t best;
-                        int x, y;
-                        key_result(sh.u.a.key[id], &best, &x, &y);
-                        d.a[id] = ARes{hsub ? best * 2 : best, i16((x + sh.u.a.kxo[id]) * 4),
-                                       i16((y + sh.u.a.kyo[id]) * 4)};
-                    }
-                    wave_lds_fence();
-                    dec_prehme_list(d, job, vmask, rnd);
-                }
-                const bool last_ph = rnd == 1 || !two_lists;
-                bool nd;
-                if (!last_ph) { // round 1: the list-1 regions (lane = ref * 2 + region, bits 8 + lane)
-                    nd = prehme_l1_searched(d, job, vmask);
-                } else { // round 2: the HME-L0 quadrants of every slot searched (lane = slot, bits 16 + slot)
-                    if (c.prehme_enable)
-                        dec_prehme_prune(d, job, vmask);
-                    nd = c.enable_hme_flag && c.enable_hme_level0_flag && l0_searched(d, job, vmask);
-                }
-                const uint32_t m = (uint32_t)__ballot(nd);
-                if (lane == 0)
-                    sh.u.a.need = last_ph ? (m & 0xFFu) << 16 : (m & 0xFFu) << 8;
-            }
-        }
-    };
-    a1_tiles(0);
-    __syncthreads();
-    a1_decide(0);
-    __syncthreads();
-    HME_PRIO_LO();
-    a1_tiles(1);
-    __syncthreads();
-    a1_decide(1);
-    __syncthreads();
-    HME_PRIO_LO();
-    a1_tiles(2);
+        };
+        tiles(std::false_type()); // (a kh == 8 specialisation spills: the scheduler hoists every row)
+    }
     __syncthreads();
     HME_STAMP(3);
     // ---- D: pre-HME and level-0 decisions, then the HME-L1 table (wave 0)
+    const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH; // true on this path
     if (wid == 0) {
         HME_PRIO_HI();
-        if (lane < SVTME_A_N && lane >= SVTME_A_L0) {
+        if (lane < SVTME_A_N && lane >= SVTME_A_PH) {
             uint32_t best;
             int x, y;
             key_result(sh.u.a.key[lane], &best, &x, &y);
             d.a[lane] = ARes{hsub ? best * 2 : best, i16((x + sh.u.a.kxo[lane]) * 4), i16((y + sh.u.a.kyo[lane]) * 4)};
         }
         wave_lds_fence();
-        dec_l0(d, job, vmask); // the pre-HME decisions ran between the A1 rounds
+        dec_prehme(d, job, vmask);
+        dec_l0(d, job, vmask);
         // HME-L1 per (slot, quadrant), lane = slot * 4 + q (hme_level1_b64, :2041-2122)
         const int s = lane >> 2, q = lane & 3, l = s >> 2;
         bool mk   = false;
