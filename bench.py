@@ -43,6 +43,7 @@ compiled from the reference sources into oracle/_ref) on this host's cores
 sample of whole-picture passes of the same job, rank 0 at N = 1 only.
 """
 import argparse
+import ctypes as C
 import glob
 import json
 import math
@@ -387,9 +388,21 @@ def main():
     if world == 1:
         gpu.sync()
         recs = np.frombuffer(local[0][:chunk_bytes].cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n_sb, R)
-    cpu_baseline = parity = None
+    cpu_baseline = parity = ref_absdiff = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_baseline, parity = cpu_leg(S, W, name, recs, args.cpu_seconds)
+        cpu_baseline, parity, ref_absdiff = cpu_leg(S, W, name, recs, args.cpu_seconds)
+    valu_sad = {"achieved_T_absdiff_s": round(sad_rate, 2), "peak": SAD_PEAK_T, "frac": round(sad_rate / SAD_PEAK_T, 4),
+                "absdiff_per_sb_ref": W.ABSDIFF_PER_SB_REF[wl["windows"]],
+                "note": "SURVEY.md 8(d) nominal absdiff (distance-1 windows, no early exit) per launch / pass time"}
+    if ref_absdiff:
+        per_sb = ref_absdiff / n_sb
+        ref_rate = per_sb * sbs_launch / (device_ms * 1e-3) / 1e12
+        valu_sad.update({"reference_absdiff_per_sb": round(per_sb), "reference_T_absdiff_s": round(ref_rate, 2),
+                         "reference_frac": round(ref_rate / SAD_PEAK_T, 4),
+                         "reference_note": "absdiff the reference's searches evaluate on this job (early exits "
+                                           "and pruning included; counted by the CPU oracle) per launch / pass "
+                                           "time; the GPU also runs the pre-HME / HME-L0 searches the reference "
+                                           "may skip, in the same pass (DESIGN.md 4)"})
 
     if rank == 0:
         out = {
@@ -436,8 +449,7 @@ def main():
                          "kernel_samples": n_timed,
                          "bytes_per_launch": bytes_launch, "sbs_per_launch": sbs_launch,
                          "dominant": dom, "stages": stages, "traffic_source": prof_path,
-                         "valu_sad": {"achieved_T_absdiff_s": round(sad_rate, 2), "peak": SAD_PEAK_T,
-                                      "frac": round(sad_rate / SAD_PEAK_T, 4)},
+                         "valu_sad": valu_sad,
                          "algorithmic_frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "dram": dram,
                          "limiter": "issue / latency: neither HBM (dram.frac) nor the SAD units (valu_sad.frac) "
@@ -538,6 +550,18 @@ def cpu_leg(S, W, name, gpu_recs, cpu_seconds):
     recs, _ = S.run_checker(job, pyr[8], refs, checker, nthreads=threads, with_sb_results=False)
     first = time.perf_counter() - t0
     parity = not S.compare_records(recs, gpu_recs)
+    # the absolute differences the reference's searches evaluate on this job (early exits and
+    # pruning included), counted by the oracle's restatement of them: the real SAD work
+    absdiff = None
+    try:
+        ora = S.load_oracle()
+        ora.svtora_absdiff.restype = C.c_uint64
+        ora.svtora_absdiff.argtypes = [C.c_int]
+        ora.svtora_absdiff(1)
+        S.run_checker(job, pyr[8], refs, "oracle", nthreads=threads, with_sb_results=False)
+        absdiff = int(ora.svtora_absdiff(1))
+    except (RuntimeError, AttributeError):
+        pass
     reps = max(1, int(cpu_seconds / max(first * threads, 1e-4)))
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -557,7 +581,7 @@ def cpu_leg(S, W, name, gpu_recs, cpu_seconds):
                        f"per task on {threads} threads (all CPUs this process may use: affinity "
                        f"{len(os.sched_getaffinity(0))}, cgroup quota), "
                        f"{'reference AVX2 kernels' if kind == 'reference' else 'C restatement'}, "
-                       f"{el:.2f} s wall, CPU: {cpu_model}"}, parity)
+                       f"{el:.2f} s wall, CPU: {cpu_model}"}, parity, absdiff)
 
 
 if __name__ == "__main__":

@@ -42,10 +42,17 @@ static const uint8_t ora_z_to_raster[85] = {
 /* ---------------------------------------------------------------------------
  * Kernels (C_DEFAULT/compute_sad_c.c)
  * ------------------------------------------------------------------------- */
+/* absolute differences the reference's searches evaluate (every SAD of the
+ * path goes through ora_nxm_sad): bench.py's VALU-SAD roof counts the real
+ * work of the benched job with it */
+static __thread uint64_t t_absdiff;
+static uint64_t g_absdiff;
+
 /* compute_sad_c.c:20-37 */
 static uint32_t ora_nxm_sad(const uint8_t *src, uint32_t src_stride, const uint8_t *ref, uint32_t ref_stride,
                             uint32_t height, uint32_t width) {
     uint32_t sad = 0;
+    t_absdiff += (uint64_t)height * width;
     for (uint32_t r = 0; r < height; r++, src += src_stride, ref += ref_stride)
         for (uint32_t c = 0; c < width; c++) sad += src[c] > ref[c] ? src[c] - ref[c] : ref[c] - src[c];
     return sad;
@@ -1211,8 +1218,14 @@ static void ora_run_range(OraRange *rg) {
 }
 
 static void *ora_thread(void *p) {
+    t_absdiff = 0;
     ora_run_range((OraRange *)p);
+    __atomic_fetch_add(&g_absdiff, t_absdiff, __ATOMIC_RELAXED);
     return NULL;
+}
+
+uint64_t svtora_absdiff(int reset) {
+    return reset ? __atomic_exchange_n(&g_absdiff, 0, __ATOMIC_RELAXED) : __atomic_load_n(&g_absdiff, __ATOMIC_RELAXED);
 }
 
 uint32_t svtme_sb_total(uint32_t width, uint32_t height) { return ((width + 63) / 64) * ((height + 63) / 64); }
@@ -1242,7 +1255,7 @@ svtme_status svtora_me(const svtme_job *job, const svtme_pyr *cur, const svtme_p
         rg[t] = (OraRange){job, cur, refs, out, sbres, b, e - b};
     }
     if (nthreads == 1)
-        ora_run_range(&rg[0]);
+        ora_thread(&rg[0]);
     else {
         for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, ora_thread, &rg[t]);
         for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);

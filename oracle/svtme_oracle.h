@@ -44,6 +44,10 @@ svtme_status svtora_me(const svtme_job *job, const svtme_pyr *cur, const svtme_p
 svtme_status svtref_me(const svtme_job *job, const svtme_pyr *cur, const svtme_pyr *refs, svtme_ref_record *out,
                        svtme_sb_result *sbres, int nthreads);
 
+/* svtora only: absolute differences evaluated by svtora_me calls since the last
+ * reset (every SAD of the searches: positions x block pixels); reset != 0 clears it. */
+uint64_t svtora_absdiff(int reset);
+
 /* svtref only: select the reference kernels behind the rtcd pointers:
  * 0 = C (asm=0), 1 = the x86 AVX2 picks of aom_dsp_rtcd.c:501-515 capped at AVX2. */
 void svtref_set_simd(int simd);
