@@ -36,6 +36,8 @@ extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t
 extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" uint32_t svtme_fp_parts(const svtme_controls *c);
 extern "C" void svtme_hme_prepare(DevJob *dj);
+extern "C" bool svtme_hme_fused(const svtme_job *job);
+extern "C" bool svtme_hme_rt(const svtme_controls *c);
 
 // ----------------------------------------------------------------------------
 // errors
@@ -514,10 +516,9 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
     if (job->ctrl.num_hme_sa_w != 2 || job->ctrl.num_hme_sa_h != 2)
         return fail(SVTME_ERR_BAD_PARAMETER, "only 2x2 HME-L0 search regions are supported "
                                              "(motion_estimation.c:1875)");
-    if (job->ctrl.enable_me_sr_adjustment && job->ctrl.distance_based_hme_resizing &&
-        job->ctrl.reduce_hme_l0_sr_th_min && job->ctrl.reduce_hme_l0_sr_th_max)
-        return fail(SVTME_ERR_BAD_PARAMETER, "reduce_hme_l0_sr_th_min/max (real-time tune, enc_mode_config.c:690-703) "
-                                             "are not supported");
+    if (svtme_hme_rt(&job->ctrl) && !svtme_hme_fused(job))
+        return fail(SVTME_ERR_BAD_PARAMETER, "reduce_hme_l0_sr_th_min/max (real-time tune, enc_mode_config.c:692-704) "
+                                             "need a width that is a multiple of 64 (the fused HME kernel)");
     if (job->me_type != 0 && job->me_type != SVTME_ME_OPEN_LOOP && job->me_type != SVTME_ME_MCTF)
         return fail(SVTME_ERR_BAD_PARAMETER, "me_type %u is neither SVTME_ME_OPEN_LOOP nor SVTME_ME_MCTF",
                     job->me_type);

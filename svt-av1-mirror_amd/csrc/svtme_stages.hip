@@ -2725,6 +2725,108 @@ struct HmeA { // state of phases A0 .. B
     __attribute__((aligned(16))) uint8_t src1[32][64]; // full-resolution source, sub rows (HME-L2)
 };
 
+// A1 search table (wave 0): lane = slot * 6 + k, k < 2 pre-HME region k, else
+// HME-L0 quadrant k - 2. RND 0: every search the slots may need. The real-time
+// tune's HME-L0 reduction (reduce_hme_l0_sr_th, enc_mode_config.c:692-704) makes
+// the HME-L0 areas of slots 1-7 depend on slot 0's HME-L0 centre after its
+// worst-quadrant replacement (get_hme_l0_search_area, motion_estimation.c:
+// 1800-1867, called in slot order by hme_level0_b64 :1974-2036); then RND 1
+// has every search but those, and RND 2 those alone: the slots of bit set
+// l0need, areas from the centre (l00x, l00y)
+template <int RND>
+__device__ __forceinline__ void a1_table(HmeA &A, const DevJob &dj, uint32_t vmask, int16_t sox, int16_t soy, int kh,
+                                         uint32_t l0need = 0, int16_t l00x = 0, int16_t l00y = 0) {
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const int lane          = threadIdx.x & 63;
+    // lane = slot * 6 + k: k < 2 pre-HME region k, else HME-L0 quadrant k - 2
+    const int s = lane / 6, k = lane - 6 * (lane / 6), l = s >> 2;
+    bool on = lane < 48 && slot_valid(vmask, s) && tl_or_l0(job, l) &&
+              (k < 2 ? c.prehme_enable != 0 : (c.enable_hme_flag && c.enable_hme_level0_flag));
+    if (RND == 1)
+        on = on && (k < 2 || s == 0);
+    if (RND == 2)
+        on = on && k >= 2 && s > 0 && ((l0need >> s) & 1u);
+    bool mk    = false;
+    int items3 = 0, items2 = 0;
+    HSrch e;
+    if (on) {
+        const DevPlane &P = dj.ref[l][s & 3].lv[2];
+        int16_t aw = k < 2 ? dj.ph_sa[s][k][0] : dj.l0_sa[s][0];
+        int16_t ah = k < 2 ? dj.ph_sa[s][k][1] : dj.l0_sa[s][1];
+        if (RND == 2) // get_hme_l0_search_area from the first slot's centre (:1800-1867)
+            hme_l0_area(c, l, s & 3, dj.sdist[s], l00x, l00y, &aw, &ah);
+        int16_t xo, yo, sw, shh;
+        bool skip;
+        if (k < 2) { // prehme_core (motion_estimation.c:1568-1636)
+            prehme_area(P, sox, soy, aw, ah, &xo, &yo, &sw, &shh);
+            skip   = c.prehme_skip_search_line != 0; // compute_sad_c.c:74 (16 wide, <= 16 rows)
+            e.id   = (uint8_t)(SVTME_A_PH + s * 2 + k);
+            e.need = (uint8_t)(s * 2);
+        } else { // hme_level_0 (motion_estimation.c:835-889)
+            hme_l0_rect(c, P, sox, soy, aw, ah, (k - 2) >> 1, (k - 2) & 1, &xo, &yo, &sw, &shh);
+            skip   = false;
+            e.id   = (uint8_t)(SVTME_A_L0 + s * 4 + (k - 2));
+            e.need = (uint8_t)(s * 2 + 1);
+        }
+        A.kxo[e.id]    = xo;
+        A.kyo[e.id]    = yo;
+        const int nrows = (sw > 0 && shh > 0) ? (skip ? shh / 2 : shh) : 0;
+        if (nrows > 0) {
+            const uint8_t *w0 = P.base + (ptrdiff_t)(soy + yo) * P.stride + (sox + xo);
+            e.sh              = (uint8_t)((uintptr_t)w0 & 3);
+            e.a0              = w0 - e.sh;
+            e.sa_w            = sw;
+            e.skip            = skip;
+            const int nq      = (e.sh + sw + 3) >> 2;
+            e.ncols           = (int16_t)((nq + HQ16 - 1) / HQ16);
+            e.ncm             = magic_u32((uint32_t)e.ncols);
+            if (skip) {
+                e.cnt0  = (int16_t)nrows;
+                e.cnt1  = 0;
+                e.ylast = (int16_t)(2 * nrows - 1 + 2 * (kh - 1));
+                items3  = e.ncols * ((nrows + HT16 - 1) / HT16);
+                items2  = e.ncols * ((nrows + 1) / 2);
+            } else {
+                e.cnt0  = (int16_t)((nrows + 1) >> 1);
+                e.cnt1  = (int16_t)(nrows >> 1);
+                e.ylast = (int16_t)(nrows - 1 + 2 * (kh - 1));
+                items3  = e.ncols * 2 * ((e.cnt0 + HT16 - 1) / HT16);
+                items2  = e.ncols * 2 * ((e.cnt0 + 1) / 2);
+            }
+            mk = true;
+        }
+    }
+    // Tile shapes: a wavefront's qsad count is its tiles' row count x 64 lanes, so
+    // the HME-L0 quadrants (few rows per parity, e.g. 2 at p8, wasting a third of
+    // a 3-row tile) take 2-row tiles in wavefronts of their own when that needs
+    // fewer wavefront-rows: the 3-row group first, the 2-row group from the next
+    // multiple of 64 items
+    const bool l0    = k >= 2;
+    const int n3_pre = (int)wave_sum_u32(mk && !l0 ? (uint32_t)items3 : 0u);
+    const int n3_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items3 : 0u);
+    const int n2_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items2 : 0u);
+    const bool split = ((n3_pre + 63) / 64) * HT16 + ((n2_l0 + 63) / 64) * 2 < ((n3_pre + n3_l0 + 63) / 64) * HT16;
+    const bool t2    = mk && split && l0;
+    const int items  = t2 ? items2 : items3;
+    e.tt             = (uint8_t)(t2 ? 2 : HT16);
+    int n3s, n2s;
+    const int k3 = wave_compact(mk && !t2, &n3s), k2 = wave_compact(t2, &n2s);
+    const int i3 = wave_incl_scan(mk && !t2 ? items : 0), i2 = wave_incl_scan(t2 ? items : 0);
+    const int N3 = (int)lane63((uint32_t)i3), N2 = (int)lane63((uint32_t)i2);
+    const int base2 = (N3 + 63) & ~63;
+    if (mk) {
+        e.item0                          = t2 ? base2 + i2 - items : i3 - items;
+        A.srch[t2 ? n3s + k2 : k3] = e;
+    }
+    if (lane == 0) {
+        A.nsrch   = n3s + n2s;
+        A.nitems3 = N3;
+        A.base2   = base2;
+        A.nitems  = N2 ? base2 + N2 : N3;
+    }
+}
+
 // k_hme shared memory: the job copy, the SB's HME state, the per-record
 // full-pel results, and the phase-A..B state overlaid by the stage-C/E state
 // (dead by then)
@@ -2758,7 +2860,7 @@ struct HmeSh {
 #ifndef HME_WAVES_PER_EU
 #define HME_WAVES_PER_EU 8 // 64 VGPRs: 8 workgroups per CU
 #endif
-template <bool FP, bool SUB_ME, bool K32>
+template <bool FP, bool SUB_ME, bool K32, bool RT = false> // RT: the real-time tune's HME-L0 reduction (a1_table)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WAVES_PER_EU, HME_WAVES_PER_EU))) k_hme(const DevBatch B) {
     __shared__ HmeSh sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = UNI(tid >> 6);
@@ -2794,86 +2896,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         dec_init(d);
         if (lane < SVTME_A_N)
             sh.u.a.key[lane] = ~0ull;
-        // lane = slot * 6 + k: k < 2 pre-HME region k, else HME-L0 quadrant k - 2
-        const int s = lane / 6, k = lane - 6 * (lane / 6), l = s >> 2;
-        const bool on = lane < 48 && slot_valid(vmask, s) && tl_or_l0(job, l) &&
-                        (k < 2 ? c.prehme_enable != 0 : (c.enable_hme_flag && c.enable_hme_level0_flag));
-        bool mk    = false;
-        int items3 = 0, items2 = 0;
-        HSrch e;
-        if (on) {
-            const DevPlane &P = dj.ref[l][s & 3].lv[2];
-            const int16_t aw  = k < 2 ? dj.ph_sa[s][k][0] : dj.l0_sa[s][0];
-            const int16_t ah  = k < 2 ? dj.ph_sa[s][k][1] : dj.l0_sa[s][1];
-            int16_t xo, yo, sw, shh;
-            bool skip;
-            if (k < 2) { // prehme_core (motion_estimation.c:1568-1636)
-                prehme_area(P, sox, soy, aw, ah, &xo, &yo, &sw, &shh);
-                skip   = c.prehme_skip_search_line != 0; // compute_sad_c.c:74 (16 wide, <= 16 rows)
-                e.id   = (uint8_t)(SVTME_A_PH + s * 2 + k);
-                e.need = (uint8_t)(s * 2);
-            } else { // hme_level_0 (motion_estimation.c:835-889)
-                hme_l0_rect(c, P, sox, soy, aw, ah, (k - 2) >> 1, (k - 2) & 1, &xo, &yo, &sw, &shh);
-                skip   = false;
-                e.id   = (uint8_t)(SVTME_A_L0 + s * 4 + (k - 2));
-                e.need = (uint8_t)(s * 2 + 1);
-            }
-            sh.u.a.kxo[e.id]    = xo;
-            sh.u.a.kyo[e.id]    = yo;
-            const int nrows = (sw > 0 && shh > 0) ? (skip ? shh / 2 : shh) : 0;
-            if (nrows > 0) {
-                const uint8_t *w0 = P.base + (ptrdiff_t)(soy + yo) * P.stride + (sox + xo);
-                e.sh              = (uint8_t)((uintptr_t)w0 & 3);
-                e.a0              = w0 - e.sh;
-                e.sa_w            = sw;
-                e.skip            = skip;
-                const int nq      = (e.sh + sw + 3) >> 2;
-                e.ncols           = (int16_t)((nq + HQ16 - 1) / HQ16);
-                e.ncm             = magic_u32((uint32_t)e.ncols);
-                if (skip) {
-                    e.cnt0  = (int16_t)nrows;
-                    e.cnt1  = 0;
-                    e.ylast = (int16_t)(2 * nrows - 1 + 2 * (kh - 1));
-                    items3  = e.ncols * ((nrows + HT16 - 1) / HT16);
-                    items2  = e.ncols * ((nrows + 1) / 2);
-                } else {
-                    e.cnt0  = (int16_t)((nrows + 1) >> 1);
-                    e.cnt1  = (int16_t)(nrows >> 1);
-                    e.ylast = (int16_t)(nrows - 1 + 2 * (kh - 1));
-                    items3  = e.ncols * 2 * ((e.cnt0 + HT16 - 1) / HT16);
-                    items2  = e.ncols * 2 * ((e.cnt0 + 1) / 2);
-                }
-                mk = true;
-            }
-        }
-        // Tile shapes: a wavefront's qsad count is its tiles' row count x 64 lanes, so
-        // the HME-L0 quadrants (few rows per parity, e.g. 2 at p8, wasting a third of
-        // a 3-row tile) take 2-row tiles in wavefronts of their own when that needs
-        // fewer wavefront-rows: the 3-row group first, the 2-row group from the next
-        // multiple of 64 items
-        const bool l0    = k >= 2;
-        const int n3_pre = (int)wave_sum_u32(mk && !l0 ? (uint32_t)items3 : 0u);
-        const int n3_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items3 : 0u);
-        const int n2_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items2 : 0u);
-        const bool split = ((n3_pre + 63) / 64) * HT16 + ((n2_l0 + 63) / 64) * 2 < ((n3_pre + n3_l0 + 63) / 64) * HT16;
-        const bool t2    = mk && split && l0;
-        const int items  = t2 ? items2 : items3;
-        e.tt             = (uint8_t)(t2 ? 2 : HT16);
-        int n3s, n2s;
-        const int k3 = wave_compact(mk && !t2, &n3s), k2 = wave_compact(t2, &n2s);
-        const int i3 = wave_incl_scan(mk && !t2 ? items : 0), i2 = wave_incl_scan(t2 ? items : 0);
-        const int N3 = (int)lane63((uint32_t)i3), N2 = (int)lane63((uint32_t)i2);
-        const int base2 = (N3 + 63) & ~63;
-        if (mk) {
-            e.item0                          = t2 ? base2 + i2 - items : i3 - items;
-            sh.u.a.srch[t2 ? n3s + k2 : k3] = e;
-        }
-        if (lane == 0) {
-            sh.u.a.nsrch   = n3s + n2s;
-            sh.u.a.nitems3 = N3;
-            sh.u.a.base2   = base2;
-            sh.u.a.nitems  = N2 ? base2 + N2 : N3;
-        }
+        a1_table<RT ? 1 : 0>(sh.u.a, dj, vmask, sox, soy, kh);
     } else {
         if (zz_on) {
             // the wave's slots are wid - 1, wid + 2, wid + 5: the current rows are
@@ -2957,7 +2980,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     HME_PRIO_LO();
     HME_STAMP(2);
     // ---- A1: pre-HME regions and HME-L0 quadrants, one HT16 x HQ tile per thread
-    {
+    auto a1_tiles = [&]() {
         // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs (live in A1 only)
         uint32_t sr[8][4];
         {
@@ -3008,6 +3031,41 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             }
         };
         tiles(std::false_type()); // (a kh == 8 specialisation spills: the scheduler hoists every row)
+    };
+    a1_tiles();
+    if constexpr (RT) {
+        // the real-time tune: slot 0's HME-L0 centre after its worst-quadrant
+        // replacement (the pre-HME decisions and dec_l0 of slot 0), then the
+        // HME-L0 quadrants of slots 1-7 with the areas it selects
+        __syncthreads();
+        if (wid == 0) {
+            HME_PRIO_HI();
+            if (lane < SVTME_A_N && lane >= SVTME_A_PH) {
+                uint32_t best;
+                int x, y;
+                key_result(sh.u.a.key[lane], &best, &x, &y);
+                d.a[lane] = ARes{best * 2, i16((x + sh.u.a.kxo[lane]) * 4), // (sub-sampled rows)
+                                 i16((y + sh.u.a.kyo[lane]) * 4)};
+            }
+            wave_lds_fence();
+            dec_prehme(d, job, vmask);
+            dec_l0(d, job, vmask); // slots 1-7 read unsearched keys here: D redoes them
+            // the slots whose HME-L0 runs (dec_l0's order of exits)
+            const int s = lane;
+            bool run    = s > 0 && s < 8 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && d.do_ref[s] &&
+                       !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2));
+            if (run && c.prev_me_stage_based_exit_th) {
+                const int k = d.ph[s][0].sad <= d.ph[s][1].sad ? 0 : 1;
+                run = !(d.ph[s][k].performed && d.ph[s][k].sad < (c.prev_me_stage_based_exit_th >> 4));
+            }
+            const uint32_t l0need = (uint32_t)__ballot(run);
+            a1_table<2>(sh.u.a, dj, vmask, sox, soy, kh, l0need, d.lx[0][0], d.ly[0][0]);
+            if (lane == 0)
+                sh.u.a.need = ~0u; // the table holds only searches that run
+        }
+        __syncthreads();
+        HME_PRIO_LO();
+        a1_tiles();
     }
     __syncthreads();
     HME_STAMP(3);
@@ -3022,7 +3080,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             d.a[lane] = ARes{hsub ? best * 2 : best, i16((x + sh.u.a.kxo[lane]) * 4), i16((y + sh.u.a.kyo[lane]) * 4)};
         }
         wave_lds_fence();
-        dec_prehme(d, job, vmask);
+        if (!RT) // (RT: made before the second A1 round; its pruning is not idempotent)
+            dec_prehme(d, job, vmask);
         dec_l0(d, job, vmask);
         // HME-L1 per (slot, quadrant), lane = slot * 4 + q (hme_level1_b64, :2041-2122)
         const int s = lane >> 2, q = lane & 3, l = s >> 2;
@@ -3328,8 +3387,8 @@ static void fp_area_bound(const svtme_controls *c, uint32_t *w, uint32_t *h) {
 
 // Per-slot search parameters of k_hme that do not depend on the SB: the
 // distance, get_hme_l0_search_area (motion_estimation.c:1800-1867, here with
-// l00 = (0, 0): the real-time reduction it would read is rejected by the job
-// validator) and the pre-HME areas (prehme_core :1580-1587).
+// l00 = (0, 0); with the real-time reduction, svtme_hme_rt, k_hme recomputes
+// slots 1-7 per SB) and the pre-HME areas (prehme_core :1580-1587).
 extern "C" void svtme_hme_prepare(DevJob *dj) {
     const svtme_job &job    = dj->job;
     const svtme_controls &c = job.ctrl;
@@ -3360,6 +3419,13 @@ extern "C" bool svtme_hme_fused(const svtme_job *job) {
            getenv("SVTME_NO_FUSED_HME") == nullptr;
 }
 
+// the real-time tune's HME-L0 reduction is on (get_hme_l0_search_area,
+// motion_estimation.c:1811-1819): k_hme<..., RT = true> only
+extern "C" bool svtme_hme_rt(const svtme_controls *c) {
+    return c->enable_me_sr_adjustment && c->distance_based_hme_resizing && c->reduce_hme_l0_sr_th_min &&
+           c->reduce_hme_l0_sr_th_max;
+}
+
 extern "C" bool svtme_fp_k32(const svtme_controls *c) {
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
@@ -3386,7 +3452,8 @@ extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
     const bool full = dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     return (uint32_t)full | (uint32_t)(dj->parts != 0) << 1 | (uint32_t)svtme_fp_k32(&dj->job.ctrl) << 2 |
            (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4 |
-           (uint32_t)(dj->parts == 1) << 5 | (uint32_t)svtme_fp_wide(&dj->job.ctrl) << 6;
+           (uint32_t)(dj->parts == 1) << 5 | (uint32_t)svtme_fp_wide(&dj->job.ctrl) << 6 |
+           (uint32_t)svtme_hme_rt(&dj->job.ctrl) << 7;
 }
 
 static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
@@ -3429,19 +3496,27 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     const bool full = h0.job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     const bool k32  = svtme_fp_k32(&h0.job.ctrl);
     // the whole pass in one launch; SVTME_SPLIT_PASS=1 keeps k_hme -> k_stage_c1 -> k_stage_e (diagnostics)
+    const bool rt = svtme_hme_rt(&h0.job.ctrl); // (the validator keeps these jobs on k_hme)
+#define SVTME_HME(FP, SUB, K32)                                                                                     \
+    do {                                                                                                           \
+        if (rt)                                                                                                    \
+            SVTME_LAUNCH((svtme::k_hme<FP, SUB, K32, true>), dim3(bd.total), 0, bd);                               \
+        else                                                                                                       \
+            SVTME_LAUNCH((svtme::k_hme<FP, SUB, K32, false>), dim3(bd.total), 0, bd);                              \
+    } while (0)
     if (svtme_hme_fused(&h0.job) && h0.parts == 1 && !getenv("SVTME_SPLIT_PASS")) {
         if (full && k32)
-            SVTME_LAUNCH((svtme::k_hme<true, false, true>), dim3(bd.total), 0, bd);
+            SVTME_HME(true, false, true);
         else if (full)
-            SVTME_LAUNCH((svtme::k_hme<true, false, false>), dim3(bd.total), 0, bd);
+            SVTME_HME(true, false, false);
         else if (k32)
-            SVTME_LAUNCH((svtme::k_hme<true, true, true>), dim3(bd.total), 0, bd);
+            SVTME_HME(true, true, true);
         else
-            SVTME_LAUNCH((svtme::k_hme<true, true, false>), dim3(bd.total), 0, bd);
+            SVTME_HME(true, true, false);
         return hipGetLastError();
     }
     if (svtme_hme_fused(&h0.job)) {
-        SVTME_LAUNCH((svtme::k_hme<false, true, true>), dim3(bd.total), 0, bd);
+        SVTME_HME(false, true, true);
     } else {
     const DevBatch ba = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta_count; });
     if (ba.total)

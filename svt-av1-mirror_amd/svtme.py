@@ -306,12 +306,16 @@ class Synth:
 
 def test_frames(kind: str, w: int, h: int, ts) -> dict:
     """Deterministic test content {t: luma plane} shared by the parity tests and
-    the golden-fixture generator: a panning texture ("pan"), i.i.d. noise,
+    the golden-fixture generator: a panning texture ("pan"; "vpan" / "hpan":
+    fast vertical / horizontal motion), i.i.d. noise,
     flat, saturated (0/255) and moving stripes (exact ties everywhere)."""
     ts = list(ts)
     if kind == "pan":
         syn = Synth(w, h)
         return {t: syn.frame(t) for t in ts}
+    if kind in ("vpan", "hpan"):  # 120 px per picture, vertical / horizontal (wraps around)
+        base = Synth(w, h).frame(0)
+        return {t: np.roll(base, 120 * t, axis=0 if kind == "vpan" else 1) for t in ts}
     rng = np.random.default_rng(1234)
     if kind == "noise":
         return {t: rng.integers(0, 256, (h, w), dtype=np.uint8) for t in ts}

@@ -51,6 +51,11 @@ CASES = {
     "1080p_p8": (1920, 1080, 8, 8, False, [], True),
     "4k_p8": (3840, 2160, 8, 8, False, [], True),
     "4k10_p6": (3840, 2160, 4, 6, True, [], True),
+    # low-delay prediction (real-time tune): reduce_hme_l0_sr_th at presets >= 8
+    # (enc_mode_config.c:692-704); p10 also runs without pre-HME
+    "360p_p8_lowdelay": (640, 360, 16, 8, False, ["--pred-struct", "1"], True),
+    "360p_p10_lowdelay": (640, 360, 16, 10, False, ["--pred-struct", "1"], True),
+    "1080p_p9_lowdelay": (1920, 1080, 8, 9, False, ["--pred-struct", "1"], True),
 }
 
 

@@ -24,8 +24,8 @@ stores inputs-as-parameters plus expected outputs:
                      access) as per-picture checksums and full records
 
 Run from the repo root in the build container (needs /root/reference for the
-library build only): python tests/golden/make_golden.py [tf|configs [name ...]|rtcd]
-(tf / configs / rtcd: only those fixtures; configs name ...: only those configurations)
+library build only): python tests/golden/make_golden.py [tf|me|configs [name ...]|rtcd]
+(tf / me / configs / rtcd: only those fixtures; configs name ...: only those configurations)
 """
 import hashlib
 import json
@@ -55,6 +55,19 @@ ME_CASES = [
     ("pan320_p8_band", "pan", 320, 192, 8, 1, (7, 6), (9, 10), {"sb_begin": 3, "sb_count": 7}),
     ("pan64_p0", "pan", 64, 64, 0, 1, (7,), (9,), {}),
     ("pan320_p8_nonref", "pan", 320, 192, 8, 2, (7,), (9,), {"is_ref": False}),
+    # real-time tune (low-delay prediction, enc_mode_config.c:692-704): HME-L0 areas
+    # of every slot but the first follow the first slot's HME-L0 centre
+    # (motion_estimation.c:1800-1867); "ctrl" overrides fields of the derived controls
+    ("pan320_p8_rt200", "pan", 320, 192, 8, 1, (7, 6), (9, 10),
+     {"ctrl": {"reduce_hme_l0_sr_th_min": 8, "reduce_hme_l0_sr_th_max": 200}}),
+    ("vpan640_p8_rt100", "vpan", 640, 360, 8, 1, (7, 6, 5), (9,),
+     {"ctrl": {"reduce_hme_l0_sr_th_min": 8, "reduce_hme_l0_sr_th_max": 100}}),
+    ("hpan640_p9_rt100", "hpan", 640, 360, 9, 2, (7, 6), (9, 10),
+     {"ctrl": {"reduce_hme_l0_sr_th_min": 8, "reduce_hme_l0_sr_th_max": 100}}),
+    ("vpan640_p8_rt100_adj2", "vpan", 640, 360, 8, 1, (7, 6), (9, 10),
+     {"ctrl": {"reduce_hme_l0_sr_th_min": 8, "reduce_hme_l0_sr_th_max": 100, "enable_me_sr_adjustment": 2}}),
+    ("pan640_p8_rt200_adj2", "pan", 640, 360, 8, 1, (7, 6, 5), (9, 10),
+     {"ctrl": {"reduce_hme_l0_sr_th_min": 8, "reduce_hme_l0_sr_th_max": 200, "enable_me_sr_adjustment": 2}}),
 ]
 
 TF_CASES = [
@@ -217,14 +230,27 @@ def configs_golden(only=None):
         json.dump(meta, fh, indent=1)
 
 
+def case_controls(preset, w, h, tl, extra):
+    """svt_aom_sig_deriv_me's controls of a case, with the case's overrides"""
+    ctrl = S.ref_derive_controls(preset, 35, S.input_resolution_of(w, h), tl)
+    for k, v in extra.get("ctrl", {}).items():
+        setattr(ctrl, k, v)
+    return ctrl
+
+
 def main():
     ref = S.load_ref()
     rtcd_golden()
     with open(os.path.join(HERE, "controls.json"), "w") as fh:
         json.dump(controls_golden(), fh, indent=0)
+    me_golden(ref)
+
+
+def me_golden(ref):
     meta = []
     for name, kind, w, h, preset, tl, l0, l1, extra in ME_CASES:
-        ctrl = S.ref_derive_controls(preset, 35, S.input_resolution_of(w, h), tl)
+        ctrl = case_controls(preset, w, h, tl, extra)
+        extra = {k: v for k, v in extra.items() if k != "ctrl"}
         out = {}
         for simd in (0, 1):  # C kernels and AVX2 kernels must agree
             ref.svtref_set_simd(simd)
@@ -250,6 +276,8 @@ if __name__ == "__main__":
         configs_golden(sys.argv[2:])
     elif sys.argv[1:] == ["rtcd"]:
         rtcd_golden()
+    elif sys.argv[1:] == ["me"]:
+        me_golden(S.load_ref())
     else:
         if sys.argv[1:] != ["tf"]:
             main()

@@ -7,11 +7,14 @@ right/bottom edges, presets 4/6/8/12 (check_00_center, HME-L2, pre-HME with
 line skipping, 8x8-variance resize), flat/saturated/noise content for ties.
 """
 import ctypes as C
+import json
+import os
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 def run_case(S, gpu, kind, w, h, mode, tl, l0, l1, cur=8, gm=False, is_ref=True, e8=None, sb_begin=0, sb_count=0):
@@ -330,3 +333,58 @@ def test_picture_invalidate(svtme, gpu):
         gpu.invalidate(123456, new)
     for pn in (3007, 3008, 3009):
         gpu.release(pn)
+
+
+with open(os.path.join(GOLD, "me_cases.json")) as _fh:
+    GOLD_ME_CASES = json.load(_fh)
+
+
+@pytest.mark.parametrize("case", GOLD_ME_CASES, ids=lambda c: c["name"])
+def test_picture_vs_reference_golden(svtme, gpu, case):
+    """The GPU job against the reference's own outputs (tests/golden/me_*.npz,
+    made by libsvtref from the reference sources), controls as stored with the
+    case: the derived controls and the real-time tune's reduce_hme_l0_sr_th
+    cases (HME-L0 areas of slots 1-7 from slot 0's centre)."""
+    S = svtme
+    ctrl = S.Controls.from_dict(case["ctrl"])
+    w, h, l0, l1 = case["w"], case["h"], tuple(case["l0"]), tuple(case["l1"])
+    frames = S.test_frames(case["content"], w, h, sorted(set([8] + list(l0) + list(l1))))
+    job = S.case_job(ctrl, w, h, 8, l0, l1, case["tl"], **case["extra"])
+    for t, f in frames.items():
+        gpu.upload(3000 + t, f)
+    job.picture_number = 3000 + 8
+    for i, t in enumerate(l0):
+        job.ref_picture_number[0][i] = 3000 + t
+    for i, t in enumerate(l1):
+        job.ref_picture_number[1][i] = 3000 + t
+    try:
+        recs, sbr = gpu.submit(job)
+    finally:
+        for t in frames:
+            gpu.release(3000 + t)
+    z = np.load(os.path.join(GOLD, f"me_{case['name']}.npz"))
+    exp_recs = z["records"].view(S.REF_RECORD_DTYPE).reshape(recs.shape)
+    exp_sb = z["sb"].view(S.SB_RESULT_DTYPE).reshape(sbr.shape)
+    errs = S.compare_records(exp_recs, recs, exp_sb, sbr)
+    assert not errs, errs[:5]
+    assert S.records_checksum(recs, sbr) == case["checksum"]
+
+
+def test_realtime_reduction_needs_fused_width(svtme, gpu):
+    """reduce_hme_l0_sr_th runs on the fused HME kernel only (width a multiple
+    of 64): other widths are rejected, and the encoder glue falls back."""
+    S = svtme
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(424, 240), 1)
+    ctrl.reduce_hme_l0_sr_th_min, ctrl.reduce_hme_l0_sr_th_max = 8, 200
+    frames = S.test_frames("pan", 424, 240, [7, 8])
+    for t, f in frames.items():
+        gpu.upload(3100 + t, f)
+    job = S.make_job(424, 240, ctrl, 8, (7,), (), temporal_layer_index=1)
+    job.picture_number = 3108
+    job.ref_picture_number[0][0] = 3107
+    try:
+        with pytest.raises(RuntimeError, match="multiple of 64"):
+            gpu.submit(job)
+    finally:
+        for t in frames:
+            gpu.release(3100 + t)
