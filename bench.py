@@ -348,7 +348,12 @@ def main():
     achieved = bytes_launch / (device_ms * 1e-3) / 1e9
     stages = {}
     fused = stage_ms[0] > 0 and stage_ms[1] <= 0 and stage_ms[2] <= 0
-    names = STAGES_FUSED if fused else STAGES
+    names = list(STAGES_FUSED if fused else STAGES)
+    lib = S.load_product()
+    lib.svtme_fp_wide_lds.argtypes = [C.POINTER(S.Controls)]
+    lib.svtme_fp_wide_lds.restype = C.c_bool
+    if lib.svtme_fp_wide_lds(C.byref(jobs[0].ctrl)):
+        names[3] = "k_fp_wide"  # the wide full-pel stage with its window in LDS
     for k, st in enumerate(names):
         if stage_ms[k] <= 0:
             continue

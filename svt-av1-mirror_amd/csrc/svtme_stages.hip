@@ -2423,30 +2423,24 @@ __device__ __forceinline__ uint32_t fp_probe32(PuMin<true> &M, const uint8_t *g,
     return SUB ? s8 << 1 : s8;
 }
 
-// integer_search_b64 of one reference slot s by one wavefront (motion_estimation.c:
-// 1249-1516): search area, check_00_center, the 8x8-variance centre probe and
-// the full-pel search of search rows [h * part / parts, h * (part + 1) / parts);
-// the 85-PU argmin keys go to kp (atomic min when parts > 1), the slot state
-// to cs (part 0). src: this lane's 8x8 source block rows (lane = block by, bx).
-template <bool SUB, bool K32, int TQ = (SUB ? FP_TQ : 2), bool WIDE = false>
-__device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s, const uint32_t (&src)[SUB ? 4 : 8][2],
-                                        int by, int bx, uint64_t hme_sad, uint32_t zz, uint32_t rdiv, int16_t sc_x,
-                                        int16_t sc_y, uint8_t dref, uint8_t tf_exit, int part, uint32_t parts,
-                                        unsigned long long *kp, CSlot *cs) {
+// Search area of integer_search_b64 for reference slot s (motion_estimation.c:
+// 1282-1482): the area from the centre and the distance, check_00_center
+// (:1139-1206), the 8x8-variance centre probe and resize (:1391-1439; probe(g)
+// evaluates the centre at g, enters its keys at order 0 and returns the
+// variance) and the final clamp to the picture.
+struct FpArea {
+    int16_t xo, yo, w, h, xc, yc;
+    bool probe;
+};
+template <typename Probe>
+__device__ __forceinline__ FpArea fp_area(const DevJob &dj, const SbGeo &G, int s, uint32_t zz, uint32_t rdiv,
+                                          int16_t sc_x, int16_t sc_y, Probe probe_var) {
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const int lane          = threadIdx.x & 63;
     const int l = s >> 2, r = s & 3;
     const uint32_t ox = G.ox, oy = G.oy;
     const bool mctf   = job.me_type == SVTME_ME_MCTF;
     const DevPlane &C = dj.cur.lv[0];
-    if (!dref || tf_exit) {
-        if (part == 0 && lane == 0)
-            *cs = CSlot{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
-        return;
-    }
-
-    // search area (integer_search_b64, :1282-1351)
     const DevPlane &P = dj.ref[l][r].lv[0];
     int16_t xc = sc_x, yc = sc_y;
     uint16_t dist = ref_dist_const(job, l, r);
@@ -2489,26 +2483,10 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
         }
     }
     // 8x8-variance centre probe and search-area resize (:1391-1439); the probe's
-    // keys (order 0) stay in M, so the centre wins ties against the main search
-    PuMin<K32> M;
-    M.clear();
+    // keys (order 0) stay with the caller, so the centre wins ties against the search
     const bool probe = c.me_8x8_var_enabled && (w * h > 24);
     if (probe) {
-        const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc);
-        const int sh     = (int)((uintptr_t)g & 3);
-        uint32_t p8, p64;
-        if constexpr (K32) {
-            p8  = fp_probe32<SUB>(M, g, P.stride >> 2, src, by, bx);
-            p64 = wave_sum_u32(p8); // the 64x64 SAD at the centre
-        } else {
-            fp_rows<SUB, K32, 1>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
-            M.finalize();
-            p8  = (uint32_t)(PuMin<K32>::template out<SUB>(M.b8, true) >> 32);
-            p64 = rl32((uint32_t)(PuMin<K32>::template out<SUB>(M.b64, false) >> 32), 63);
-        }
-        const uint32_t mean = p64 / 64;
-        const int32_t diff  = (int32_t)p8 - (int32_t)mean;
-        const uint32_t var  = wave_sum_u32((uint32_t)(diff * diff)) / 64;
+        const uint32_t var = probe_var(P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc));
         if (var > c.me_sr_mult2_th) {
             w = i16((max(1, w * 3 / 2) + 7) & ~0x7);
             h = i16(max(1, h * 3 / 2));
@@ -2536,6 +2514,48 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     h  = ((org_y + yo) < -pad) ? i16(h - (-pad - (org_y + yo))) : h;
     yo = ((org_y + yo) > pic_h - 1) ? i16(yo - ((org_y + yo) - (pic_h - 1))) : yo;
     h  = (org_y + yo + h > pic_h) ? i16(max(1, h - ((org_y + yo + h) - pic_h))) : h;
+    return FpArea{xo, yo, w, h, xc, yc, probe};
+}
+
+// integer_search_b64 of one reference slot s by one wavefront (motion_estimation.c:
+// 1249-1516): search area (fp_area) and the full-pel search of search rows
+// [h * part / parts, h * (part + 1) / parts); the 85-PU argmin keys go to kp
+// (atomic min when parts > 1), the slot state to cs (part 0). src: this lane's
+// 8x8 source block rows (lane = block by, bx).
+template <bool SUB, bool K32, int TQ = (SUB ? FP_TQ : 2), bool WIDE = false>
+__device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s, const uint32_t (&src)[SUB ? 4 : 8][2],
+                                        int by, int bx, uint64_t hme_sad, uint32_t zz, uint32_t rdiv, int16_t sc_x,
+                                        int16_t sc_y, uint8_t dref, uint8_t tf_exit, int part, uint32_t parts,
+                                        unsigned long long *kp, CSlot *cs) {
+    const int lane = threadIdx.x & 63;
+    const int l = s >> 2, r = s & 3;
+    const uint32_t ox = G.ox, oy = G.oy;
+    if (!dref || tf_exit) {
+        if (part == 0 && lane == 0)
+            *cs = CSlot{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
+        return;
+    }
+    const DevPlane &P = dj.ref[l][r].lv[0];
+    PuMin<K32> M;
+    M.clear();
+    const FpArea A = fp_area(dj, G, s, zz, rdiv, sc_x, sc_y, [&](const uint8_t *g) {
+        const int sh = (int)((uintptr_t)g & 3);
+        uint32_t p8, p64;
+        if constexpr (K32) {
+            p8  = fp_probe32<SUB>(M, g, P.stride >> 2, src, by, bx);
+            p64 = wave_sum_u32(p8); // the 64x64 SAD at the centre
+        } else {
+            fp_rows<SUB, K32, 1>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, 1, 1, 0, 1, 0u, src, by, bx);
+            M.finalize();
+            p8  = (uint32_t)(PuMin<K32>::template out<SUB>(M.b8, true) >> 32);
+            p64 = rl32((uint32_t)(PuMin<K32>::template out<SUB>(M.b64, false) >> 32), 63);
+        }
+        const uint32_t mean = p64 / 64;
+        const int32_t diff  = (int32_t)p8 - (int32_t)mean;
+        return wave_sum_u32((uint32_t)(diff * diff)) / 64;
+    });
+    const int16_t xo = A.xo, yo = A.yo, w = A.w, h = A.h, xc = A.xc, yc = A.yc;
+    const bool probe = A.probe;
 
     // full-pel search of this part's rows (open_loop_me_fullpel_search_sblock, :781-817)
     const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yo) * P.stride + ((int)ox + xo);
@@ -2621,6 +2641,327 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
     unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
     fp_slot<SUB, K32, (SUB ? FP_TQ : 2), WIDE>(dj, G, s, src, by, bx, hme_sad, zz, rdiv, sc_x, sc_y, dref, tf_exit, part,
                                              parts, kp, cs);
+}
+
+// ============================================================================
+// k_fp_wide: the wide full-pel search (areas of 24 positions and more, e.g. the
+// 64x64 override; sub-sampled rows, 32-bit keys) with the window in LDS.
+//
+// A workgroup takes 4 consecutive row bands (parts) of one (SB, reference): it
+// stages the window rows of all 4 once, realigned to position 0 (fw_a) and
+// shifted by one dword (fw_b[j] = fw_a[j + 1]), so every reference dword pair a
+// qsad reads is one 8-byte LDS read, even pairs from fw_a and odd pairs from
+// fw_b: no v_alignbyte, no register moves for misaligned pairs, and the L1 /
+// TA path idle during the search.
+// Lane = by2 * 16 + hr * 8 + bx: the 8x8 blocks (2 by2, bx) and (2 by2 + 1, bx)
+// of the SB (an 8x16 column) at search rows of parity hr. The 16x16 SADs are
+// summed on packed u16 pairs (no carries: <= 32 640), lane bx & 1 keeping one
+// parity of positions; the 32x32 sums (the horizontal halves packed, <= 65 280)
+// leave one position per lane through one permlane16_swap (rows by2 even: c,
+// odd: c + 4, c = bx < 4 ? bx : 7 - bx, so the row_half_mirror partner in the
+// other 32x32 column holds the same position for the 64x64 sum); keys carry
+// the position within the set (inline constants), the set's raster order is
+// added once per set.
+// ============================================================================
+#define FPW_PITCH 48 // dwords per LDS row: 192 bytes = 64 (mod 128), so the two search rows
+                     // of a 16-lane read group (hr = 0, 1) fall on disjoint bank halves
+#define FPW_ROWS 96  // window rows per workgroup (4 bands + 62; the host bounds the band height)
+#ifndef FPW_TQ
+#define FPW_TQ 4 // position quads per set (2 quad pairs, 16 positions; 6 wastes a third of the
+               // last set at 64 positions, 8 measures the same as 4)
+#endif
+
+struct FpW {
+    uint32_t b8t, b8b, b16, b32, b64; // K32 keys: 8x8 / 16x16 (sad << 16 | order), 32x32 / 64x64 (sad << 12 | order)
+};
+
+// min over lanes l and l ^ 8 (the two search-row halves), in place
+__device__ __forceinline__ uint32_t fpw_min_hr(uint32_t v) {
+    return min_u32(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false)); // row_ror:8
+}
+
+// One quad pair (positions e0 .. e0 + 7 of the set) of both blocks: 8x8 keys of
+// each block, then the 16x16 / 32x32 / 64x64 sums and keys into the set minima.
+// T / T2 (top), Bq / B2 (bottom): the qsad accumulators of quads a and b.
+// MASK: positions >= ev are outside the area (the last, partial pair).
+template <bool MASK>
+__device__ __forceinline__ void fpw_pair(FpW &m, unsigned long long T, unsigned long long T2, unsigned long long Bq,
+                                         unsigned long long B2, int e0, int ev, uint32_t sel16, uint32_t sel32,
+                                         int p16, int p32) {
+    const uint32_t tl = (uint32_t)T, th = (uint32_t)(T >> 32), tl2 = (uint32_t)T2, th2 = (uint32_t)(T2 >> 32);
+    const uint32_t bl = (uint32_t)Bq, bh = (uint32_t)(Bq >> 32), bl2 = (uint32_t)B2, bh2 = (uint32_t)(B2 >> 32);
+    auto k8 = [&](uint32_t v, int e) { // (sad << 16 | e) of position e of a packed pair
+        const uint32_t k = (e & 1) ? ((v & 0xFFFF0000u) | (uint32_t)e) : ((v << 16) | (uint32_t)e);
+        return (MASK && e >= ev) ? 0xFFFFFFFFu : k;
+    };
+    m.b8t = min_u32(min_u32(m.b8t, k8(tl, e0)), k8(tl, e0 + 1));
+    m.b8t = min_u32(min_u32(m.b8t, k8(th, e0 + 2)), k8(th, e0 + 3));
+    m.b8t = min_u32(min_u32(m.b8t, k8(tl2, e0 + 4)), k8(tl2, e0 + 5));
+    m.b8t = min_u32(min_u32(m.b8t, k8(th2, e0 + 6)), k8(th2, e0 + 7));
+    m.b8b = min_u32(min_u32(m.b8b, k8(bl, e0)), k8(bl, e0 + 1));
+    m.b8b = min_u32(min_u32(m.b8b, k8(bh, e0 + 2)), k8(bh, e0 + 3));
+    m.b8b = min_u32(min_u32(m.b8b, k8(bl2, e0 + 4)), k8(bl2, e0 + 5));
+    m.b8b = min_u32(min_u32(m.b8b, k8(bh2, e0 + 6)), k8(bh2, e0 + 7));
+    // 8x16 columns, then 16x16 over bx ^ 1 (packed: both halves stay below 2^15)
+    const uint32_t sl = dpp_add<0xB1>(tl + bl), sh = dpp_add<0xB1>(th + bh);
+    const uint32_t sl2 = dpp_add<0xB1>(tl2 + bl2), sh2 = dpp_add<0xB1>(th2 + bh2);
+    // lane parity p16 keeps positions e0 + 2i + p16: (half p16 of the pair) << 16 | e0 + 2i
+    auto k16 = [&](uint32_t v, int e) {
+        const uint32_t k = __builtin_amdgcn_perm(v, (uint32_t)e, sel16);
+        return (MASK && e + p16 >= ev) ? 0xFFFFFFFFu : k;
+    };
+    m.b16 = min_u32(min_u32(m.b16, k16(sl, e0)), k16(sh, e0 + 2));
+    m.b16 = min_u32(min_u32(m.b16, k16(sl2, e0 + 4)), k16(sh2, e0 + 6));
+    // 32x16 over bx ^ 2 (packed, <= 65 280), then this lane's position of quad a
+    // and of quad b (byte select), and the vertical 32x32 sum over by2 ^ 1 (one
+    // permlane16_swap: rows by2 even get position c, odd c + 4)
+    const uint32_t xl = dpp_add<0x4E>(sl), xh = dpp_add<0x4E>(sh);
+    const uint32_t xl2 = dpp_add<0x4E>(sl2), xh2 = dpp_add<0x4E>(sh2);
+    const uint32_t va = __builtin_amdgcn_perm(xh, xl, sel32), vb = __builtin_amdgcn_perm(xh2, xl2, sel32);
+    const auto sw       = __builtin_amdgcn_permlane16_swap(va, vb, false, false);
+    const uint32_t s32  = sw[0] + sw[1];
+    const uint32_t k32  = (s32 << 12) | (uint32_t)e0;
+    m.b32               = min_u32(m.b32, (MASK && e0 + p32 >= ev) ? 0xFFFFFFFFu : k32);
+    // 64x64: the mirrored 32x32 column (bx <-> 7 - bx, same position), then by2 ^ 2
+    const uint32_t s64h = dpp_add<0x141>(s32); // row_half_mirror
+    const auto sw2      = __builtin_amdgcn_permlane32_swap(s64h, s64h, false, false);
+    const uint32_t s64  = sw2[0] + sw2[1];
+    const uint32_t k64  = (s64 << 12) | (uint32_t)e0;
+    m.b64               = min_u32(m.b64, (MASK && e0 + p32 >= ev) ? 0xFFFFFFFFu : k64);
+}
+
+// set-local minima (orders within the set) into the running minima (raster order)
+__device__ __forceinline__ uint32_t fpw_rebase(uint32_t b, uint32_t m, uint32_t base) {
+    return min_u32(b, m == 0xFFFFFFFFu ? m : m + base);
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) k_fp_wide(const DevBatch B) {
+    __shared__ uint32_t fw_a[FPW_ROWS * FPW_PITCH], fw_b[FPW_ROWS * FPW_PITCH];
+    constexpr int ROWS = 4, RSTEP = 2; // sub-sampled rows
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total) // the whole workgroup: totals are multiples of 4
+        return;
+    uint32_t gw;
+    const DevJob &dj        = batch_job(B, u, &gw);
+    const svtme_job &job    = dj.job;
+    const uint32_t parts    = dj.parts;
+    const uint32_t per_sb   = dj.R * parts;
+    const uint32_t sb_local = UNI(gw / per_sb);
+    const uint32_t rem      = gw - sb_local * per_sb;
+    const int k             = UNI(rem / parts);
+    const int part          = UNI(rem - (uint32_t)k * parts);
+    const int s             = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
+    const SbGeo G           = sb_geo(dj, sb_local);
+    const uint32_t ox = G.ox, oy = G.oy;
+    const bool mctf   = job.me_type == SVTME_ME_MCTF;
+    const int by2 = lane >> 4, hr = (lane >> 3) & 1, bx = lane & 7;
+    const int c32 = bx < 4 ? bx : 7 - bx;
+
+    // the lane's two 8x8 source blocks (rows 2 by2 * 8 + blk * 8 + 2 rr), issued first
+    const DevPlane &C = dj.cur.lv[0];
+    uint32_t src[2][ROWS][2];
+#pragma unroll
+    for (int blk = 0; blk < 2; blk++)
+#pragma unroll
+        for (int rr = 0; rr < ROWS; rr++) {
+            const uint32_t *sp = (const uint32_t *)(C.base +
+                                                    (ptrdiff_t)(oy + (2 * by2 + blk) * 8 + rr * RSTEP) * C.stride +
+                                                    ox + bx * 8);
+            src[blk][rr][0] = sp[0];
+            src[blk][rr][1] = sp[1];
+        }
+    const SlotCentre scv   = final_centre(job, dj.bst + sb_local, valid_mask(job));
+    const uint64_t hme_sad = rl64(scv.hme_sad, s);
+    const uint32_t zz = rl32(scv.zz, s), rdiv = rl32(scv.reduce_div, s);
+    const int16_t sc_x    = (int16_t)rl32((uint32_t)(int32_t)scv.sc_x, s);
+    const int16_t sc_y    = (int16_t)rl32((uint32_t)(int32_t)scv.sc_y, s);
+    const uint8_t dref    = (uint8_t)rl32(scv.do_ref, s);
+    const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
+    CSlot *cs             = dj.cslot + (size_t)sb_local * dj.R + k;
+    unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
+    if (!dref || tf_exit) { // the same for the workgroup's 4 bands
+        if (part == 0 && lane == 0)
+            *cs = CSlot{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
+        return;
+    }
+    const DevPlane &P = dj.ref[s >> 2][s & 3].lv[0];
+    const int sdw     = P.stride >> 2;
+    FpW b{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    const FpArea A = fp_area(dj, G, s, zz, rdiv, sc_x, sc_y, [&](const uint8_t *g) {
+        // the centre: both blocks' raw 8x8 SADs (order 0 in every class)
+        g                                 = uni_ptr(g);
+        const int sh                      = (int)((uintptr_t)g & 3);
+        const __amdgpu_buffer_rsrc_t rs   = plane_rsrc(g - sh);
+        uint32_t s8[2];
+#pragma unroll
+        for (int blk = 0; blk < 2; blk++) {
+            const uint32_t lo = (uint32_t)(((2 * by2 + blk) * 8) * sdw + bx * 2) * 4u;
+            u32x4a4 d[ROWS];
+#pragma unroll
+            for (int rr = 0; rr < ROWS; rr++) d[rr] = bld4(rs, lo, (uint32_t)(rr * RSTEP * sdw) * 4u);
+            uint32_t a = 0;
+#pragma unroll
+            for (int rr = 0; rr < ROWS; rr++) {
+                a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d[rr].y, d[rr].x, (uint32_t)sh), src[blk][rr][0], a);
+                a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d[rr].z, d[rr].y, (uint32_t)sh), src[blk][rr][1], a);
+            }
+            s8[blk] = a;
+        }
+        const uint32_t s16 = dpp_add<0xB1>(s8[0] + s8[1]);
+        const uint32_t s32h = dpp_add<0x4E>(s16);
+        const auto w16 = __builtin_amdgcn_permlane16_swap(s32h, s32h, false, false);
+        const uint32_t s32 = w16[0] + w16[1];
+        const uint32_t s64h = dpp_add<0x141>(s32);
+        const auto w32 = __builtin_amdgcn_permlane32_swap(s64h, s64h, false, false);
+        const uint32_t s64 = w32[0] + w32[1];
+        b.b8t = s8[0] << 16, b.b8b = s8[1] << 16, b.b16 = s16 << 16, b.b32 = s32 << 12, b.b64 = s64 << 12;
+        // the variance of the 64 8x8 SADs as the reference counts them (doubled); every
+        // block sits in two lanes (hr = 0, 1)
+        const uint32_t p8t = s8[0] << 1, p8b = s8[1] << 1;
+        const uint32_t mean = (wave_sum_u32(p8t + p8b) >> 1) / 64;
+        const int32_t dt = (int32_t)p8t - (int32_t)mean, db = (int32_t)p8b - (int32_t)mean;
+        return (wave_sum_u32((uint32_t)(dt * dt) + (uint32_t)(db * db)) >> 1) / 64;
+    });
+    const int w = A.w, h = A.h;
+
+    // stage the rows [Y0, Y1 + 62) of the 4 bands: fw_a[row][j] = window dword j
+    // (realigned), fw_b[row][j] = fw_a[row][j + 1]
+    const uint8_t *g = uni_ptr(P.base + (ptrdiff_t)((int)oy + A.yo) * P.stride + ((int)ox + A.xo));
+    const int sh     = (int)((uintptr_t)g & 3);
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(g - sh);
+    const int part0 = part & ~3;
+    const int Y0 = (int)(((uint32_t)h * part0) / parts), Y1 = (int)(((uint32_t)h * (part0 + 4)) / parts);
+    const int nq     = (w + 3) >> 2;
+    const int nsets  = (nq + FPW_TQ - 1) / FPW_TQ;
+    const int ndw    = 14 + (nsets - 1) * FPW_TQ + FPW_TQ + 2; // fw_a dwords a lane's pairs reach
+    const int nrows  = Y1 - Y0 + 62;
+    {
+        const uint32_t mrow = magic_u32((uint32_t)(ndw + 1));
+        const int total     = nrows * (ndw + 1);
+        for (int i0 = 0; i0 < total; i0 += 4 * 256) {
+            uint32_t r0[4], r1[4];
+            int row[4], j[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int i = i0 + t * 256 + (int)threadIdx.x;
+                row[t]      = mdiv(i, mrow);
+                j[t]        = i - row[t] * (ndw + 1);
+                r0[t] = r1[t] = 0;
+                if (i < total) {
+                    const uint32_t off = ((uint32_t)(Y0 + row[t]) * (uint32_t)sdw + (uint32_t)j[t]) * 4u;
+                    r0[t] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
+                    r1[t] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 4u), 0, 0);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const int i = i0 + t * 256 + (int)threadIdx.x;
+                if (i < total) {
+                    const uint32_t v = __builtin_amdgcn_alignbyte(r1[t], r0[t], (uint32_t)sh);
+                    fw_a[row[t] * FPW_PITCH + j[t]] = v;
+                    if (j[t] > 0)
+                        fw_b[row[t] * FPW_PITCH + j[t] - 1] = v;
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // this band's search rows; the two halves of the wave take rows ty and ty + 1
+    const int y0 = (int)(((uint32_t)h * part) / parts), y1 = (int)(((uint32_t)h * (part + 1)) / parts);
+    const uint32_t obase = A.probe ? 1u : 0u; // the centre probe wins ties: order 0
+    const uint32_t sel16 = (bx & 1) ? 0x07060100u : 0x05040100u;
+    const uint32_t sel32 = (c32 & 2) ? ((c32 & 1) ? 0x0C0C0706u : 0x0C0C0504u) : ((c32 & 1) ? 0x0C0C0302u : 0x0C0C0100u);
+    const int p16 = bx & 1, p32 = c32 + 4 * (by2 & 1);
+    const int L   = 2 * bx;
+    for (int ty = y0; ty < y1; ty += 2) {
+        const int tyh = min(ty + hr, y1 - 1); // an odd band: half 1 repeats the last row (same keys)
+        for (int set = 0; set < nsets; set++) {
+            const int tq = set * FPW_TQ;
+            unsigned long long acc[2][FPW_TQ];
+#pragma unroll
+            for (int blk = 0; blk < 2; blk++)
+#pragma unroll
+                for (int iq = 0; iq < FPW_TQ; iq++) acc[blk][iq] = 0;
+#pragma unroll
+            for (int blk = 0; blk < 2; blk++)
+#pragma unroll
+                for (int rr = 0; rr < ROWS; rr++) {
+                    const int ro = (tyh - Y0 + (2 * by2 + blk) * 8 + rr * RSTEP) * FPW_PITCH + L + tq;
+                    const uint2 *pa = (const uint2 *)(fw_a + ro), *pb = (const uint2 *)(fw_b + ro);
+                    uint2 q[FPW_TQ + 1]; // q[j] = (A[j], A[j + 1])
+#pragma unroll
+                    for (int i = 0; i <= FPW_TQ / 2; i++) q[2 * i] = pa[i];
+#pragma unroll
+                    for (int i = 0; i < FPW_TQ / 2; i++) q[2 * i + 1] = pb[i];
+#pragma unroll
+                    for (int iq = 0; iq < FPW_TQ; iq++) {
+                        acc[blk][iq] = qsad(q[iq].x, q[iq].y, src[blk][rr][0], acc[blk][iq]);
+                        acc[blk][iq] = qsad(q[iq + 1].x, q[iq + 1].y, src[blk][rr][1], acc[blk][iq]);
+                    }
+                }
+            // the SADs exist here: otherwise the compiler sinks the qsads of the
+            // later pairs into their (conditional) uses and keeps every row live
+#pragma unroll
+            for (int blk = 0; blk < 2; blk++)
+#pragma unroll
+                for (int iq = 0; iq < FPW_TQ; iq++) asm volatile("" : "+v"(acc[blk][iq]));
+            FpW m{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            const int left = w - 4 * tq; // positions of the area in this set (wave-uniform)
+#pragma unroll
+            for (int pp = 0; pp < FPW_TQ / 2; pp++) {
+                const int ev = left - 8 * pp;
+                if (ev <= 0)
+                    break;
+                if (ev >= 8)
+                    fpw_pair<false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1], 8 * pp,
+                                    8, sel16, sel32, p16, p32);
+                else
+                    fpw_pair<true>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1], 8 * pp,
+                                   ev + 8 * pp, sel16, sel32, p16, p32);
+            }
+            const uint32_t ob = obase + (uint32_t)(tyh * w + 4 * tq);
+            b.b8t = fpw_rebase(b.b8t, m.b8t, ob);
+            b.b8b = fpw_rebase(b.b8b, m.b8b, ob);
+            b.b16 = fpw_rebase(b.b16, m.b16, ob + (uint32_t)p16);
+            b.b32 = fpw_rebase(b.b32, m.b32, ob + (uint32_t)p32);
+            b.b64 = fpw_rebase(b.b64, m.b64, ob + (uint32_t)p32);
+        }
+    }
+    // both halves, then the lanes of each class
+    b.b8t = fpw_min_hr(b.b8t), b.b8b = fpw_min_hr(b.b8b), b.b16 = fpw_min_hr(b.b16);
+    b.b32 = fpw_min_hr(b.b32), b.b64 = fpw_min_hr(b.b64);
+    // 16x16: the two parities (bx ^ 1); 32x32: the 4 positions of quad a / b (bx ^ 1,
+    // bx ^ 2) and the two rows (by2 ^ 1); 64x64: every lane
+    b.b16 = min_u32(b.b16, (uint32_t)__builtin_amdgcn_update_dpp((int)b.b16, (int)b.b16, 0xB1, 0xF, 0xF, false));
+    b.b32 = PuMin<true>::quad_min(b.b32);
+    {
+        const auto t = __builtin_amdgcn_permlane16_swap(b.b32, b.b32, false, false);
+        b.b32        = min_u32(t[0], t[1]);
+    }
+    b.b64 = wave_min_u32(b.b64);
+    auto out8 = [](uint32_t v) -> unsigned long long { // 16-bit orders; SUB SADs doubled
+        return v == 0xFFFFFFFFu ? ~0ull : ((unsigned long long)((v >> 16) << 1) << 32) | (v & 0xFFFFu);
+    };
+    auto out12 = [](uint32_t v) -> unsigned long long {
+        return v == 0xFFFFFFFFu ? ~0ull : ((unsigned long long)((v >> 12) << 1) << 32) | (v & 0xFFFu);
+    };
+    auto morton = [](int y, int x) { // Z order of the 85-PU table (by bits odd, bx bits even)
+        return (x & 1) | ((y & 1) << 1) | ((x & 2) << 1) | ((y & 2) << 2) | ((x & 4) << 2) | ((y & 4) << 3);
+    };
+    if (hr == 0) {
+        atomicMin(&kp[21 + morton(2 * by2, bx)], out8(b.b8t));
+        atomicMin(&kp[21 + morton(2 * by2 + 1, bx)], out8(b.b8b));
+        if ((bx & 1) == 0)
+            atomicMin(&kp[5 + morton(by2, bx >> 1)], out8(b.b16));
+        if ((bx & 3) == 0 && (by2 & 1) == 0)
+            atomicMin(&kp[1 + morton(by2 >> 1, bx >> 2)], out12(b.b32));
+        if (lane == 0)
+            atomicMin(&kp[0], out12(b.b64));
+    }
+    if (part == 0 && lane == 0)
+        *cs = CSlot{hme_sad, zz, sc_x, sc_y, A.xo, A.yo, A.w, A.xc, A.yc, 1, dref, (uint8_t)A.probe, 0};
 }
 
 // Per SB: decode the argmin keys kb[k][85] of the R records (slot state cin[k])
@@ -3437,12 +3778,29 @@ extern "C" bool svtme_fp_wide(const svtme_controls *c) {
     return c->me_sa.sa_min.width >= 24 && c->me_sa.sa_max.width >= 24;
 }
 
+// k_fp_wide applies: sub-sampled rows, 32-bit keys, a wide area of more than one
+// band, and the window of 4 bands in its LDS rows (FPW_PITCH dwords, bands of
+// at most 8 rows with up to 16 parts)
+extern "C" bool svtme_fp_wide_lds(const svtme_controls *c) {
+    if (c->me_search_method == SVTME_FULL_SAD_SEARCH || c->enable_me_sr_adjustment == 2 || !svtme_fp_k32(c) ||
+        !svtme_fp_wide(c) || getenv("SVTME_NO_FP_WIDE"))
+        return false;
+    uint32_t w, h;
+    fp_area_bound(c, &w, &h);
+    const uint32_t nsets = ((w + 3) / 4 + FPW_TQ - 1) / FPW_TQ;
+    return (w * h) / 512 >= 2 && 14 + nsets * FPW_TQ + 2 + 1 <= FPW_PITCH && h <= 8 * 16;
+}
+
 extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {
     if (c->enable_me_sr_adjustment == 2)
         return 0; // slot 0's 64x64 SAD feeds the other slots' areas: per-SB k_stage_c
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
-    const uint32_t parts = (w * h) / 512;
+    uint32_t parts = (w * h) / 512;
+    if (svtme_fp_wide_lds(c)) { // workgroups of 4 bands of <= 8 rows
+        parts = parts > (h + 7) / 8 ? parts : (h + 7) / 8;
+        parts = (parts + 3) & ~3u;
+    }
     return parts < 1 ? 1 : (parts > 16 ? 16 : parts);
 }
 
@@ -3453,7 +3811,7 @@ extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
     return (uint32_t)full | (uint32_t)(dj->parts != 0) << 1 | (uint32_t)svtme_fp_k32(&dj->job.ctrl) << 2 |
            (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4 |
            (uint32_t)(dj->parts == 1) << 5 | (uint32_t)svtme_fp_wide(&dj->job.ctrl) << 6 |
-           (uint32_t)svtme_hme_rt(&dj->job.ctrl) << 7;
+           (uint32_t)svtme_hme_rt(&dj->job.ctrl) << 7 | (uint32_t)svtme_fp_wide_lds(&dj->job.ctrl) << 8;
 }
 
 static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
@@ -3535,7 +3893,9 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
         const DevBatch bc = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.R * j.parts; });
         const dim3 grid((bc.total + 3) / 4);
         const bool wide = svtme_fp_wide(&h0.job.ctrl);
-        if (full && k32 && wide)
+        if (svtme_fp_wide_lds(&h0.job.ctrl))
+            SVTME_LAUNCH(svtme::k_fp_wide, grid, 3, bc);
+        else if (full && k32 && wide)
             SVTME_LAUNCH((svtme::k_stage_c1<false, true, true>), grid, 3, bc);
         else if (full && k32)
             SVTME_LAUNCH((svtme::k_stage_c1<false, true>), grid, 3, bc);
