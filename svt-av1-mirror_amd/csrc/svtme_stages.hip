@@ -2649,7 +2649,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
 //
 // A workgroup takes 4 consecutive row bands (parts) of one (SB, reference): it
 // stages the window rows of all 4 once, realigned to position 0 (fw_a) and
-// shifted by one dword (fw_b[j] = fw_a[j + 1]), so every reference dword pair a
+// shifted by one dword (fw_b[j] = fw_a[j + 1], beside fw_a in the row), so every reference dword pair a
 // qsad reads is one 8-byte LDS read, even pairs from fw_a and odd pairs from
 // fw_b: no v_alignbyte, no register moves for misaligned pairs, and the L1 /
 // TA path idle during the search.
@@ -2663,8 +2663,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
 // the position within the set (inline constants), the set's raster order is
 // added once per set.
 // ============================================================================
-#define FPW_PITCH 48 // dwords per LDS row: 192 bytes = 64 (mod 128), so the two search rows
-                     // of a 16-lane read group (hr = 0, 1) fall on disjoint bank halves
+#define FPW_PITCH 80 // dwords per LDS row (fw_a then fw_b): 320 bytes = 64 (mod 128), so the two
+                     // search rows of a 16-lane read group (hr = 0, 1) fall on disjoint bank halves
+#define FPW_BOFF 40  // fw_b within the row: one base address serves both copies
 #define FPW_ROWS 96  // window rows per workgroup (4 bands + 62; the host bounds the band height)
 #ifndef FPW_TQ
 #define FPW_TQ 4 // position quads per set (2 quad pairs, 16 positions; 6 wastes a third of the
@@ -2735,8 +2736,11 @@ __device__ __forceinline__ uint32_t fpw_rebase(uint32_t b, uint32_t m, uint32_t 
     return min_u32(b, m == 0xFFFFFFFFu ? m : m + base);
 }
 
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) k_fp_wide(const DevBatch B) {
-    __shared__ uint32_t fw_a[FPW_ROWS * FPW_PITCH], fw_b[FPW_ROWS * FPW_PITCH];
+#ifndef FPW_WAVES
+#define FPW_WAVES 5 // waves per SIMD: 5 workgroups of 30 KB LDS per CU
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WAVES, FPW_WAVES))) k_fp_wide(const DevBatch B) {
+    __shared__ __attribute__((aligned(16))) uint32_t fw[FPW_ROWS * FPW_PITCH]; // rows: fw_a | fw_b
     constexpr int ROWS = 4, RSTEP = 2; // sub-sampled rows
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
@@ -2837,31 +2841,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
     const int ndw    = 14 + (nsets - 1) * FPW_TQ + FPW_TQ + 2; // fw_a dwords a lane's pairs reach
     const int nrows  = Y1 - Y0 + 62;
     {
-        const uint32_t mrow = magic_u32((uint32_t)(ndw + 1));
-        const int total     = nrows * (ndw + 1);
+        // groups of 4 dwords: fw_a[4 g .. 4 g + 3] and fw_b[4 g .. 4 g + 3] from the raw
+        // dwords 4 g .. 4 g + 5 of the row (one 16-byte and two 4-byte loads)
+        const int ng        = (ndw + 1 + 3) >> 2;
+        const uint32_t mg   = magic_u32((uint32_t)ng);
+        const int total     = nrows * ng;
         for (int i0 = 0; i0 < total; i0 += 4 * 256) {
-            uint32_t r0[4], r1[4];
-            int row[4], j[4];
+            u32x4a4 r[4];
+            uint32_t r4[4], r5[4];
+            int row[4], gq[4];
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 const int i = i0 + t * 256 + (int)threadIdx.x;
-                row[t]      = mdiv(i, mrow);
-                j[t]        = i - row[t] * (ndw + 1);
-                r0[t] = r1[t] = 0;
+                row[t]      = mdiv(i, mg);
+                gq[t]       = i - row[t] * ng;
                 if (i < total) {
-                    const uint32_t off = ((uint32_t)(Y0 + row[t]) * (uint32_t)sdw + (uint32_t)j[t]) * 4u;
-                    r0[t] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, 0, 0);
-                    r1[t] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 4u), 0, 0);
+                    const uint32_t off = ((uint32_t)(Y0 + row[t]) * (uint32_t)sdw + 4u * (uint32_t)gq[t]) * 4u;
+                    r[t]  = bld4(rs, off, 0);
+                    r4[t] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 16u), 0, 0);
+                    r5[t] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 20u), 0, 0);
                 }
             }
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 const int i = i0 + t * 256 + (int)threadIdx.x;
                 if (i < total) {
-                    const uint32_t v = __builtin_amdgcn_alignbyte(r1[t], r0[t], (uint32_t)sh);
-                    fw_a[row[t] * FPW_PITCH + j[t]] = v;
-                    if (j[t] > 0)
-                        fw_b[row[t] * FPW_PITCH + j[t] - 1] = v;
+                    const uint32_t a0 = __builtin_amdgcn_alignbyte(r[t].y, r[t].x, (uint32_t)sh);
+                    const uint32_t a1 = __builtin_amdgcn_alignbyte(r[t].z, r[t].y, (uint32_t)sh);
+                    const uint32_t a2 = __builtin_amdgcn_alignbyte(r[t].w, r[t].z, (uint32_t)sh);
+                    const uint32_t a3 = __builtin_amdgcn_alignbyte(r4[t], r[t].w, (uint32_t)sh);
+                    const uint32_t a4 = __builtin_amdgcn_alignbyte(r5[t], r4[t], (uint32_t)sh);
+                    uint32_t *d = fw + row[t] * FPW_PITCH + 4 * gq[t];
+                    *(uint4 *)d              = make_uint4(a0, a1, a2, a3);
+                    *(uint4 *)(d + FPW_BOFF) = make_uint4(a1, a2, a3, a4);
                 }
             }
         }
@@ -2889,7 +2901,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
 #pragma unroll
                 for (int rr = 0; rr < ROWS; rr++) {
                     const int ro = (tyh - Y0 + (2 * by2 + blk) * 8 + rr * RSTEP) * FPW_PITCH + L + tq;
-                    const uint2 *pa = (const uint2 *)(fw_a + ro), *pb = (const uint2 *)(fw_b + ro);
+                    const uint2 *pa = (const uint2 *)(fw + ro), *pb = (const uint2 *)(fw + ro + FPW_BOFF);
                     uint2 q[FPW_TQ + 1]; // q[j] = (A[j], A[j + 1])
 #pragma unroll
                     for (int i = 0; i <= FPW_TQ / 2; i++) q[2 * i] = pa[i];
@@ -2922,11 +2934,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))
                                    ev + 8 * pp, sel16, sel32, p16, p32);
             }
             const uint32_t ob = obase + (uint32_t)(tyh * w + 4 * tq);
-            b.b8t = fpw_rebase(b.b8t, m.b8t, ob);
-            b.b8b = fpw_rebase(b.b8b, m.b8b, ob);
-            b.b16 = fpw_rebase(b.b16, m.b16, ob + (uint32_t)p16);
-            b.b32 = fpw_rebase(b.b32, m.b32, ob + (uint32_t)p32);
-            b.b64 = fpw_rebase(b.b64, m.b64, ob + (uint32_t)p32);
+            if (left >= 8) { // a whole first pair: every class of every lane has a key
+                b.b8t = min_u32(b.b8t, m.b8t + ob);
+                b.b8b = min_u32(b.b8b, m.b8b + ob);
+                b.b16 = min_u32(b.b16, m.b16 + ob + (uint32_t)p16);
+                b.b32 = min_u32(b.b32, m.b32 + ob + (uint32_t)p32);
+                b.b64 = min_u32(b.b64, m.b64 + ob + (uint32_t)p32);
+            } else {
+                b.b8t = fpw_rebase(b.b8t, m.b8t, ob);
+                b.b8b = fpw_rebase(b.b8b, m.b8b, ob);
+                b.b16 = fpw_rebase(b.b16, m.b16, ob + (uint32_t)p16);
+                b.b32 = fpw_rebase(b.b32, m.b32, ob + (uint32_t)p32);
+                b.b64 = fpw_rebase(b.b64, m.b64, ob + (uint32_t)p32);
+            }
         }
     }
     // both halves, then the lanes of each class
@@ -3788,7 +3808,7 @@ extern "C" bool svtme_fp_wide_lds(const svtme_controls *c) {
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
     const uint32_t nsets = ((w + 3) / 4 + FPW_TQ - 1) / FPW_TQ;
-    return (w * h) / 512 >= 2 && 14 + nsets * FPW_TQ + 2 + 1 <= FPW_PITCH && h <= 8 * 16;
+    return (w * h) / 512 >= 2 && 14 + nsets * FPW_TQ + 2 + 1 <= FPW_BOFF && h <= 8 * 16;
 }
 
 extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {
