@@ -3,7 +3,7 @@
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/fpwide_ab; mkdir -p $O
 for L in $LIBS; do
-  SVTME_LIB=svt-av1-mirror_amd/$L.so timeout -k 10 300 python3 -u -m pytest tests/test_configs.py tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/t_$L.log 2>&1 || { tail -20 $O/t_$L.log; exit 1; }
+  SVTME_LIB=svt-av1-mirror_amd/$L.so timeout -k 10 300 python3 -u -m pytest tests/test_configs.py tests/test_gpu_parity.py tests/test_gpu_fpwide.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/t_$L.log 2>&1 || { tail -20 $O/t_$L.log; exit 1; }
   echo "$L $(tail -1 $O/t_$L.log)"
 done
 for r in 1 2; do

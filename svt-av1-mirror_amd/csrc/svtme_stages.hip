@@ -2736,6 +2736,9 @@ __device__ __forceinline__ uint32_t fpw_rebase(uint32_t b, uint32_t m, uint32_t 
     return min_u32(b, m == 0xFFFFFFFFu ? m : m + base);
 }
 
+#ifndef FPW_W0
+#define FPW_W0 1 // the per-(SB, reference) prologue by wave 0 only
+#endif
 #ifndef FPW_WAVES
 #define FPW_WAVES 5 // waves per SIMD: 5 workgroups of 30 KB LDS per CU
 #endif
@@ -2775,58 +2778,88 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
             src[blk][rr][0] = sp[0];
             src[blk][rr][1] = sp[1];
         }
-    const SlotCentre scv   = final_centre(job, dj.bst + sb_local, valid_mask(job));
-    const uint64_t hme_sad = rl64(scv.hme_sad, s);
-    const uint32_t zz = rl32(scv.zz, s), rdiv = rl32(scv.reduce_div, s);
-    const int16_t sc_x    = (int16_t)rl32((uint32_t)(int32_t)scv.sc_x, s);
-    const int16_t sc_y    = (int16_t)rl32((uint32_t)(int32_t)scv.sc_y, s);
-    const uint8_t dref    = (uint8_t)rl32(scv.do_ref, s);
-    const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
-    CSlot *cs             = dj.cslot + (size_t)sb_local * dj.R + k;
+    CSlot *cs              = dj.cslot + (size_t)sb_local * dj.R + k;
     unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
-    if (!dref || tf_exit) { // the same for the workgroup's 4 bands
-        if (part == 0 && lane == 0)
-            *cs = CSlot{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
-        return;
-    }
-    const DevPlane &P = dj.ref[s >> 2][s & 3].lv[0];
-    const int sdw     = P.stride >> 2;
+    const DevPlane &P      = dj.ref[s >> 2][s & 3].lv[0];
+    const int sdw          = P.stride >> 2;
     FpW b{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    const FpArea A = fp_area(dj, G, s, zz, rdiv, sc_x, sc_y, [&](const uint8_t *g) {
-        // the centre: both blocks' raw 8x8 SADs (order 0 in every class)
-        g                                 = uni_ptr(g);
-        const int sh                      = (int)((uintptr_t)g & 3);
-        const __amdgpu_buffer_rsrc_t rs   = plane_rsrc(g - sh);
-        uint32_t s8[2];
-#pragma unroll
-        for (int blk = 0; blk < 2; blk++) {
-            const uint32_t lo = (uint32_t)(((2 * by2 + blk) * 8) * sdw + bx * 2) * 4u;
-            u32x4a4 d[ROWS];
-#pragma unroll
-            for (int rr = 0; rr < ROWS; rr++) d[rr] = bld4(rs, lo, (uint32_t)(rr * RSTEP * sdw) * 4u);
-            uint32_t a = 0;
-#pragma unroll
-            for (int rr = 0; rr < ROWS; rr++) {
-                a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d[rr].y, d[rr].x, (uint32_t)sh), src[blk][rr][0], a);
-                a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d[rr].z, d[rr].y, (uint32_t)sh), src[blk][rr][1], a);
-            }
-            s8[blk] = a;
+    // search centre, area and centre probe: the same for the workgroup's 4 bands,
+    // made by wave 0 and handed to the others through LDS (FPW_W0 = 0: every wave)
+    auto prologue = [&](FpArea &A) -> bool {
+        const SlotCentre scv   = final_centre(job, dj.bst + sb_local, valid_mask(job));
+        const uint64_t hme_sad = rl64(scv.hme_sad, s);
+        const uint32_t zz = rl32(scv.zz, s), rdiv = rl32(scv.reduce_div, s);
+        const int16_t sc_x    = (int16_t)rl32((uint32_t)(int32_t)scv.sc_x, s);
+        const int16_t sc_y    = (int16_t)rl32((uint32_t)(int32_t)scv.sc_y, s);
+        const uint8_t dref    = (uint8_t)rl32(scv.do_ref, s);
+        const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
+        if (!dref || tf_exit) {
+            if (part == 0 && lane == 0)
+                *cs = CSlot{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
+            return false;
         }
-        const uint32_t s16 = dpp_add<0xB1>(s8[0] + s8[1]);
-        const uint32_t s32h = dpp_add<0x4E>(s16);
-        const auto w16 = __builtin_amdgcn_permlane16_swap(s32h, s32h, false, false);
-        const uint32_t s32 = w16[0] + w16[1];
-        const uint32_t s64h = dpp_add<0x141>(s32);
-        const auto w32 = __builtin_amdgcn_permlane32_swap(s64h, s64h, false, false);
-        const uint32_t s64 = w32[0] + w32[1];
-        b.b8t = s8[0] << 16, b.b8b = s8[1] << 16, b.b16 = s16 << 16, b.b32 = s32 << 12, b.b64 = s64 << 12;
-        // the variance of the 64 8x8 SADs as the reference counts them (doubled); every
-        // block sits in two lanes (hr = 0, 1)
-        const uint32_t p8t = s8[0] << 1, p8b = s8[1] << 1;
-        const uint32_t mean = (wave_sum_u32(p8t + p8b) >> 1) / 64;
-        const int32_t dt = (int32_t)p8t - (int32_t)mean, db = (int32_t)p8b - (int32_t)mean;
-        return (wave_sum_u32((uint32_t)(dt * dt) + (uint32_t)(db * db)) >> 1) / 64;
-    });
+        A = fp_area(dj, G, s, zz, rdiv, sc_x, sc_y, [&](const uint8_t *g) {
+            // the centre: both blocks' raw 8x8 SADs (order 0 in every class)
+            g                                 = uni_ptr(g);
+            const int sh                      = (int)((uintptr_t)g & 3);
+            const __amdgpu_buffer_rsrc_t rs   = plane_rsrc(g - sh);
+            uint32_t s8[2];
+#pragma unroll
+            for (int blk = 0; blk < 2; blk++) {
+                const uint32_t lo = (uint32_t)(((2 * by2 + blk) * 8) * sdw + bx * 2) * 4u;
+                u32x4a4 d[ROWS];
+#pragma unroll
+                for (int rr = 0; rr < ROWS; rr++) d[rr] = bld4(rs, lo, (uint32_t)(rr * RSTEP * sdw) * 4u);
+                uint32_t a = 0;
+#pragma unroll
+                for (int rr = 0; rr < ROWS; rr++) {
+                    a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d[rr].y, d[rr].x, (uint32_t)sh), src[blk][rr][0], a);
+                    a = __builtin_amdgcn_sad_u8(__builtin_amdgcn_alignbyte(d[rr].z, d[rr].y, (uint32_t)sh), src[blk][rr][1], a);
+                }
+                s8[blk] = a;
+            }
+            const uint32_t s16 = dpp_add<0xB1>(s8[0] + s8[1]);
+            const uint32_t s32h = dpp_add<0x4E>(s16);
+            const auto w16 = __builtin_amdgcn_permlane16_swap(s32h, s32h, false, false);
+            const uint32_t s32 = w16[0] + w16[1];
+            const uint32_t s64h = dpp_add<0x141>(s32);
+            const auto w32 = __builtin_amdgcn_permlane32_swap(s64h, s64h, false, false);
+            const uint32_t s64 = w32[0] + w32[1];
+            b.b8t = s8[0] << 16, b.b8b = s8[1] << 16, b.b16 = s16 << 16, b.b32 = s32 << 12, b.b64 = s64 << 12;
+            // the variance of the 64 8x8 SADs as the reference counts them (doubled); every
+            // block sits in two lanes (hr = 0, 1)
+            const uint32_t p8t = s8[0] << 1, p8b = s8[1] << 1;
+            const uint32_t mean = (wave_sum_u32(p8t + p8b) >> 1) / 64;
+            const int32_t dt = (int32_t)p8t - (int32_t)mean, db = (int32_t)p8b - (int32_t)mean;
+            return (wave_sum_u32((uint32_t)(dt * dt) + (uint32_t)(db * db)) >> 1) / 64;
+        });
+        if (part == 0 && lane == 0)
+            *cs = CSlot{hme_sad, zz, sc_x, sc_y, A.xo, A.yo, A.w, A.xc, A.yc, 1, dref, (uint8_t)A.probe, 0};
+        return true;
+    };
+    FpArea A;
+#if FPW_W0
+    __shared__ FpArea fx_area;
+    __shared__ uint32_t fx_keys[5][64], fx_run;
+    if (wid == 0) {
+        const bool run = prologue(A);
+        if (lane == 0) {
+            fx_run  = run;
+            fx_area = A;
+        }
+        fx_keys[0][lane] = b.b8t, fx_keys[1][lane] = b.b8b, fx_keys[2][lane] = b.b16;
+        fx_keys[3][lane] = b.b32, fx_keys[4][lane] = b.b64;
+    }
+    __syncthreads();
+    if (!fx_run)
+        return;
+    A     = fx_area;
+    b.b8t = fx_keys[0][lane], b.b8b = fx_keys[1][lane], b.b16 = fx_keys[2][lane];
+    b.b32 = fx_keys[3][lane], b.b64 = fx_keys[4][lane];
+#else
+    if (!prologue(A))
+        return;
+#endif
     const int w = A.w, h = A.h;
 
     // stage the rows [Y0, Y1 + 62) of the 4 bands: fw_a[row][j] = window dword j
@@ -2980,8 +3013,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
         if (lane == 0)
             atomicMin(&kp[0], out12(b.b64));
     }
-    if (part == 0 && lane == 0)
-        *cs = CSlot{hme_sad, zz, sc_x, sc_y, A.xo, A.yo, A.w, A.xc, A.yc, 1, dref, (uint8_t)A.probe, 0};
 }
 
 // Per SB: decode the argmin keys kb[k][85] of the R records (slot state cin[k])
