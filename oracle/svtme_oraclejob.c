@@ -182,12 +182,6 @@ svtme_status svtme_submit_picture(svtme_ctx *c, const svtme_job *job, svtme_ref_
                                   svtme_sb_result *sb_results) {
     if (!c || !job || !ref_records)
         return ora_fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_picture: null argument");
-    /* the GPU library's validator (svtme_host.cpp validate_job): the real-time
-     * HME-L0 reduction only where its fused HME kernel runs */
-    if (job->ctrl.enable_me_sr_adjustment && job->ctrl.distance_based_hme_resizing &&
-        job->ctrl.reduce_hme_l0_sr_th_min && job->ctrl.reduce_hme_l0_sr_th_max &&
-        ((job->width % 64) || job->ctrl.hme_search_method == SVTME_FULL_SAD_SEARCH))
-        return ora_fail(SVTME_ERR_BAD_PARAMETER, "reduce_hme_l0_sr_th needs a width that is a multiple of 64");
     pthread_mutex_lock(&c->mu);
     svtme_status st = SVTME_OK;
     const struct OraPic *cur = find(c, job->picture_number);

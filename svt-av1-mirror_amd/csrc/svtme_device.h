@@ -53,6 +53,10 @@ struct BState {
     int16_t hx[8][4], hy[8][4];
     uint32_t zz[8];
     uint8_t do_ref[8];
+    // real-time tune on the split path (k_stage_d<true>): the HME-L0 area of
+    // every slot from slot 0's centre, and the slots whose HME-L0 runs (bit s)
+    int16_t rt_sa[8][2];
+    uint8_t rt_need;
 };
 
 // Per (SB, reference record) state the wide full-pel stage (k_stage_c1)
@@ -78,6 +82,8 @@ struct DevJob {
     BState *bst;                   // [sb_count] stage-B state
     uint32_t ta_count;             // stage-A searches per SB
     uint8_t ta_list[SVTME_A_N];    // their ARes indices
+    uint32_t ta1_count;            // real-time tune, split path: the second stage-A round
+    uint8_t ta1_list[8];           // (TA_L0RT << 3 | slot)
     uint32_t tb_count;             // stage-B refinements per SB
     uint8_t tb_list[32];           // their (slot << 2 | quadrant)
     unsigned long long *keys;      // [sb_count][R][85] full-pel argmin keys (sad << 32 | order)

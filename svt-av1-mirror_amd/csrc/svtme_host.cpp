@@ -34,6 +34,7 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
 extern "C" uint32_t svtme_launch_key(const DevJob *dj);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
+extern "C" void svtme_stage_a1_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" uint32_t svtme_fp_parts(const svtme_controls *c);
 extern "C" void svtme_hme_prepare(DevJob *dj);
 extern "C" bool svtme_hme_fused(const svtme_job *job);
@@ -516,9 +517,6 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
     if (job->ctrl.num_hme_sa_w != 2 || job->ctrl.num_hme_sa_h != 2)
         return fail(SVTME_ERR_BAD_PARAMETER, "only 2x2 HME-L0 search regions are supported "
                                              "(motion_estimation.c:1875)");
-    if (svtme_hme_rt(&job->ctrl) && !svtme_hme_fused(job))
-        return fail(SVTME_ERR_BAD_PARAMETER, "reduce_hme_l0_sr_th_min/max (real-time tune, enc_mode_config.c:692-704) "
-                                             "need a width that is a multiple of 64 (the fused HME kernel)");
     if (job->me_type != 0 && job->me_type != SVTME_ME_OPEN_LOOP && job->me_type != SVTME_ME_MCTF)
         return fail(SVTME_ERR_BAD_PARAMETER, "me_type %u is neither SVTME_ME_OPEN_LOOP nor SVTME_ME_MCTF",
                     job->me_type);
@@ -654,6 +652,7 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
         hj[k].keys  = hj[k].parts ? L.d_keys + slot_off * SVTME_PU_COUNT : nullptr;
         hj[k].cslot = hj[k].parts ? L.d_cslot + slot_off : nullptr;
         svtme_stage_a_list(&hj[k].job, hj[k].ta_list, &hj[k].ta_count);
+        svtme_stage_a1_list(&hj[k].job, hj[k].ta1_list, &hj[k].ta1_count);
         svtme_stage_b_list(&hj[k].job, hj[k].tb_list, &hj[k].tb_count);
         svtme_hme_prepare(&hj[k]);
         sb_off += count[k];

@@ -34,6 +34,8 @@
 
 #include "svtme_me_common.h"
 
+extern "C" bool svtme_hme_rt(const svtme_controls *c); // (host dispatch, end of file)
+
 namespace svtme {
 
 
@@ -439,9 +441,12 @@ __device__ __forceinline__ uint32_t zz_finish(const ZzLoads &z) {
 }
 
 // Stage A wave kinds (DevJob.ta_list entry = kind << 3 | slot)
-#define TA_HME 0 // zz SAD + the four HME-L0 quadrants of one slot
-#define TA_PH 1  // the two pre-HME regions of one slot
+#define TA_HME 0   // zz SAD + the four HME-L0 quadrants of one slot
+#define TA_PH 1    // the two pre-HME regions of one slot
+#define TA_ZZ 2    // zz SAD only (real-time tune, slots 1-7: their HME-L0 waits for slot 0's)
+#define TA_L0RT 3  // the four HME-L0 quadrants with the area k_stage_d<true> left in BState
 
+template <bool R1> // R1: the real-time tune's second round (DevJob.ta1_list)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_stage_a(const DevBatch B) {
     __shared__ __attribute__((aligned(16))) uint8_t srcb[4][256];
     __shared__ uint32_t wbuf[4][STAGE_A_BUF_DW];
@@ -453,8 +458,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))
     const DevJob &dj        = batch_job(B, u, &gw);
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
-    const uint32_t sb_local = UNI(gw / dj.ta_count);
-    const int entry         = UNI(dj.ta_list[gw - sb_local * dj.ta_count]);
+    const uint32_t tac      = R1 ? dj.ta1_count : dj.ta_count;
+    const uint32_t sb_local = UNI(gw / tac);
+    const int entry         = UNI((R1 ? dj.ta1_list : dj.ta_list)[gw - sb_local * tac]);
     const int kind = entry >> 3, s = entry & 7, l = s >> 2, r = s & 3;
     const SbGeo G   = sb_geo(dj, sb_local);
     ARes *out       = dj.ares + (size_t)sb_local * SVTME_A_N;
@@ -471,9 +477,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))
     const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
     const int bws = (int)(G.bw >> 2), bhs = hsub ? (int)(G.bh >> 2) >> 1 : (int)(G.bh >> 2);
 
-    if (kind == TA_HME) {
+    if (kind != TA_PH) {
+        // real-time tune, second round: only the slots whose HME-L0 runs
+        const BState *rb = dj.bst + sb_local;
+        if (kind == TA_L0RT && !((rb->rt_need >> s) & 1u))
+            return;
         // zz SAD (init_zz_sad, motion_estimation.c:2382-2437)
-        const bool zz   = c.me_early_exit_th || c.me_safe_limit_zz_th;
+        const bool zz   = kind != TA_L0RT && (c.me_early_exit_th || c.me_safe_limit_zz_th);
         const bool zz64 = zz && G.bw == 64 && G.bh == 64;
         const DevPlane &F = dj.ref[l][r].lv[0];
         const DevPlane &C = dj.cur.lv[0];
@@ -483,13 +493,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))
         if (zz64)
             zz_issue(zl, zr, 2 * F.stride, zc, 2 * C.stride);
         // the four HME-L0 quadrants (hme_level_0, motion_estimation.c:835-889), staged as one box
-        const bool l0 = c.enable_hme_flag && c.enable_hme_level0_flag;
+        const bool l0 = kind != TA_ZZ && c.enable_hme_flag && c.enable_hme_level0_flag;
         SadGeo gq[4];
         int16_t qxo[4], qyo[4];
         int boxl = 0x7fff, boxt = 0x7fff, wdwb = 0, wrowsb = 0;
         if (l0) {
             int16_t sa_w, sa_h;
-            hme_l0_area(c, l, r, dist, 0, 0, &sa_w, &sa_h);
+            if (kind == TA_L0RT)
+                sa_w = rb->rt_sa[s][0], sa_h = rb->rt_sa[s][1];
+            else
+                hme_l0_area(c, l, r, dist, 0, 0, &sa_w, &sa_h);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 int16_t sw, shh;
@@ -788,6 +801,11 @@ __device__ __forceinline__ void dec_l0(Dec &d, const svtme_job &job, uint32_t vm
     }
 }
 
+// RT0 (real-time tune, between the two stage-A rounds): the decisions up to
+// slot 0's HME-L0 centre, then the HME-L0 areas of slots 1-7 from it
+// (get_hme_l0_search_area, motion_estimation.c:1800-1867) and the slots whose
+// HME-L0 runs (dec_l0's exits) into BState for the second round
+template <bool RT0>
 __global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
     __shared__ Dec dec[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -807,6 +825,27 @@ __global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
     dec_prehme(d, job, vmask);
     dec_l0(d, job, vmask);
     BState *b = dj.bst + sb_local;
+    if constexpr (RT0) {
+        const svtme_controls &c = job.ctrl;
+        const int s = lane, l = s >> 2;
+        bool run    = s > 0 && s < 8 && slot_valid(vmask, s) && tl_or_l0(job, l) && d.do_ref[s] &&
+                   !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2));
+        if (run && c.prev_me_stage_based_exit_th) {
+            const int k = d.ph[s][0].sad <= d.ph[s][1].sad ? 0 : 1;
+            run = !(d.ph[s][k].performed && d.ph[s][k].sad < (c.prev_me_stage_based_exit_th >> 4));
+        }
+        const uint32_t need = (uint32_t)__ballot(run);
+        if (s < 8) {
+            int16_t w = 0, h = 0;
+            if (slot_valid(vmask, s))
+                hme_l0_area(c, l, s & 3, dj.sdist[s], d.lx[0][0], d.ly[0][0], &w, &h);
+            b->rt_sa[s][0] = w;
+            b->rt_sa[s][1] = h;
+        }
+        if (lane == 0)
+            b->rt_need = (uint8_t)need;
+        return;
+    }
     if (lane < 32) {
         (&b->lx[0][0])[lane]   = (&d.lx[0][0])[lane];
         (&b->ly[0][0])[lane]   = (&d.ly[0][0])[lane];
@@ -3728,11 +3767,33 @@ extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t
             continue;
         if (!(job->temporal_layer_index > 0 || l == 0))
             continue;
-        if (c.me_early_exit_th || c.me_safe_limit_zz_th || (c.enable_hme_flag && c.enable_hme_level0_flag))
+        const bool zz = c.me_early_exit_th || c.me_safe_limit_zz_th;
+        const bool l0 = c.enable_hme_flag && c.enable_hme_level0_flag;
+        if (svtme_hme_rt(&c) && s > 0) { // HME-L0 in the second round (svtme_stage_a1_list)
+            if (zz)
+                list[n++] = (uint8_t)((TA_ZZ << 3) | s);
+        } else if (zz || l0)
             list[n++] = (uint8_t)((TA_HME << 3) | s);
         if (c.prehme_enable)
             list[n++] = (uint8_t)((TA_PH << 3) | s);
     }
+    *count = n;
+}
+
+// Real-time tune on the split path: the second stage-A round, the HME-L0
+// quadrants of slots 1-7 (areas from slot 0's centre, k_stage_d<true>).
+extern "C" void svtme_stage_a1_list(const svtme_job *job, uint8_t *list, uint32_t *count) {
+    const svtme_controls &c = job->ctrl;
+    uint32_t n = 0;
+    if (svtme_hme_rt(&c) && c.enable_hme_flag && c.enable_hme_level0_flag)
+        for (int s = 1; s < 8; s++) {
+            const int l = s >> 2, r = s & 3;
+            if (l >= job->num_lists || r >= job->num_refs[l])
+                continue;
+            if (!(job->temporal_layer_index > 0 || l == 0))
+                continue;
+            list[n++] = (uint8_t)((TA_L0RT << 3) | s);
+        }
     *count = n;
 }
 
@@ -3905,7 +3966,7 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     const bool full = h0.job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     const bool k32  = svtme_fp_k32(&h0.job.ctrl);
     // the whole pass in one launch; SVTME_SPLIT_PASS=1 keeps k_hme -> k_stage_c1 -> k_stage_e (diagnostics)
-    const bool rt = svtme_hme_rt(&h0.job.ctrl); // (the validator keeps these jobs on k_hme)
+    const bool rt = svtme_hme_rt(&h0.job.ctrl); // the real-time tune's HME-L0 reduction
 #define SVTME_HME(FP, SUB, K32)                                                                                     \
     do {                                                                                                           \
         if (rt)                                                                                                    \
@@ -3929,8 +3990,15 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     } else {
     const DevBatch ba = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta_count; });
     if (ba.total)
-        SVTME_LAUNCH(svtme::k_stage_a, dim3((ba.total + 3) / 4), 0, ba);
-    SVTME_LAUNCH(svtme::k_stage_d, dim3((bd.total + 3) / 4), 1, bd);
+        SVTME_LAUNCH(svtme::k_stage_a<false>, dim3((ba.total + 3) / 4), 0, ba);
+    if (rt) { // the real-time tune: slot 0's HME-L0 centre, then the other slots' HME-L0
+        const DevBatch ba1 =
+            make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta1_count; });
+        hipLaunchKernelGGL(svtme::k_stage_d<true>, dim3((bd.total + 3) / 4), dim3(256), 0, s, bd);
+        if (ba1.total)
+            hipLaunchKernelGGL(svtme::k_stage_a<true>, dim3((ba1.total + 3) / 4), dim3(256), 0, s, ba1);
+    }
+    SVTME_LAUNCH(svtme::k_stage_d<false>, dim3((bd.total + 3) / 4), 1, bd);
     const DevBatch bb = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.tb_count; });
     if (bb.total) {
         if (h0.job.ctrl.enable_hme_level2_flag)

@@ -56,6 +56,7 @@ CASES = {
     "360p_p8_lowdelay": (640, 360, 16, 8, False, ["--pred-struct", "1"], True),
     "360p_p10_lowdelay": (640, 360, 16, 10, False, ["--pred-struct", "1"], True),
     "1080p_p9_lowdelay": (1920, 1080, 8, 9, False, ["--pred-struct", "1"], True),
+    "240p_p8_lowdelay": (426, 240, 16, 8, False, ["--pred-struct", "1"], True),
 }
 
 

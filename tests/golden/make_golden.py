@@ -68,6 +68,9 @@ ME_CASES = [
      {"ctrl": {"reduce_hme_l0_sr_th_min": 8, "reduce_hme_l0_sr_th_max": 100, "enable_me_sr_adjustment": 2}}),
     ("pan640_p8_rt200_adj2", "pan", 640, 360, 8, 1, (7, 6, 5), (9, 10),
      {"ctrl": {"reduce_hme_l0_sr_th_min": 8, "reduce_hme_l0_sr_th_max": 200, "enable_me_sr_adjustment": 2}}),
+    # a width that is not a multiple of 64: the split HME path's two stage-A rounds
+    ("vpan424_p8_rt100", "vpan", 424, 240, 8, 1, (7, 6), (9, 10),
+     {"ctrl": {"reduce_hme_l0_sr_th_min": 8, "reduce_hme_l0_sr_th_max": 100}}),
 ]
 
 TF_CASES = [

@@ -18,7 +18,7 @@ import pytest
 import encoder_harness as E
 
 CPU_CASES = ["ra360_p12", "240p_p8_ragged", "360p_p4", "360p_p8_notf", "360p_superres", "1080p_p8", "4k_p8",
-             "360p_p8_lowdelay", "360p_p10_lowdelay"]
+             "360p_p8_lowdelay", "360p_p10_lowdelay", "240p_p8_lowdelay"]
 GPU_CASES = list(E.CASES)
 
 

@@ -370,21 +370,10 @@ def test_picture_vs_reference_golden(svtme, gpu, case):
     assert S.records_checksum(recs, sbr) == case["checksum"]
 
 
-def test_realtime_reduction_needs_fused_width(svtme, gpu):
-    """reduce_hme_l0_sr_th runs on the fused HME kernel only (width a multiple
-    of 64): other widths are rejected, and the encoder glue falls back."""
-    S = svtme
-    ctrl = S.derive_controls(8, 35, S.input_resolution_of(424, 240), 1)
-    ctrl.reduce_hme_l0_sr_th_min, ctrl.reduce_hme_l0_sr_th_max = 8, 200
-    frames = S.test_frames("pan", 424, 240, [7, 8])
-    for t, f in frames.items():
-        gpu.upload(3100 + t, f)
-    job = S.make_job(424, 240, ctrl, 8, (7,), (), temporal_layer_index=1)
-    job.picture_number = 3108
-    job.ref_picture_number[0][0] = 3107
-    try:
-        with pytest.raises(RuntimeError, match="multiple of 64"):
-            gpu.submit(job)
-    finally:
-        for t in frames:
-            gpu.release(3100 + t)
+@pytest.mark.parametrize("case", [c for c in GOLD_ME_CASES if "_rt" in c["name"]], ids=lambda c: c["name"])
+def test_realtime_split_path_vs_reference_golden(svtme, gpu, case, monkeypatch):
+    """The real-time tune's HME-L0 reduction on the split HME path (k_stage_a ->
+    k_stage_d<true> -> k_stage_a<true> -> k_stage_d), forced for widths k_hme
+    would take, against the reference's outputs."""
+    monkeypatch.setenv("SVTME_NO_FUSED_HME", "1")
+    test_picture_vs_reference_golden(svtme, gpu, case)
