@@ -399,6 +399,13 @@ def main():
     valu_sad = {"achieved_T_absdiff_s": round(sad_rate, 2), "peak": SAD_PEAK_T, "frac": round(sad_rate / SAD_PEAK_T, 4),
                 "absdiff_per_sb_ref": W.ABSDIFF_PER_SB_REF[wl["windows"]],
                 "note": "SURVEY.md 8(d) nominal absdiff (distance-1 windows, no early exit) per launch / pass time"}
+    if "k_fp_wide" in stages and wl["windows"] in W.FULLPEL_ABSDIFF_PER_SB_REF:  # the wide full-pel stage alone
+        fp_absdiff = W.FULLPEL_ABSDIFF_PER_SB_REF[wl["windows"]] * R * sbs_launch
+        fp_rate = fp_absdiff / (stages["k_fp_wide"]["avg_ms"] * 1e-3) / 1e12
+        valu_sad["fullpel_stage"] = {"kernel": "k_fp_wide", "absdiff_per_launch": fp_absdiff,
+                                     "achieved_T_absdiff_s": round(fp_rate, 2),
+                                     "frac": round(fp_rate / SAD_PEAK_T, 4),
+                                     "note": "full-pel absdiff (positions x 2048) per launch / k_fp_wide time"}
     if ref_absdiff:
         per_sb = ref_absdiff / n_sb
         ref_rate = per_sb * sbs_launch / (device_ms * 1e-3) / 1e12

@@ -42,6 +42,8 @@ WORKLOADS["1080p_p8"] = WORKLOADS["1080p_sa64"]
 WINDOW_BYTES = {"p8": 16798, "p6": 38121, "p8_sa64": 28241}
 # absdiff operations per SB and reference (secondary, VALU-SAD roof)
 ABSDIFF_PER_SB_REF = {"p8": 196608, "p6": 845824, "p8_sa64": 8536064}
+# of which the full-pel search: positions x 64x32 sub-sampled pixels (the 64x64 override: 4096 x 2048)
+FULLPEL_ABSDIFF_PER_SB_REF = {"p8_sa64": 4096 * 2048}
 
 
 def bytes_per_sb(windows: str, refs: int) -> int:
