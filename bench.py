@@ -354,6 +354,10 @@ def main():
     lib.svtme_fp_wide_lds.restype = C.c_bool
     if lib.svtme_fp_wide_lds(C.byref(jobs[0].ctrl)):
         names[3] = "k_fp_wide"  # the wide full-pel stage with its window in LDS
+    lib.svtme_l1_full.argtypes = [C.POINTER(S.Controls)]
+    lib.svtme_l1_full.restype = C.c_bool
+    if not fused and lib.svtme_l1_full(C.byref(jobs[0].ctrl)):
+        names[2] = "k_l1_full"  # full-SAD HME-L1, two quadrants per wavefront
     for k, st in enumerate(names):
         if stage_ms[k] <= 0:
             continue

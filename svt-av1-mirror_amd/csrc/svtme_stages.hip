@@ -3054,6 +3054,176 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
     }
 }
 
+// ============================================================================
+// k_l1_full: HME level 1 with full-SAD rows (TF-ME levels 0-2, hme_level1_b64
+// :2041-2122 / hme_level_1 :923-1022): the 32x32 quarter-resolution block over
+// up to 16 x 16 positions per (slot, quadrant). One wavefront takes two
+// quadrants of one slot (lanes 32 h .. 32 h + 31: quadrant 2 qp + h); a lane
+// owns one aligned position quad of two position rows (y = 2 i, 2 i + 1), so
+// every reference row it loads (16-byte buffer loads, realigned once with
+// v_alignbyte) feeds 8 qsads of each of the two rows; the source row, the same
+// for the whole wave, sits in SGPRs (scalar loads). Accumulators are flushed
+// to 32 bits every 8 block rows (u16 lanes: 8 x 32 x 255 < 2^16).
+// Applies when HME-L2 is off and the L1 area is at most 16 x 16 (k_stage_b
+// otherwise).
+// ============================================================================
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_l1_full(const DevBatch B) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total)
+        return;
+    uint32_t gw;
+    const DevJob &dj        = batch_job(B, u, &gw);
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const uint32_t npairs   = dj.tb_count >> 1; // the list holds the 4 quadrants of each slot in order
+    const uint32_t sb_local = UNI(gw / npairs);
+    const int e0            = UNI(dj.tb_list[2 * (gw - sb_local * npairs)]);
+    const int s = e0 >> 2, half = lane >> 5, q = (e0 & 3) + half, l = s >> 2, r = s & 3;
+    const int qd = lane & 3, pr = (lane >> 2) & 7; // position quad, position row pair
+    const SbGeo G = sb_geo(dj, sb_local);
+    BState *b     = dj.bst + sb_local;
+    const DevPlane &P = dj.ref[l][r].lv[1];
+    const int16_t qx = i16(((int16_t)G.ox) >> 1), qy = i16(((int16_t)G.oy) >> 1);
+    const int bw = (int)(G.bw >> 1), bh = (int)(G.bh >> 1), nd = bw >> 2;
+
+    // the decisions of hme_level1_b64 (:2058-2083) for this lane's quadrant
+    const uint32_t zz   = b->zz[s];
+    const uint8_t dref  = b->do_ref[s];
+    const int16_t X0    = b->lx[s][q], Y0 = b->ly[s][q];
+    const uint64_t S0   = b->lsad[s][q];
+    int16_t X = 0, Y = 0;
+    uint64_t SD = 0;
+    bool search = false;
+    if (c.me_early_exit_th && zz < (c.me_early_exit_th >> 2)) {
+        X = Y = 0, SD = 0;
+    } else if (!dref) {
+        X = Y = 0, SD = U32MAX;
+    } else if (c.prev_me_stage_based_exit_th && S0 < (c.prev_me_stage_based_exit_th >> 5)) {
+        X = X0, Y = Y0, SD = S0;
+    } else
+        search = true;
+    int16_t xo = 0, yo = 0, sw = 0, shh = 0;
+    if (search)
+        hme_refine_rect(1, P, qx, qy, (int16_t)c.hme_l1_sa.width, (int16_t)c.hme_l1_sa.height, i16(X0 >> 1),
+                        i16(Y0 >> 1), &xo, &yo, &sw, &shh);
+    // window of this lane: plane position (qx + xo, qy + yo); raw dwords from the aligned base.
+    // The buffer starts at the plane's allocation (its top-left margin), so that every
+    // window offset is non-negative; lanes with no position of the area read inside it:
+    // columns from quad 0, rows clamped to the window's last row
+    const uint8_t *w0  = P.base + (ptrdiff_t)(qy + yo) * P.stride + (qx + xo);
+    const int sh       = (int)((uintptr_t)w0 & 3);
+    const int rowbytes = P.stride;
+    const uint8_t *pa  = uni_ptr(P.base - (ptrdiff_t)SVTME_DEV_Q_TOP * P.stride - SVTME_DEV_Q_LEFT);
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(pa); // the slot's quarter plane: uniform
+    const int32_t wofs = (int32_t)((w0 - sh) - pa);
+    const int qcol     = 4 * qd < sw ? qd : 0;
+    const int rlast    = (shh > 0 ? shh - 1 : 0) + bh;
+    const bool any     = __ballot(search && sw > 0 && shh > 0) != 0;
+    uint32_t acc32[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+    if (any) {
+        const DevPlane &Qc = dj.cur.lv[1];
+        const uint8_t *sp0 = uni_ptr(Qc.base + (ptrdiff_t)qy * Qc.stride + qx);
+        const int sst      = UNI(Qc.stride);
+        unsigned long long a0 = 0, a1 = 0; // position rows 2 pr, 2 pr + 1
+        // one reference row 2 pr + t of the window (raw dwords qd .. qd + 9, realigned to
+        // d[0 .. 8]): block row t of position row 2 pr (D0) and block row t - 1 of 2 pr + 1
+        // (D1). The row loop is peeled and chunked so that no qsad is predicated (uniform
+        // conditions inside the body became v_cndmask pairs); prefetching the next row one
+        // iteration ahead measured slower (66 VGPRs, 7 waves)
+        auto row = [&](int t, auto D0, auto D1, auto FW) {
+            constexpr bool do0 = decltype(D0)::value, do1 = decltype(D1)::value, fw = decltype(FW)::value;
+            const uint32_t off = (uint32_t)(wofs + min(2 * pr + t, rlast) * rowbytes + 4 * qcol);
+            const u32x4a4 ra = bld4(rs, off, 0), rb = bld4(rs, off + 16u, 0);
+            const uint32_t r8 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 32u), 0, 0);
+            const uint32_t r9 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 36u), 0, 0);
+            const uint32_t raw[10] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w, r8, r9};
+            uint32_t d[9];
+#pragma unroll
+            for (int j = 0; j < 9; j++) d[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], (uint32_t)sh);
+            // source rows t and t - 1: scalar loads (nothing carried between rows)
+            const uint8_t *s0 = sp0 + (ptrdiff_t)(do0 ? t : t - 1) * sst;
+            const uint4 c0 = sld4(s0), c1 = sld4(s0 + 16);
+            const uint4 p0 = do0 && do1 ? sld4(s0 - sst) : c0, p1 = do0 && do1 ? sld4(s0 - sst + 16) : c1;
+            const uint32_t sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            const uint32_t sp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (fw || k < nd) {
+                    if (do0)
+                        a0 = qsad(d[k], d[k + 1], sc[k], a0);
+                    if (do1)
+                        a1 = qsad(d[k], d[k + 1], do0 ? sp[k] : sc[k], a1);
+                }
+            }
+        };
+        auto flush = [&]() { // at most 8 block rows per u16 lane (8 x 32 x 255 < 2^16)
+            qsad_unpack(a0, acc32[0]);
+            qsad_unpack(a1, acc32[1]);
+            a0 = a1 = 0;
+        };
+        auto rows = [&](auto FW) {
+            row(0, std::true_type(), std::false_type(), FW);
+            for (int t0 = 1; t0 < bh;) { // chunks [1, 8), [8, 16), ...: position row 2 pr gets 8 rows per flush
+                const int t1 = min((t0 | 7) + 1, bh);
+                for (int t = t0; t < t1; t++)
+                    row(t, std::true_type(), std::true_type(), FW);
+                flush();
+                t0 = t1;
+            }
+            row(bh, std::false_type(), std::true_type(), FW);
+            flush();
+        };
+        if (nd == 8)
+            rows(std::true_type());
+        else
+            rows(std::false_type());
+    }
+    // keys (sad << 32 | y << 16 | x) of this lane's positions inside the area, then
+    // the minimum over the 32 lanes of the half (DPP in rows, then row 0 -> 1 / 2 -> 3)
+    unsigned long long best = ~0ull;
+    if (search) {
+#pragma unroll
+        for (int yy = 0; yy < 2; yy++)
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int x = 4 * qd + e, y = 2 * pr + yy;
+                if (x < sw && y < shh) {
+                    const unsigned long long k = ((unsigned long long)acc32[yy][e] << 32) | ((uint32_t)y << 16) | (uint32_t)x;
+                    best = k < best ? k : best;
+                }
+            }
+    }
+    {
+        auto step = [&](uint32_t tl, uint32_t th) {
+            const unsigned long long t = ((unsigned long long)th << 32) | tl;
+            best                       = t < best ? t : best;
+        };
+#define L1MIN(CTRL, RM) step(dpp_or<CTRL, RM>((uint32_t)best, U32MAX), dpp_or<CTRL, RM>((uint32_t)(best >> 32), U32MAX))
+        L1MIN(DPP_ROW_SHR(1), 0xF);
+        L1MIN(DPP_ROW_SHR(2), 0xF);
+        L1MIN(DPP_ROW_SHR(4), 0xF);
+        L1MIN(DPP_ROW_SHR(8), 0xF);
+        L1MIN(DPP_ROW_BCAST15, 0xA);
+#undef L1MIN
+    }
+    const unsigned long long kb = ((unsigned long long)rl32((uint32_t)(best >> 32), 31) << 32) | rl32((uint32_t)best, 31);
+    const unsigned long long kt = ((unsigned long long)rl32((uint32_t)(best >> 32), 63) << 32) | rl32((uint32_t)best, 63);
+    if (search) {
+        uint32_t bs;
+        int x, y;
+        key_result(half ? kt : kb, &bs, &x, &y);
+        SD = bs; // full-SAD rows: not doubled
+        X  = i16((x + xo) * 2);
+        Y  = i16((y + yo) * 2);
+    }
+    if ((lane & 31) == 0) {
+        b->hx[s][q]   = X;
+        b->hy[s][q]   = Y;
+        b->hsad[s][q] = SD;
+    }
+}
+
 // Per SB: decode the argmin keys kb[k][85] of the R records (slot state cin[k])
 // into best SAD / MV per PU (strict-< first minimum in search order), then
 // stage_c_tail; all threads of the workgroup. reset: leave kb at ~0 (banded
@@ -3879,6 +4049,14 @@ extern "C" bool svtme_hme_rt(const svtme_controls *c) {
            c->reduce_hme_l0_sr_th_max;
 }
 
+// k_l1_full applies: full-SAD HME rows, HME-L1 without L2, an L1 area of at most
+// 16 x 16 positions (TF-ME levels 0-2)
+extern "C" bool svtme_l1_full(const svtme_controls *c) {
+    return c->hme_search_method == SVTME_FULL_SAD_SEARCH && c->enable_hme_flag && c->enable_hme_level1_flag &&
+           !c->enable_hme_level2_flag && c->hme_l1_sa.width <= 16 && c->hme_l1_sa.height <= 16 &&
+           !getenv("SVTME_NO_L1_FULL");
+}
+
 extern "C" bool svtme_fp_k32(const svtme_controls *c) {
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
@@ -3923,7 +4101,8 @@ extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
     return (uint32_t)full | (uint32_t)(dj->parts != 0) << 1 | (uint32_t)svtme_fp_k32(&dj->job.ctrl) << 2 |
            (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4 |
            (uint32_t)(dj->parts == 1) << 5 | (uint32_t)svtme_fp_wide(&dj->job.ctrl) << 6 |
-           (uint32_t)svtme_hme_rt(&dj->job.ctrl) << 7 | (uint32_t)svtme_fp_wide_lds(&dj->job.ctrl) << 8;
+           (uint32_t)svtme_hme_rt(&dj->job.ctrl) << 7 | (uint32_t)svtme_fp_wide_lds(&dj->job.ctrl) << 8 |
+           (uint32_t)svtme_l1_full(&dj->job.ctrl) << 9;
 }
 
 static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
@@ -4000,7 +4179,11 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     }
     SVTME_LAUNCH(svtme::k_stage_d<false>, dim3((bd.total + 3) / 4), 1, bd);
     const DevBatch bb = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.tb_count; });
-    if (bb.total) {
+    if (bb.total && svtme_l1_full(&h0.job.ctrl)) { // two quadrants per wavefront
+        const DevBatch b2 =
+            make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * (j.tb_count / 2); });
+        SVTME_LAUNCH(svtme::k_l1_full, dim3((b2.total + 3) / 4), 2, b2);
+    } else if (bb.total) {
         if (h0.job.ctrl.enable_hme_level2_flag)
             SVTME_LAUNCH(svtme::k_stage_b<true>, dim3((bb.total + 3) / 4), 2, bb);
         else

@@ -9,6 +9,7 @@ exactly the one whose records are pinned against the reference.
   4k10_p6     configs[3]: 3840x2160 10-bit p6 (MSB plane), refs as the encoder (1+1)
   8k_p8       configs[4]: 7680x4320 p8, 4 refs (sharded over GPUs in bench --mode band)
   4k_p8_mixed configs[2] on mixed-motion content (per-region motion and noise)
+  4k_tf_p8    the temporal-filtering ME (ME_MCTF) of configs[2]'s encode (TF level 2 controls)
   ra360_p12   configs[0]: 640x360 p12, 30 pictures random access (ra_sequence)
 
 Inputs are the integer PCG32 panning texture of SURVEY.md 8(d): current picture
@@ -34,20 +35,34 @@ WORKLOADS = {
                         content="mixed",
                         desc="3840x2160 8-bit preset 8, 4 refs (L0 d=1,2; L1 d=1,2), open-loop ME, mixed-motion "
                              "content (256x256 regions: static / slow / pan / fast / beyond range / noise)"),
+    # temporal-filtering ME of configs[2]'s encode: the M8 tf_level 8 parameters (enc_handle.c:3125-3150:
+    # hme_me_level 2 -> FULL-SAD HME L0 + L1, 8x8 full-pel, qp_opt; me_exit_th 16 x 16), central picture 8
+    # against its nearest past picture (temporal_filtering.c:3127-3174)
+    "4k_tf_p8": dict(w=3840, h=2160, tf=dict(level=2, qp_opt=1, qp=35, exit_th=16 * 16), tl=1, l0=(7,), l1=(),
+                     windows="tf2", ten_bit=False,
+                     desc="3840x2160 8-bit TF-ME (ME_MCTF) of preset 8 (hme_me_level 2: full-SAD HME, 8x8 "
+                          "full-pel), central picture vs its nearest past picture"),
 }
 # the bench accepted "1080p_p8" in round 1
 WORKLOADS["1080p_p8"] = WORKLOADS["1080p_sa64"]
 
 # algorithmic bytes per SB = src 2688 + R x (nominal ref windows + 680 B out)
-WINDOW_BYTES = {"p8": 16798, "p6": 38121, "p8_sa64": 28241}
+WINDOW_BYTES = {"p8": 16798, "p6": 38121, "p8_sa64": 28241,
+                # TF level 2 (full rows): HME-L0 4 quadrants at 1/16 (48 x 32), HME-L1 4 x (16 + 32)^2 at 1/4,
+                # full-pel (8 + 64)^2
+                "tf2": 48 * 32 + 4 * 48 * 48 + 72 * 72}
+# source bytes per SB the searches read (sub-sampled rows: 64x32 + 32x16 + 16x8; full rows for tf2)
+SRC_BYTES = {"tf2": 64 * 64 + 32 * 32 + 16 * 16}
 # absdiff operations per SB and reference (secondary, VALU-SAD roof)
-ABSDIFF_PER_SB_REF = {"p8": 196608, "p6": 845824, "p8_sa64": 8536064}
+ABSDIFF_PER_SB_REF = {"p8": 196608, "p6": 845824, "p8_sa64": 8536064,
+                      # zz 64x32 + L0 4 x (16 x 8) x 16^2 + L1 4 x 16^2 x 32^2 + full-pel 64 x 64^2
+                      "tf2": 2048 + 512 * 256 + 1024 * 1024 + 64 * 4096}
 # of which the full-pel search: positions x 64x32 sub-sampled pixels (the 64x64 override: 4096 x 2048)
 FULLPEL_ABSDIFF_PER_SB_REF = {"p8_sa64": 4096 * 2048}
 
 
 def bytes_per_sb(windows: str, refs: int) -> int:
-    return 2688 + refs * (WINDOW_BYTES[windows] + 680)
+    return SRC_BYTES.get(windows, 2688) + refs * (WINDOW_BYTES[windows] + 680)
 
 
 def workload_frame(name: str, syn: "S.Synth", t: int):
@@ -68,6 +83,9 @@ def workload_frames(name: str) -> dict:
 
 def workload_controls(name: str) -> S.Controls:
     wl = WORKLOADS[name]
+    if wl.get("tf"):  # svt_aom_sig_deriv_me_tf + set_hme_search_params_mctf
+        tf = wl["tf"]
+        return S.derive_controls_tf(tf["level"], tf["qp_opt"], tf["qp"], S.input_resolution_of(wl["w"], wl["h"]))
     ctrl = S.derive_controls(wl["mode"], 35, S.input_resolution_of(wl["w"], wl["h"]), wl["tl"])
     if wl.get("sa64"):  # fixed 64x64 full-pel area
         ctrl.me_sa.sa_min.width = ctrl.me_sa.sa_min.height = 64
@@ -81,10 +99,12 @@ def workload_job(name: str, base: int = 0, sb_begin: int = 0, sb_count: int = 0)
     """The picture job; picture numbers are base + t (t = 8 current, refs as listed)."""
     wl = WORKLOADS[name]
     res = S.input_resolution_of(wl["w"], wl["h"])
+    tf = wl.get("tf")
+    kw = dict(me_type=S.ME_MCTF, tf_me_exit_th=tf["exit_th"]) if tf else {}
     return S.make_job(wl["w"], wl["h"], workload_controls(name), base + 8, [base + t for t in wl["l0"]],
                       [base + t for t in wl["l1"]], temporal_layer_index=wl["tl"],
                       enable_me_8x8=(res <= S.RES_720P), ref_count_used=(3, 2), sb_begin=sb_begin,
-                      sb_count=sb_count)
+                      sb_count=sb_count, **kw)
 
 
 # ----------------------------------------------------------------------------

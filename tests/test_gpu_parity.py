@@ -121,6 +121,13 @@ MCTF_CASES = [  # content, w, h, tf hme_me_level, qp_opt, cur, ref, tl, tf_me_ex
     ("noise", 192, 128, 3, 0, 8, 6, 2, 0),
     ("flat", 192, 128, 4, 0, 8, 7, 1, 1),
     ("stripes", 320, 192, 2, 0, 8, 9, 1, 50000),
+    # levels 1-2 take k_l1_full: ragged widths and heights (partial 32x32 blocks), fast motion
+    # (windows clamped at the picture edges), noise and saturated content (no HME exits)
+    ("noise", 200, 136, 2, 1, 8, 7, 1, 0),
+    ("vpan", 424, 240, 2, 0, 8, 7, 1, 0),
+    ("hpan", 264, 200, 1, 0, 8, 9, 1, 0),
+    ("sat", 192, 128, 2, 1, 8, 6, 2, 0),
+    ("pan", 72, 40, 1, 0, 8, 7, 1, 0),
 ]
 
 
