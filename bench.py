@@ -358,6 +358,10 @@ def main():
     lib.svtme_l1_full.restype = C.c_bool
     if not fused and lib.svtme_l1_full(C.byref(jobs[0].ctrl)):
         names[2] = "k_l1_full"  # full-SAD HME-L1, two quadrants per wavefront
+    lib.svtme_l0_full_job.argtypes = [C.POINTER(S.Job)]
+    lib.svtme_l0_full_job.restype = C.c_bool
+    if not fused and lib.svtme_l0_full_job(C.byref(jobs[0])):
+        names[0] = "k_l0_full"  # full-SAD zz + HME-L0, one wavefront per (SB, slot)
     for k, st in enumerate(names):
         if stage_ms[k] <= 0:
             continue

@@ -3055,6 +3055,162 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
 }
 
 // ============================================================================
+// k_l0_full: stage A of full-SAD HME jobs without pre-HME (TF-ME levels 0-2:
+// the zz SAD and hme_level_0, motion_estimation.c:835-889, 2382-2437) with
+// HME-L0 quadrants of at most 16 x 16 positions. One wavefront per (SB, slot):
+// lanes 16 qq .. 16 qq + 15 take quadrant qq, a lane one aligned position
+// quad of PR position rows (each loaded reference row feeds all of them), the
+// 16 x 16 sixteenth-resolution source row in SGPRs. u16 accumulators hold the
+// whole block (16 x 16 x 255 < 2^16). Partial SBs need a width of a multiple
+// of 16 (whole source dwords); k_stage_a otherwise.
+// ============================================================================
+template <int PR> // position rows per lane: 2 (quadrants up to 8 rows) or 4 (up to 16)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_l0_full(const DevBatch B) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
+    if (u >= B.total)
+        return;
+    uint32_t gw;
+    const DevJob &dj        = batch_job(B, u, &gw);
+    const svtme_job &job    = dj.job;
+    const svtme_controls &c = job.ctrl;
+    const uint32_t sb_local = UNI(gw / dj.ta_count);
+    const int entry         = UNI(dj.ta_list[gw - sb_local * dj.ta_count]); // TA_HME << 3 | slot
+    const int s = entry & 7, l = s >> 2, r = s & 3;
+    const SbGeo G   = sb_geo(dj, sb_local);
+    ARes *out       = dj.ares + (size_t)sb_local * SVTME_A_N;
+    const DevPlane &P = dj.ref[l][r].lv[2];
+    const int16_t sox = i16(((int16_t)G.ox) >> 2), soy = i16(((int16_t)G.oy) >> 2);
+    const int bws = (int)(G.bw >> 2), bhs = (int)(G.bh >> 2), nd = bws >> 2;
+
+    // zz SAD (init_zz_sad, motion_estimation.c:2382-2437): sub-sampled 64 x 32 at full resolution
+    const bool zz = c.me_early_exit_th || c.me_safe_limit_zz_th;
+    if (zz) {
+        const DevPlane &F = dj.ref[l][r].lv[0];
+        const DevPlane &Cf = dj.cur.lv[0];
+        const uint8_t *zr = F.base + (ptrdiff_t)G.oy * F.stride + G.ox;
+        const uint8_t *zc = Cf.base + (ptrdiff_t)G.oy * Cf.stride + G.ox;
+        uint32_t v;
+        if (G.bw == 64 && G.bh == 64) {
+            ZzLoads zl;
+            zz_issue(zl, zr, 2 * F.stride, zc, 2 * Cf.stride);
+            v = zz_finish(zl);
+        } else
+            v = wave_nxm(zr, 2 * F.stride, zc, 2 * Cf.stride, (int)(G.bh >> 1), (int)G.bw);
+        if (lane == 0)
+            out[SVTME_A_ZZ + s] = ARes{v, 0, 0};
+    }
+    if (!(c.enable_hme_flag && c.enable_hme_level0_flag))
+        return;
+    // this lane's quadrant (hme_level_0 :835-889)
+    const int qq = lane >> 4, qd = lane & 3, rp = (lane >> 2) & 3; // position rows PR rp .. PR rp + PR - 1
+    int16_t sa_w, sa_h;
+    hme_l0_area(c, l, r, ref_dist_const(job, l, r), 0, 0, &sa_w, &sa_h);
+    int16_t xo, yo, sw, shh;
+    hme_l0_rect(c, P, sox, soy, sa_w, sa_h, qq >> 1, qq & 1, &xo, &yo, &sw, &shh);
+    const uint8_t *w0  = P.base + (ptrdiff_t)(soy + yo) * P.stride + (sox + xo);
+    const int sh       = (int)((uintptr_t)w0 & 3);
+    const int rowbytes = P.stride;
+    const uint8_t *pa  = uni_ptr(P.base - (ptrdiff_t)SVTME_DEV_S_TOP * P.stride - SVTME_DEV_S_LEFT);
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(pa); // the slot's sixteenth plane (allocation start)
+    const int32_t wofs = (int32_t)((w0 - sh) - pa);
+    const int qcol     = 4 * qd < sw ? qd : 0;       // lanes without a position read inside the window
+    const int rlast    = (shh > 0 ? shh - 1 : 0) + bhs;
+    const DevPlane &Sc = dj.cur.lv[2];
+    const uint8_t *sp0 = uni_ptr(Sc.base + (ptrdiff_t)soy * Sc.stride + sox);
+    const int sst      = UNI(Sc.stride);
+    unsigned long long a[PR] = {}; // position rows PR rp + j
+    // reference row PR rp + t feeds block row t - j of position row PR rp + j for every j
+    // with 0 <= t - j < bhs (ACT: bit j); the head and tail rows are unrolled so that
+    // every condition is a constant (no predicated qsads)
+    auto row = [&](int t, auto ACT, auto FW) {
+        constexpr uint32_t act = decltype(ACT)::value;
+        constexpr bool fw      = decltype(FW)::value;
+        const uint32_t off = (uint32_t)(wofs + min(PR * rp + t, rlast) * rowbytes + 4 * qcol);
+        const u32x4a4 ra   = bld4(rs, off, 0);
+        const uint32_t r4  = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 16u), 0, 0);
+        const uint32_t r5  = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 20u), 0, 0);
+        const uint32_t raw[6] = {ra.x, ra.y, ra.z, ra.w, r4, r5};
+        uint32_t d[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) d[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], (uint32_t)sh);
+#pragma unroll
+        for (int j = 0; j < PR; j++) {
+            if (!((act >> j) & 1u))
+                continue;
+            const uint4 sv        = sld4(sp0 + (ptrdiff_t)(t - j) * sst);
+            const uint32_t c4[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (fw || k < nd)
+                    a[j] = qsad(d[k], d[k + 1], c4[k], a[j]);
+        }
+    };
+    auto rows = [&](auto FW) {
+        using A1 = std::integral_constant<uint32_t, 1u>;
+        using A3 = std::integral_constant<uint32_t, 3u>;
+        using A7 = std::integral_constant<uint32_t, 7u>;
+        using AE = std::integral_constant<uint32_t, 14u>;
+        using AC = std::integral_constant<uint32_t, 12u>;
+        using A8 = std::integral_constant<uint32_t, 8u>;
+        using A2 = std::integral_constant<uint32_t, 2u>;
+        using AF = std::integral_constant<uint32_t, (1u << PR) - 1u>;
+        // head: t < PR - 1 (position rows j <= t)
+        row(0, A1(), FW);
+        if constexpr (PR == 4) {
+            row(1, A3(), FW);
+            row(2, A7(), FW);
+        }
+        for (int t = PR - 1; t < bhs; t++) // every position row
+            row(t, AF(), FW);
+        // tail: t = bhs + i (position rows j > i)
+        if constexpr (PR == 4) {
+            row(bhs, AE(), FW);
+            row(bhs + 1, AC(), FW);
+            row(bhs + 2, A8(), FW);
+        } else
+            row(bhs, A2(), FW);
+    };
+    if (nd == 4)
+        rows(std::true_type());
+    else
+        rows(std::false_type());
+    // keys (sad << 32 | y << 16 | x) of the lane's positions inside the quadrant's area,
+    // then the minimum over the quadrant's 16 lanes (one DPP row)
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (int j = 0; j < PR; j++) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int x = 4 * qd + e, y = PR * rp + j;
+            if (x < sw && y < shh) {
+                const uint32_t sad = (uint32_t)(a[j] >> (16 * e)) & 0xFFFFu;
+                const unsigned long long k = ((unsigned long long)sad << 32) | ((uint32_t)y << 16) | (uint32_t)x;
+                best = k < best ? k : best;
+            }
+        }
+    }
+    {
+        auto step = [&](uint32_t tl, uint32_t th) {
+            const unsigned long long t = ((unsigned long long)th << 32) | tl;
+            best                       = t < best ? t : best;
+        };
+#define L0MIN(CTRL) step(dpp_or<CTRL>((uint32_t)best, U32MAX), dpp_or<CTRL>((uint32_t)(best >> 32), U32MAX))
+        L0MIN(DPP_ROW_SHR(1));
+        L0MIN(DPP_ROW_SHR(2));
+        L0MIN(DPP_ROW_SHR(4));
+        L0MIN(DPP_ROW_SHR(8));
+#undef L0MIN
+    }
+    if ((lane & 15) == 15) {
+        uint32_t bs;
+        int x, y;
+        key_result(best, &bs, &x, &y);
+        out[SVTME_A_L0 + s * 4 + qq] = ARes{bs, i16((x + xo) * 4), i16((y + yo) * 4)}; // full rows: not doubled
+    }
+}
+
+// ============================================================================
 // k_l1_full: HME level 1 with full-SAD rows (TF-ME levels 0-2, hme_level1_b64
 // :2041-2122 / hme_level_1 :923-1022): the 32x32 quarter-resolution block over
 // up to 16 x 16 positions per (slot, quadrant). One wavefront takes two
@@ -4057,6 +4213,36 @@ extern "C" bool svtme_l1_full(const svtme_controls *c) {
            !getenv("SVTME_NO_L1_FULL");
 }
 
+// k_l0_full applies: full-SAD HME rows, HME-L0 on, no pre-HME, HME-L0 quadrants of
+// at most 16 x 8 positions for every slot, whole source dwords on partial SBs
+extern "C" bool svtme_l0_full(const DevJob *dj) {
+    const svtme_controls &c = dj->job.ctrl;
+    if (c.hme_search_method != SVTME_FULL_SAD_SEARCH || c.prehme_enable || !c.enable_hme_flag ||
+        !c.enable_hme_level0_flag || svtme_hme_rt(&c) || (dj->job.width % 64) % 16 != 0 ||
+        getenv("SVTME_NO_L0_FULL"))
+        return false;
+    for (int s = 0; s < 8; s++)
+        if (dj->l0_sa[s][0] > 16 || dj->l0_sa[s][1] > 16)
+            return false;
+    return true;
+}
+
+// the same test on a job (bench / diagnostics: which kernel runs stage A)
+extern "C" bool svtme_l0_full_job(const svtme_job *job) {
+    DevJob dj{};
+    dj.job = *job;
+    svtme_hme_prepare(&dj);
+    return svtme_l0_full(&dj);
+}
+
+// position rows per lane of k_l0_full: 2 when every quadrant has at most 8 rows
+static bool l0_full_short(const DevJob *dj) {
+    for (int s = 0; s < 8; s++)
+        if (dj->l0_sa[s][1] > 8)
+            return false;
+    return true;
+}
+
 extern "C" bool svtme_fp_k32(const svtme_controls *c) {
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
@@ -4102,7 +4288,7 @@ extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
            (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4 |
            (uint32_t)(dj->parts == 1) << 5 | (uint32_t)svtme_fp_wide(&dj->job.ctrl) << 6 |
            (uint32_t)svtme_hme_rt(&dj->job.ctrl) << 7 | (uint32_t)svtme_fp_wide_lds(&dj->job.ctrl) << 8 |
-           (uint32_t)svtme_l1_full(&dj->job.ctrl) << 9;
+           (uint32_t)svtme_l1_full(&dj->job.ctrl) << 9 | (uint32_t)svtme_l0_full(dj) << 10;
 }
 
 static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
@@ -4168,7 +4354,14 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
         SVTME_HME(false, true, true);
     } else {
     const DevBatch ba = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta_count; });
-    if (ba.total)
+    bool short_l0 = true;
+    for (uint32_t k = 0; k < n; k++)
+        short_l0 = short_l0 && l0_full_short(&h_jobs[k]);
+    if (ba.total && svtme_l0_full(&h0) && short_l0)
+        SVTME_LAUNCH(svtme::k_l0_full<2>, dim3((ba.total + 3) / 4), 0, ba);
+    else if (ba.total && svtme_l0_full(&h0))
+        SVTME_LAUNCH(svtme::k_l0_full<4>, dim3((ba.total + 3) / 4), 0, ba);
+    else if (ba.total)
         SVTME_LAUNCH(svtme::k_stage_a<false>, dim3((ba.total + 3) / 4), 0, ba);
     if (rt) { // the real-time tune: slot 0's HME-L0 centre, then the other slots' HME-L0
         const DevBatch ba1 =
