@@ -2437,6 +2437,50 @@ __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint8_t *g, int 
 
 
 
+#ifndef SVTME_FP8X8 // 0: the 8 x 8 area through fp_rows32 (A/B builds)
+#define SVTME_FP8X8 1
+#endif
+// K32 full rows, an 8 x 8 area searched whole (TF-ME level 2: me_sa 8 x 8): the
+// 15 reference rows of the lane's block are loaded once each and every one
+// feeds all (search row, block row) pairs it belongs to, instead of 8 rows per
+// search row (8x fewer loads and realignments); then the 8 sets of keys.
+__device__ __forceinline__ void fp_rows32_8x8(PuMin<true> &M, const uint8_t *g, int sdw, uint32_t obase,
+                                              const uint32_t (&src)[8][2], int by, int bx) {
+    g     = uni_ptr(g);
+    sdw   = UNI(sdw);
+    obase = (uint32_t)UNI(obase);
+    const uint32_t qb = PuMin<true>::quad_b_rows();
+    const int sh      = (int)((uintptr_t)g & 3);
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(g - sh);
+    const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2) * 4u;
+    unsigned long long acc[8][2];
+#pragma unroll
+    for (int ty = 0; ty < 8; ty++) acc[ty][0] = acc[ty][1] = 0;
+#pragma unroll
+    for (int R = 0; R < 15; R++) { // reference row R = search row ty + block row R - ty
+        const u32x4a4 t4  = bld4(rs, lo, (uint32_t)(R * sdw) * 4u);
+        const uint32_t t5 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lo + 16u), (int)(R * sdw * 4), 0);
+        const uint32_t d0 = __builtin_amdgcn_alignbyte(t4.y, t4.x, (uint32_t)sh);
+        const uint32_t d1 = __builtin_amdgcn_alignbyte(t4.z, t4.y, (uint32_t)sh);
+        const uint32_t d2 = __builtin_amdgcn_alignbyte(t4.w, t4.z, (uint32_t)sh);
+        const uint32_t d3 = __builtin_amdgcn_alignbyte(t5, t4.w, (uint32_t)sh);
+#pragma unroll
+        for (int ty = 0; ty < 8; ty++) {
+            const int r = R - ty;
+            if (r < 0 || r > 7)
+                continue;
+            acc[ty][0] = qsad64(pair(d0, d1), src[r][0], acc[ty][0]);
+            acc[ty][0] = qsad64(pair(d1, d2), src[r][1], acc[ty][0]);
+            acc[ty][1] = qsad64(pair(d1, d2), src[r][0], acc[ty][1]);
+            acc[ty][1] = qsad64(pair(d2, d3), src[r][1], acc[ty][1]);
+        }
+    }
+#pragma unroll
+    for (int ty = 0; ty < 8; ty++)
+        M.template add_quads<true>((uint32_t)acc[ty][0], (uint32_t)(acc[ty][0] >> 32), (uint32_t)acc[ty][1],
+                                   (uint32_t)(acc[ty][1] >> 32), obase + (uint32_t)(ty * 8), 0, 8, qb);
+}
+
 // The 8x8-variance probe of fp_slot (K32): this lane's raw 8x8 SAD at window
 // position 0 (dword-aligned buffer loads realigned by v_alignbyte) into M;
 // returns it as the reference counts it (SUB: doubled)
@@ -2602,7 +2646,12 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     const int nq     = (sh + w + 3) >> 2;
     const int y0 = (int)(((uint32_t)h * part) / parts), y1 = (int)(((uint32_t)h * (part + 1)) / parts);
     const uint32_t obase = probe ? 1u : 0u; // the centre probe wins ties: order 0
-    if constexpr (K32)
+    if constexpr (K32 && !SUB) {
+        if (w == 8 && h == 8 && parts == 1 && SVTME_FP8X8) // the whole 8 x 8 area in one pass
+            fp_rows32_8x8(M, g, P.stride >> 2, obase, src, by, bx);
+        else
+            fp_rows32<SUB, WIDE ? 6 : 2>(M, g, P.stride >> 2, w, y0, y1, obase, src, by, bx);
+    } else if constexpr (K32)
         fp_rows32<SUB, WIDE ? 6 : 2>(M, g, P.stride >> 2, w, y0, y1, obase, src, by, bx);
     else
         fp_rows<SUB, K32, TQ>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
