@@ -24,7 +24,7 @@ def main(out):
         by_dispatch = defaultdict(dict)
         names = {}
         for r in rows:
-            if not any(t in r["Kernel_Name"] for t in ("k_stage", "k_hme", "k_fp")):
+            if not any(t in r["Kernel_Name"] for t in ("k_stage", "k_hme", "k_fp", "k_l0", "k_l1")):
                 continue
             by_dispatch[r["Dispatch_Id"]][r["Counter_Name"]] = float(r["Counter_Value"])
             names[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0]

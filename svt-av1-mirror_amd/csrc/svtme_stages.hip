@@ -2437,48 +2437,74 @@ __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint8_t *g, int 
 
 
 
-#ifndef SVTME_FP8X8 // 0: the 8 x 8 area through fp_rows32 (A/B builds)
-#define SVTME_FP8X8 1
+#ifndef SVTME_FP_WHOLE // 0: every area through fp_rows32 (A/B builds)
+#define SVTME_FP_WHOLE 1
 #endif
-// K32 full rows, an 8 x 8 area searched whole (TF-ME level 2: me_sa 8 x 8): the
-// 15 reference rows of the lane's block are loaded once each and every one
-// feeds all (search row, block row) pairs it belongs to, instead of 8 rows per
-// search row (8x fewer loads and realignments); then the 8 sets of keys.
-__device__ __forceinline__ void fp_rows32_8x8(PuMin<true> &M, const uint8_t *g, int sdw, uint32_t obase,
-                                              const uint32_t (&src)[8][2], int by, int bx) {
-    g     = uni_ptr(g);
-    sdw   = UNI(sdw);
-    obase = (uint32_t)UNI(obase);
-    const uint32_t qb = PuMin<true>::quad_b_rows();
-    const int sh      = (int)((uintptr_t)g & 3);
-    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(g - sh);
-    const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2) * 4u;
-    unsigned long long acc[8][2];
+#ifndef SVTME_HME_WHOLE // the whole-area shapes k_hme takes (fp_slot WHOLE bits)
+#define SVTME_HME_WHOLE 2
+#endif
+// K32, an area 8 wide searched whole (TF-ME level 2: 8 x 8 full rows; the p8
+// searches: 8 x 3 / 8 x 4 sub-sampled rows): every reference row of the lane's
+// block is loaded and realigned once and feeds each (search row, block row) pair
+// it belongs to, instead of once per pair (8 x 8 full rows: 15 row loads instead
+// of 64; 8 x 4 sub-sampled: 10 instead of 16). Only search rows of one parity
+// share sub-sampled reference rows: fp_whole_class runs the NT search rows
+// ty = c + NC j of parity class c (NC = 2 sub-sampled, 1 full rows).
+template <bool SUB, int NT>
+__device__ __forceinline__ void fp_whole_class(PuMin<true> &M, const __amdgpu_buffer_rsrc_t rs, uint32_t lo, int sdw,
+                                               int sh, uint32_t qb, uint32_t obase, int c,
+                                               const uint32_t (&src)[SUB ? 4 : 8][2]) {
+    constexpr int ROWS = SUB ? 4 : 8, NC = SUB ? 2 : 1;
+    unsigned long long acc[NT][2];
 #pragma unroll
-    for (int ty = 0; ty < 8; ty++) acc[ty][0] = acc[ty][1] = 0;
+    for (int j = 0; j < NT; j++) acc[j][0] = acc[j][1] = 0;
 #pragma unroll
-    for (int R = 0; R < 15; R++) { // reference row R = search row ty + block row R - ty
-        const u32x4a4 t4  = bld4(rs, lo, (uint32_t)(R * sdw) * 4u);
-        const uint32_t t5 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lo + 16u), (int)(R * sdw * 4), 0);
+    for (int k = 0; k < NT + ROWS - 1; k++) { // reference row c + NC k: block row k - j of search row j
+        const uint32_t ro = (uint32_t)((c + NC * k) * sdw) * 4u;
+        const u32x4a4 t4  = bld4(rs, lo, ro);
+        const uint32_t t5 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lo + 16u), (int)ro, 0);
         const uint32_t d0 = __builtin_amdgcn_alignbyte(t4.y, t4.x, (uint32_t)sh);
         const uint32_t d1 = __builtin_amdgcn_alignbyte(t4.z, t4.y, (uint32_t)sh);
         const uint32_t d2 = __builtin_amdgcn_alignbyte(t4.w, t4.z, (uint32_t)sh);
         const uint32_t d3 = __builtin_amdgcn_alignbyte(t5, t4.w, (uint32_t)sh);
 #pragma unroll
-        for (int ty = 0; ty < 8; ty++) {
-            const int r = R - ty;
-            if (r < 0 || r > 7)
+        for (int j = 0; j < NT; j++) {
+            const int r = k - j;
+            if (r < 0 || r >= ROWS)
                 continue;
-            acc[ty][0] = qsad64(pair(d0, d1), src[r][0], acc[ty][0]);
-            acc[ty][0] = qsad64(pair(d1, d2), src[r][1], acc[ty][0]);
-            acc[ty][1] = qsad64(pair(d1, d2), src[r][0], acc[ty][1]);
-            acc[ty][1] = qsad64(pair(d2, d3), src[r][1], acc[ty][1]);
+            acc[j][0] = qsad64(pair(d0, d1), src[r][0], acc[j][0]);
+            acc[j][0] = qsad64(pair(d1, d2), src[r][1], acc[j][0]);
+            acc[j][1] = qsad64(pair(d1, d2), src[r][0], acc[j][1]);
+            acc[j][1] = qsad64(pair(d2, d3), src[r][1], acc[j][1]);
         }
     }
 #pragma unroll
-    for (int ty = 0; ty < 8; ty++)
-        M.template add_quads<true>((uint32_t)acc[ty][0], (uint32_t)(acc[ty][0] >> 32), (uint32_t)acc[ty][1],
-                                   (uint32_t)(acc[ty][1] >> 32), obase + (uint32_t)(ty * 8), 0, 8, qb);
+    for (int j = 0; j < NT; j++)
+        M.template add_quads<true>((uint32_t)acc[j][0], (uint32_t)(acc[j][0] >> 32), (uint32_t)acc[j][1],
+                                   (uint32_t)(acc[j][1] >> 32), obase + (uint32_t)((c + NC * j) * 8), 0, 8, qb);
+}
+
+// the whole 8-wide area: full rows h = 8 (one class), sub-sampled h = 3 or 4
+// (class 0: search rows 0, 2; class 1: row 1, or rows 1, 3)
+template <bool SUB>
+__device__ __forceinline__ void fp_rows32_whole(PuMin<true> &M, const uint8_t *g, int sdw, int h, uint32_t obase,
+                                                const uint32_t (&src)[SUB ? 4 : 8][2], int by, int bx) {
+    g     = uni_ptr(g);
+    sdw   = UNI(sdw);
+    h     = UNI(h);
+    obase = (uint32_t)UNI(obase);
+    const uint32_t qb = PuMin<true>::quad_b_rows();
+    const int sh      = (int)((uintptr_t)g & 3);
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(g - sh);
+    const uint32_t lo = (uint32_t)((by * 8) * sdw + bx * 2) * 4u;
+    if constexpr (SUB) {
+        fp_whole_class<true, 2>(M, rs, lo, sdw, sh, qb, obase, 0, src);
+        if (h == 4)
+            fp_whole_class<true, 2>(M, rs, lo, sdw, sh, qb, obase, 1, src);
+        else
+            fp_whole_class<true, 1>(M, rs, lo, sdw, sh, qb, obase, 1, src);
+    } else
+        fp_whole_class<false, 8>(M, rs, lo, sdw, sh, qb, obase, 0, src);
 }
 
 // The 8x8-variance probe of fp_slot (K32): this lane's raw 8x8 SAD at window
@@ -2605,7 +2631,7 @@ __device__ __forceinline__ FpArea fp_area(const DevJob &dj, const SbGeo &G, int 
 // [h * part / parts, h * (part + 1) / parts); the 85-PU argmin keys go to kp
 // (atomic min when parts > 1), the slot state to cs (part 0). src: this lane's
 // 8x8 source block rows (lane = block by, bx).
-template <bool SUB, bool K32, int TQ = (SUB ? FP_TQ : 2), bool WIDE = false>
+template <bool SUB, bool K32, int TQ = (SUB ? FP_TQ : 2), bool WIDE = false, int WHOLE = 7>
 __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s, const uint32_t (&src)[SUB ? 4 : 8][2],
                                         int by, int bx, uint64_t hme_sad, uint32_t zz, uint32_t rdiv, int16_t sc_x,
                                         int16_t sc_y, uint8_t dref, uint8_t tf_exit, int part, uint32_t parts,
@@ -2646,13 +2672,14 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     const int nq     = (sh + w + 3) >> 2;
     const int y0 = (int)(((uint32_t)h * part) / parts), y1 = (int)(((uint32_t)h * (part + 1)) / parts);
     const uint32_t obase = probe ? 1u : 0u; // the centre probe wins ties: order 0
-    if constexpr (K32 && !SUB) {
-        if (w == 8 && h == 8 && parts == 1 && SVTME_FP8X8) // the whole 8 x 8 area in one pass
-            fp_rows32_8x8(M, g, P.stride >> 2, obase, src, by, bx);
+    if constexpr (K32) {
+        // an area 8 wide searched whole (wave-uniform)
+        const bool whole = SVTME_FP_WHOLE && !WIDE && w == 8 && parts == 1; // WIDE: areas >= 24 wide
+        if ((SUB ? (WHOLE & 2) && (h == 3 || h == 4) : (WHOLE & 1) && h == 8) && whole)
+            fp_rows32_whole<SUB>(M, g, P.stride >> 2, h, obase, src, by, bx);
         else
             fp_rows32<SUB, WIDE ? 6 : 2>(M, g, P.stride >> 2, w, y0, y1, obase, src, by, bx);
-    } else if constexpr (K32)
-        fp_rows32<SUB, WIDE ? 6 : 2>(M, g, P.stride >> 2, w, y0, y1, obase, src, by, bx);
+    }
     else
         fp_rows<SUB, K32, TQ>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
     M.finalize();
@@ -4110,7 +4137,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         }
         const int s         = k < gj.job.num_refs[0] ? k : 4 + (k - gj.job.num_refs[0]);
         const SlotCentre &v = sh.cen[s];
-        fp_slot<SUB_ME, K32, 2>(gj, G, s, src, by, bx, rl64(v.hme_sad, 0), (uint32_t)UNI(v.zz), (uint32_t)UNI(v.reduce_div),
+        fp_slot<SUB_ME, K32, 2, false, SVTME_HME_WHOLE>(gj, G, s, src, by, bx, rl64(v.hme_sad, 0), (uint32_t)UNI(v.zz), (uint32_t)UNI(v.reduce_div),
                                 (int16_t)UNI(v.sc_x), (int16_t)UNI(v.sc_y), (uint8_t)UNI(v.do_ref),
                                 (uint8_t)UNI(sh.tf_exit), 0, 1u, &sh.u.st.keys[k][0], &sh.cin[k]);
     }
