@@ -3286,6 +3286,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
 }
 
+#ifndef SVTME_L1_LDS // 0: k_l1_full's rows from global memory, realigned per row (A/B builds)
+#define SVTME_L1_LDS 1
+#endif
+#define L1W_PITCH 12                  // dwords per staged window row (16 positions + 31 columns + 1)
+#define L1W_HALF (48 * L1W_PITCH + 4) // 48 rows; + 4 dwords: the two halves' rows on different banks
 // ============================================================================
 // k_l1_full: HME level 1 with full-SAD rows (TF-ME levels 0-2, hme_level1_b64
 // :2041-2122 / hme_level_1 :923-1022): the 32x32 quarter-resolution block over
@@ -3351,8 +3356,63 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     const int32_t wofs = (int32_t)((w0 - sh) - pa);
     const int qcol     = 4 * qd < sw ? qd : 0;
     const int rlast    = (shh > 0 ? shh - 1 : 0) + bh;
-    const bool any     = __ballot(search && sw > 0 && shh > 0) != 0;
+    const bool active  = search && sw > 0 && shh > 0;
+    const bool any     = __ballot(active) != 0;
     uint32_t acc32[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+#if SVTME_L1_LDS
+    // this half's window in LDS, realigned to position 0: rows 0 .. rlast (<= 47) x
+    // 12 dwords (positions 0 .. 15 + 31 block columns + 1); every qsad pair is then
+    // one 4-byte-aligned 8-byte LDS read (ds_read2_b32), with no v_alignbyte and no
+    // register copies for the odd pairs in the row loop
+    __shared__ __attribute__((aligned(16))) uint32_t l1w[4][2][L1W_HALF];
+    uint32_t *win = l1w[wid][half];
+    if (any) {
+        if (active) { // 30 lanes of the half: 10 rows x 3 dword groups per pass
+            const int l32 = lane & 31, rr = l32 / 3, cg = l32 - 3 * rr;
+            for (int r0 = 0; r0 <= rlast; r0 += 10) {
+                const int row = r0 + rr;
+                if (rr < 10 && row <= rlast) {
+                    const uint32_t off = (uint32_t)(wofs + row * rowbytes + 16 * cg);
+                    const u32x4a4 t4   = bld4(rs, off, 0);
+                    const uint32_t t5  = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 16u), 0, 0);
+                    *(uint4 *)&win[row * L1W_PITCH + 4 * cg] =
+                        make_uint4(__builtin_amdgcn_alignbyte(t4.y, t4.x, (uint32_t)sh),
+                                   __builtin_amdgcn_alignbyte(t4.z, t4.y, (uint32_t)sh),
+                                   __builtin_amdgcn_alignbyte(t4.w, t4.z, (uint32_t)sh),
+                                   __builtin_amdgcn_alignbyte(t5, t4.w, (uint32_t)sh));
+                }
+            }
+        }
+        wave_lds_fence();
+        const DevPlane &Qc = dj.cur.lv[1];
+        const uint8_t *sp0 = uni_ptr(Qc.base + (ptrdiff_t)qy * Qc.stride + qx);
+        const int sst      = UNI(Qc.stride);
+        unsigned long long a0 = 0, a1 = 0; // position rows 2 pr, 2 pr + 1
+        // reference row 2 pr + t of the window: block row t of position row 2 pr (D0)
+        // and block row t - 1 of 2 pr + 1 (D1); lanes without a position read row
+        // rlast / column quad 0 (their keys are dropped)
+        auto row = [&](int t, auto D0, auto D1, auto FW) {
+            constexpr bool do0 = decltype(D0)::value, do1 = decltype(D1)::value, fw = decltype(FW)::value;
+            const uint32_t *wr = win + min(2 * pr + t, rlast) * L1W_PITCH + qcol;
+            // source rows t and t - 1: scalar loads (nothing carried between rows)
+            const uint8_t *s0 = sp0 + (ptrdiff_t)(do0 ? t : t - 1) * sst;
+            const uint4 c0 = sld4(s0), c1 = sld4(s0 + 16);
+            const uint4 p0 = do0 && do1 ? sld4(s0 - sst) : c0, p1 = do0 && do1 ? sld4(s0 - sst + 16) : c1;
+            const uint32_t sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+            const uint32_t sp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                if (fw || k < nd) {
+                    const u32x2a4 v              = *(const u32x2a4 *)(wr + k);
+                    const unsigned long long pk = pair(v.x, v.y);
+                    if (do0)
+                        a0 = qsad64(pk, sc[k], a0);
+                    if (do1)
+                        a1 = qsad64(pk, do0 ? sp[k] : sc[k], a1);
+                }
+            }
+        };
+#else
     if (any) {
         const DevPlane &Qc = dj.cur.lv[1];
         const uint8_t *sp0 = uni_ptr(Qc.base + (ptrdiff_t)qy * Qc.stride + qx);
@@ -3389,6 +3449,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 }
             }
         };
+#endif
         auto flush = [&]() { // at most 8 block rows per u16 lane (8 x 32 x 255 < 2^16)
             qsad_unpack(a0, acc32[0]);
             qsad_unpack(a1, acc32[1]);
