@@ -125,6 +125,8 @@ def main():
     ap.add_argument("--no-single-picture", "--no-alt-mode", dest="no_alt", action="store_true",
                     help="skip the timing of the other picture count (batched / single picture)")
     ap.add_argument("--no-upload", action="store_true", help="skip the host-upload (PCIe-inclusive) timing")
+    ap.add_argument("--no-sb-results", action="store_true",
+                    help="skip the timing of the same steps with the per-SB results (candidates, distortions) written")
     ap.add_argument("--lanes", type=int, default=2, choices=(1, 2),
                     help="submission lanes the timed steps alternate over (svtme_submit_batch_device_lane); the "
                          "overlapped two-lane rate is reported beside the one-lane value")
@@ -274,6 +276,35 @@ def main():
             ta = torch.tensor([alt_ms], dtype=torch.float64, device=dev)
             dist.all_reduce(ta, op=dist.ReduceOp.MAX)
             alt_ms = float(ta.item())
+    # the same steps with the per-SB results written too (svtme_sb_result: candidate
+    # arrays, me_distortion, GM flags, motion_estimation.c:2520-3007), which the
+    # encoder's PA-ME consumer reads beside the records; `value` is the records alone
+    # (the north star's best MV + SAD per PU)
+    sb_ms = None
+    if not args.no_sb_results and jobs[0].me_type != S.ME_MCTF:
+        sbsz = S.SB_RESULT_DTYPE.itemsize
+        lsb = torch.zeros(P * count * sbsz, dtype=torch.uint8, device=dev)
+
+        def step_sb(i):
+            b = i & 1
+            for g0 in range(0, P, LP):
+                g1 = min(P, g0 + LP)
+                lane = nlaunch[0] % NL
+                nlaunch[0] += 1
+                gpu.submit_batch_device(jobs[g0:g1], [local[b].data_ptr() + p * chunk_bytes for p in range(g0, g1)],
+                                        [lsb.data_ptr() + p * count * sbsz for p in range(g0, g1)], lane=lane)
+        for i in range(args.warmup):
+            step_sb(i)
+        fence()
+        t0s = time.perf_counter()
+        for i in range(args.steps):
+            step_sb(args.warmup + i)
+        fence()
+        sb_ms = (time.perf_counter() - t0s) / args.steps * 1e3
+        if world > 1:
+            ts = torch.tensor([sb_ms], dtype=torch.float64, device=dev)
+            dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+            sb_ms = float(ts.item())
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -454,6 +485,10 @@ def main():
                 "algorithmic_hbm_gbps": round(bps * n_sb * P_alt / (alt_ms * 1e-3) / 1e9, 1),
                 "note": "one picture per GPU per step, consecutive steps alternating the two submission lanes "
                         "(svtme_submit_batch_device_lane): kernels of consecutive steps overlap, wall clock"},
+            "with_sb_results": None if sb_ms is None else {
+                "ms_per_step": round(sb_ms, 4), "value": round(n_sb * P / (sb_ms * 1e-3), 1),
+                "note": "the same steps writing the per-SB results too (svtme_sb_result: candidate arrays, "
+                        "me_distortion, GM flags) that the encoder's PA-ME consumer reads beside the records"},
             "upload": upload,
             "sb_ref_per_s": round(value * R, 1),
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),

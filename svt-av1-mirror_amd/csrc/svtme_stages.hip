@@ -1181,11 +1181,17 @@ __device__ __forceinline__ Row8 row8(const uint8_t *a0, int stride, int ro, int 
 // position rows yf + 2t (t < tv); plane rows are clamped to ylast. Rows are
 // loaded two ahead of their use. Returns the tile's minimum key
 // (sad << 32 | y << 16 | x), ~0 if no position is valid.
+#ifndef SVTME_A1_UNI_KH
+#define SVTME_A1_UNI_KH 1
+#endif
 template <int T, bool FULLK = false> // FULLK: a full-height SB (kh == 8), no row checks
 __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                          int yf, int tv, int ylast, int kh,
                                                          const uint32_t (&sr)[8][4]) {
     constexpr int NR = T + 7;
+#if SVTME_A1_UNI_KH
+    kh = UNI(kh); // the block-row checks become scalar compares and branches
+#endif
     unsigned long long acc[T][HQ16];
 #pragma unroll
     for (int t = 0; t < T; t++)
