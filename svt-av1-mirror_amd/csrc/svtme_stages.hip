@@ -2637,17 +2637,68 @@ __device__ __forceinline__ FpArea fp_area(const DevJob &dj, const SbGeo &G, int 
 // [h * part / parts, h * (part + 1) / parts); the 85-PU argmin keys go to kp
 // (atomic min when parts > 1), the slot state to cs (part 0). src: this lane's
 // 8x8 source block rows (lane = block by, bx).
+// TF-ME records written by the wavefront that searched them: an ME_MCTF job has
+// no me_prune_ref (motion_estimation.c:3103, the records of one SB are
+// independent) and no candidate arrays (:3126), so with one band per record and
+// no per-SB output the record is the decode of this wavefront's 85 keys
+// (stage_e_body / stage_c_tail's record words) and k_stage_e is not launched
+__device__ __forceinline__ bool direct_records(const DevJob &dj) {
+    return dj.job.me_type == SVTME_ME_MCTF && dj.parts == 1 && dj.out_sb == nullptr;
+}
+__device__ __forceinline__ void direct_record(svtme_ref_record *rec, const CSlot &v, unsigned long long k8,
+                                              unsigned long long k16, unsigned long long k32, unsigned long long k64) {
+    const int lane   = threadIdx.x & 63;
+    uint32_t *o      = (uint32_t *)rec;
+    const uint32_t wm = magic_u32((uint32_t)max(1, (int)v.w));
+    auto put = [&](unsigned long long key, int pu) {
+        uint32_t sad = U32MAX, mv = 0;
+        if (v.searched) {
+            const uint32_t ord = (uint32_t)key;
+            sad                = (uint32_t)(key >> 32);
+            int16_t mx, my;
+            if (v.probe && ord == 0) {
+                mx = v.xc;
+                my = v.yc;
+            } else {
+                const int p = (int)ord - (int)v.probe;
+                const int q = mdiv(p, wm);
+                my          = i16(v.yo + q);
+                mx          = i16(v.xo + (p - q * v.w));
+            }
+            mv = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
+        }
+        o[pu]      = sad;
+        o[85 + pu] = mv;
+    };
+    put(k8, 21 + lane);
+    if ((lane & 3) == 0)
+        put(k16, 5 + (lane >> 2));
+    if ((lane & 15) == 0)
+        put(k32, 1 + (lane >> 4));
+    if (lane == 63)
+        put(k64, 0);
+    if (lane < 6) {
+        const uint32_t t[6] = {(uint32_t)v.hme_sad, (uint32_t)(v.hme_sad >> 32),
+                               (uint32_t)(uint16_t)v.sc_x | ((uint32_t)(uint16_t)v.sc_y << 16), v.zz,
+                               (uint32_t)v.searched | ((uint32_t)v.do_ref << 8) | ((uint32_t)v.tf_exit << 16), 0u};
+        o[170 + lane] = t[lane];
+    }
+}
+
 template <bool SUB, bool K32, int TQ = (SUB ? FP_TQ : 2), bool WIDE = false, int WHOLE = 7>
 __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s, const uint32_t (&src)[SUB ? 4 : 8][2],
                                         int by, int bx, uint64_t hme_sad, uint32_t zz, uint32_t rdiv, int16_t sc_x,
                                         int16_t sc_y, uint8_t dref, uint8_t tf_exit, int part, uint32_t parts,
-                                        unsigned long long *kp, CSlot *cs) {
+                                        unsigned long long *kp, CSlot *cs, svtme_ref_record *rec = nullptr) {
     const int lane = threadIdx.x & 63;
     const int l = s >> 2, r = s & 3;
     const uint32_t ox = G.ox, oy = G.oy;
     if (!dref || tf_exit) {
+        const CSlot cv{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
         if (part == 0 && lane == 0)
-            *cs = CSlot{hme_sad, zz, sc_x, sc_y, 0, 0, 0, 0, 0, 0, dref, 0, tf_exit};
+            *cs = cv;
+        if (rec)
+            direct_record(rec, cv, 0, 0, 0, 0);
         return;
     }
     const DevPlane &P = dj.ref[l][r].lv[0];
@@ -2710,8 +2761,11 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
         if (lane == 63)
             atomicMin(&kp[0], k64);
     }
+    const CSlot cv{hme_sad, zz, sc_x, sc_y, xo, yo, w, xc, yc, 1, dref, (uint8_t)probe, 0};
     if (part == 0 && lane == 0)
-        *cs = CSlot{hme_sad, zz, sc_x, sc_y, xo, yo, w, xc, yc, 1, dref, (uint8_t)probe, 0};
+        *cs = cv;
+    if (rec)
+        direct_record(rec, cv, k8, k16, k32, k64);
 }
 
 
@@ -2760,8 +2814,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
     const uint8_t tf_exit = mctf && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // motion_estimation.c:3109-3113
     CSlot *cs = dj.cslot + (size_t)sb_local * dj.R + k;
     unsigned long long *kp = dj.keys + ((size_t)sb_local * dj.R + k) * SVTME_PU_COUNT;
+    svtme_ref_record *rec = direct_records(dj) ? dj.out_records + (size_t)sb_local * dj.R + k : nullptr;
     fp_slot<SUB, K32, (SUB ? FP_TQ : 2), WIDE>(dj, G, s, src, by, bx, hme_sad, zz, rdiv, sc_x, sc_y, dref, tf_exit, part,
-                                             parts, kp, cs);
+                                             parts, kp, cs, rec);
 }
 
 // ============================================================================
@@ -4545,7 +4600,12 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
             SVTME_LAUNCH((svtme::k_stage_c1<true, true>), grid, 3, bc);
         else
             SVTME_LAUNCH((svtme::k_stage_c1<true, false>), grid, 3, bc);
-        SVTME_LAUNCH(svtme::k_stage_e, dim3(be.total), 4, be);
+        bool direct = true; // every record made by k_stage_c1 (direct_records)
+        for (uint32_t k = 0; k < n; k++)
+            direct = direct && h_jobs[k].job.me_type == SVTME_ME_MCTF && h_jobs[k].parts == 1 && !h_jobs[k].out_sb &&
+                     !svtme_fp_wide_lds(&h_jobs[k].job.ctrl);
+        if (!direct)
+            SVTME_LAUNCH(svtme::k_stage_e, dim3(be.total), 4, be);
     } else if (full)
         SVTME_LAUNCH(svtme::k_stage_c<false>, dim3(be.total), 3, be);
     else

@@ -143,6 +143,9 @@ def test_mctf_parity(svtme, gpu, case):
         gpu.upload(4000 + t, f)
     job = S.case_job(ctrl, w, h, 4000 + cur, (4000 + ref,), (), tl, me_type=S.ME_MCTF, tf_me_exit_th=th)
     recs, sbr = gpu.submit(job)
+    # without per-SB results the split path's records come from the searching
+    # wavefronts themselves (direct_records: no k_stage_e launch)
+    recs_direct, _ = gpu.submit(job, with_sb_results=False)
     pyr = {t: S.build_host_pyramid(f, "oracle") for t, f in frames.items()}
     ojob = S.case_job(ctrl, w, h, cur, (ref,), (), tl, me_type=S.ME_MCTF, tf_me_exit_th=th)
     orecs, osbr = S.run_checker(ojob, pyr[cur], {(0, 0): pyr[ref]}, "oracle", nthreads=8)
@@ -150,6 +153,7 @@ def test_mctf_parity(svtme, gpu, case):
         gpu.release(4000 + t)
     errs = S.compare_records(orecs, recs, osbr, sbr)
     assert not errs, errs[:5]
+    assert recs_direct.tobytes() == recs.tobytes()
 
 
 def _controls_case(S, gpu, ctrl, w, h, l0, l1, tl=1, kind="pan"):
