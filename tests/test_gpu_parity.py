@@ -156,6 +156,35 @@ def test_mctf_parity(svtme, gpu, case):
     assert recs_direct.tobytes() == recs.tobytes()
 
 
+def test_mctf_batch_mixed_outputs(svtme, gpu):
+    """A batch of TF-ME jobs (one launch group) where only the middle job asks for
+    per-SB results: k_stage_e then runs for every job and rewrites the records the
+    direct jobs' wavefronts already wrote. Records equal the single-job ones, with
+    and without per-SB results in the batch."""
+    import torch
+
+    S = svtme
+    w, h = 640, 360
+    frames = S.test_frames("pan", w, h, [5, 6, 7, 8, 9])
+    for t, f in frames.items():
+        gpu.upload(4500 + t, f)
+    ctrl = S.derive_controls_tf(2, 1, 35, S.input_resolution_of(w, h))
+    jobs = [S.case_job(ctrl, w, h, 4508, (4500 + r,), (), 1, me_type=S.ME_MCTF, tf_me_exit_th=0) for r in (7, 9, 6)]
+    single = [gpu.submit(j, with_sb_results=False)[0] for j in jobs]
+    nb = single[0].nbytes
+    nsb = single[0].shape[0]
+    for with_mid_sb in (False, True):
+        bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in jobs]
+        sbs = [None, torch.zeros(nsb * S.SB_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda"), None]
+        gpu.submit_batch_device(jobs, [b.data_ptr() for b in bufs],
+                                [s.data_ptr() if s is not None else None for s in sbs] if with_mid_sb else None)
+        gpu.sync()
+        for k, b in enumerate(bufs):
+            assert b.cpu().numpy().tobytes() == single[k].tobytes(), (with_mid_sb, k)
+    for t in frames:
+        gpu.release(4500 + t)
+
+
 def _controls_case(S, gpu, ctrl, w, h, l0, l1, tl=1, kind="pan"):
     frames = S.test_frames(kind, w, h, sorted(set([8] + list(l0) + list(l1))))
     for t, f in frames.items():
