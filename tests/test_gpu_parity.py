@@ -417,3 +417,43 @@ def test_realtime_split_path_vs_reference_golden(svtme, gpu, case, monkeypatch):
     would take, against the reference's outputs."""
     monkeypatch.setenv("SVTME_NO_FUSED_HME", "1")
     test_picture_vs_reference_golden(svtme, gpu, case)
+
+
+def test_job_validation_errors(svtme, gpu):
+    """Malformed jobs are refused with SVTME_ERR_BAD_PARAMETER and a message,
+    before anything is launched, and the context stays usable: a picture that is
+    not resident, a size that is not a multiple of 8 or does not match the
+    resident planes, an SB range outside the picture, reference counts beyond
+    the reference's 2 x 4, an unknown me_type."""
+    import copy
+
+    S = svtme
+    w, h = 320, 192
+    syn = S.Synth(w, h)
+    frames = {t: syn.frame(t) for t in (7, 8)}
+    for t, f in frames.items():
+        gpu.upload(6000 + t, f)
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    good = S.make_job(w, h, ctrl, 6008, (6007,), (), temporal_layer_index=1, ref_count_used=(1, 0))
+    ok_recs, _ = gpu.submit(good)
+
+    def bad(mut, needle):
+        j = copy.copy(good)
+        mut(j)
+        with pytest.raises(RuntimeError) as ei:
+            gpu.submit(j)
+        assert "0x" in str(ei.value) and needle in str(ei.value), str(ei.value)
+
+    bad(lambda j: setattr(j, "picture_number", 6999), "not resident")
+    bad(lambda j: j.ref_picture_number[0].__setitem__(0, 6998), "not resident")
+    bad(lambda j: setattr(j, "width", w + 4), "multiple of 8")
+    bad(lambda j: setattr(j, "width", w - 64), "is 320x192")
+    bad(lambda j: setattr(j, "sb_begin", S.sb_total(w, h)), "outside the picture")
+    bad(lambda j: setattr(j, "sb_count", S.sb_total(w, h) + 1), "outside the picture")
+    bad(lambda j: j.num_refs.__setitem__(0, 5), "reference counts")
+    bad(lambda j: setattr(j, "me_type", 7), "me_type")
+    # the context still serves a good job with the same result
+    again, _ = gpu.submit(good)
+    assert again.tobytes() == ok_recs.tobytes()
+    for t in frames:
+        gpu.release(6000 + t)
