@@ -3381,8 +3381,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     const uint32_t npairs   = dj.tb_count >> 1; // the list holds the 4 quadrants of each slot in order
     const uint32_t sb_local = UNI(gw / npairs);
     const int e0            = UNI(dj.tb_list[2 * (gw - sb_local * npairs)]);
-    const int s = e0 >> 2, half = lane >> 5, q = (e0 & 3) + half, l = s >> 2, r = s & 3;
-    const int qd = lane & 3, pr = (lane >> 2) & 7; // position quad, position row pair
+    // lane = rh * 32 + half * 16 + pr_lo * 4 + qd: a quadrant (half) takes rows 0 and 2 or 1 and 3 of
+    // the wave, so each 32-lane LDS group reads position row pairs 0-3 (rh = 0) or 4-7 of both
+    // quadrants: 24 pr + qd (+ the other window's 580 = 4 mod 32) are 32 distinct banks (lanes 0-31
+    // of one quadrant had pr and pr + 4 on one bank)
+    const int half = (lane >> 4) & 1, s = e0 >> 2, q = (e0 & 3) + half, l = s >> 2, r = s & 3;
+    const int qd = lane & 3, pr = ((lane >> 5) << 2) | ((lane >> 2) & 3); // position quad, position row pair
     const SbGeo G = sb_geo(dj, sb_local);
     BState *b     = dj.bst + sb_local;
     const DevPlane &P = dj.ref[l][r].lv[1];
@@ -3433,7 +3437,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     uint32_t *win = l1w[wid][half];
     if (any) {
         if (active) { // 30 lanes of the half: 10 rows x 3 dword groups per pass
-            const int l32 = lane & 31, rr = l32 / 3, cg = l32 - 3 * rr;
+            const int l32 = (lane & 15) | ((lane >> 5) << 4), rr = l32 / 3, cg = l32 - 3 * rr;
             for (int r0 = 0; r0 <= rlast; r0 += 10) {
                 const int row = r0 + rr;
                 if (rr < 10 && row <= rlast) {
@@ -3538,7 +3542,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             rows(std::false_type());
     }
     // keys (sad << 32 | y << 16 | x) of this lane's positions inside the area, then
-    // the minimum over the 32 lanes of the half (DPP in rows, then row 0 -> 1 / 2 -> 3)
+    // the minimum over the 32 lanes of the half (DPP in rows, then rows 0 + 2 / 1 + 3)
     unsigned long long best = ~0ull;
     if (search) {
 #pragma unroll
@@ -3562,11 +3566,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         L1MIN(DPP_ROW_SHR(2), 0xF);
         L1MIN(DPP_ROW_SHR(4), 0xF);
         L1MIN(DPP_ROW_SHR(8), 0xF);
-        L1MIN(DPP_ROW_BCAST15, 0xA);
 #undef L1MIN
     }
-    const unsigned long long kb = ((unsigned long long)rl32((uint32_t)(best >> 32), 31) << 32) | rl32((uint32_t)best, 31);
-    const unsigned long long kt = ((unsigned long long)rl32((uint32_t)(best >> 32), 63) << 32) | rl32((uint32_t)best, 63);
+    auto rowmin = [&](int ln) {
+        return ((unsigned long long)rl32((uint32_t)(best >> 32), ln) << 32) | rl32((uint32_t)best, ln);
+    };
+    const unsigned long long kb0 = rowmin(15), kb1 = rowmin(47), kt0 = rowmin(31), kt1 = rowmin(63);
+    const unsigned long long kb = kb0 < kb1 ? kb0 : kb1, kt = kt0 < kt1 ? kt0 : kt1;
     if (search) {
         uint32_t bs;
         int x, y;
@@ -3575,7 +3581,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         X  = i16((x + xo) * 2);
         Y  = i16((y + yo) * 2);
     }
-    if ((lane & 31) == 0) {
+    if ((lane & 47) == 0) { // lanes 0 and 16
         b->hx[s][q]   = X;
         b->hy[s][q]   = Y;
         b->hsad[s][q] = SD;
