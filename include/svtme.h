@@ -311,6 +311,18 @@ void *svtme_lane_stream(svtme_ctx *ctx, uint32_t lane);
  * not recorded and the read sets svtme_last_error(). */
 svtme_status svtme_set_timing(svtme_ctx *ctx, int enable);
 uint32_t svtme_timing_read(svtme_ctx *ctx, float stage_ms[5]);
+/* Kernel-path selection of a context, for diagnostics and A/B runs: each bit
+ * forces a general path where a specialised kernel would apply (results are
+ * identical). 0, the default, takes every specialised kernel that applies. A
+ * context starts with the bits of the environment variables named below (read
+ * once, at svtme_ctx_create); svtme_set_paths replaces them for the jobs
+ * submitted after it. */
+#define SVTME_PATH_NO_FUSED_HME 1u /* SVTME_NO_FUSED_HME: k_stage_a -> k_stage_d -> k_stage_b, not k_hme */
+#define SVTME_PATH_NO_L1_FULL 2u   /* SVTME_NO_L1_FULL: full-SAD HME-L1 on k_stage_b, not k_l1_full */
+#define SVTME_PATH_NO_L0_FULL 4u   /* SVTME_NO_L0_FULL: full-SAD stage A on k_stage_a, not k_l0_full */
+#define SVTME_PATH_NO_FP_WIDE 8u   /* SVTME_NO_FP_WIDE: wide full-pel areas on k_stage_c1, not k_fp_wide */
+#define SVTME_PATH_SPLIT_PASS 16u  /* SVTME_SPLIT_PASS: k_hme -> k_stage_c1 -> k_stage_e, not one k_hme */
+svtme_status svtme_set_paths(svtme_ctx *ctx, uint32_t paths);
 /* Device pointer of the last job's record buffer (for RCCL all-gather). */
 void *svtme_device_records(svtme_ctx *ctx, uint64_t *bytes);
 /* The HIP stream (hipStream_t) the context launches on, for event timing. */

@@ -93,6 +93,7 @@ struct DevJob {
     uint16_t sdist[8];             // |picture distance| of slot s (ref_dist_const)
     int16_t l0_sa[8][2];           // HME-L0 area (get_hme_l0_search_area)
     int16_t ph_sa[8][2][2];        // pre-HME region areas (prehme_core)
+    uint32_t paths;                // SVTME_PATH_* of the submitting context (host dispatch only)
 };
 
 // A launch over a batch of picture jobs (svtme_submit_batch_device). The jobs

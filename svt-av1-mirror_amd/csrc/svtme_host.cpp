@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -35,7 +36,7 @@ extern "C" uint32_t svtme_launch_key(const DevJob *dj);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_a1_list(const svtme_job *job, uint8_t *list, uint32_t *count);
-extern "C" uint32_t svtme_fp_parts(const svtme_controls *c);
+extern "C" uint32_t svtme_fp_parts_paths(const svtme_controls *c, uint32_t paths);
 extern "C" void svtme_hme_prepare(DevJob *dj);
 extern "C" bool svtme_hme_fused(const svtme_job *job);
 extern "C" bool svtme_hme_rt(const svtme_controls *c);
@@ -141,6 +142,7 @@ struct svtme_ctx {
     int t_pending = 0;
     uint32_t t_dropped = 0;
     Lane lanes[SVTME_LANES]; // lanes[0].s == stream
+    uint32_t paths = 0;      // SVTME_PATH_* (svtme_set_paths; the environment at creation)
     std::mutex mu;
 };
 
@@ -168,7 +170,26 @@ extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
         return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     c->lanes[0].s = c->stream;
+    // kernel-path selection from the environment, read once (diagnostic A/B runs)
+    static const struct {
+        const char *var;
+        uint32_t bit;
+    } env_paths[] = {{"SVTME_NO_FUSED_HME", SVTME_PATH_NO_FUSED_HME}, {"SVTME_NO_L1_FULL", SVTME_PATH_NO_L1_FULL},
+                     {"SVTME_NO_L0_FULL", SVTME_PATH_NO_L0_FULL},       {"SVTME_NO_FP_WIDE", SVTME_PATH_NO_FP_WIDE},
+                     {"SVTME_SPLIT_PASS", SVTME_PATH_SPLIT_PASS}};
+    for (const auto &e : env_paths)
+        if (const char *v = getenv(e.var))
+            if (*v && strcmp(v, "0") != 0)
+                c->paths |= e.bit;
     *out = c;
+    return SVTME_OK;
+}
+
+extern "C" svtme_status svtme_set_paths(svtme_ctx *c, uint32_t paths) {
+    if (!c || (paths & ~31u))
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_set_paths: null ctx or unknown path bits 0x%x", paths);
+    std::lock_guard<std::mutex> lk(c->mu);
+    c->paths = paths;
     return SVTME_OK;
 }
 
@@ -542,7 +563,8 @@ static svtme_status validate_job(svtme_ctx *c, const svtme_job *job, DevJob *dj,
         return SVTME_OK;
     };
     memset(dj, 0, sizeof(*dj));
-    dj->job = *job;
+    dj->job   = *job;
+    dj->paths = c->paths;
     svtme_status st;
     if ((st = find(job->picture_number, &dj->cur)))
         return st;
@@ -623,7 +645,7 @@ static svtme_status submit_batch_locked(svtme_ctx *c, const svtme_job *jobs, uin
         return st;
     bool any_banded = false, any_single = false, any_wide = false;
     for (uint32_t k = 0; k < n; k++) {
-        hj[k].parts = svtme_fp_parts(&hj[k].job.ctrl);
+        hj[k].parts = svtme_fp_parts_paths(&hj[k].job.ctrl, hj[k].paths);
         any_wide |= hj[k].parts != 0;
         any_banded |= hj[k].parts > 1;
         any_single |= hj[k].parts == 1;

@@ -1181,17 +1181,12 @@ __device__ __forceinline__ Row8 row8(const uint8_t *a0, int stride, int ro, int 
 // position rows yf + 2t (t < tv); plane rows are clamped to ylast. Rows are
 // loaded two ahead of their use. Returns the tile's minimum key
 // (sad << 32 | y << 16 | x), ~0 if no position is valid.
-#ifndef SVTME_A1_UNI_KH
-#define SVTME_A1_UNI_KH 1
-#endif
 template <int T, bool FULLK = false> // FULLK: a full-height SB (kh == 8), no row checks
 __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                          int yf, int tv, int ylast, int kh,
                                                          const uint32_t (&sr)[8][4]) {
     constexpr int NR = T + 7;
-#if SVTME_A1_UNI_KH
     kh = UNI(kh); // the block-row checks become scalar compares and branches
-#endif
     unsigned long long acc[T][HQ16];
 #pragma unroll
     for (int t = 0; t < T; t++)
@@ -2443,12 +2438,8 @@ __device__ __forceinline__ void fp_rows32(PuMin<true> &M, const uint8_t *g, int 
 
 
 
-#ifndef SVTME_FP_WHOLE // 0: every area through fp_rows32 (A/B builds)
-#define SVTME_FP_WHOLE 1
-#endif
-#ifndef SVTME_HME_WHOLE // the whole-area shapes k_hme takes (fp_slot WHOLE bits)
-#define SVTME_HME_WHOLE 2
-#endif
+// the whole-area shapes k_hme takes (fp_slot WHOLE bits: 1 full rows 8 x 8, 2 sub-sampled 8 x 3 / 8 x 4)
+#define HME_WHOLE 2
 // K32, an area 8 wide searched whole (TF-ME level 2: 8 x 8 full rows; the p8
 // searches: 8 x 3 / 8 x 4 sub-sampled rows): every reference row of the lane's
 // block is loaded and realigned once and feeds each (search row, block row) pair
@@ -2735,7 +2726,7 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     const uint32_t obase = probe ? 1u : 0u; // the centre probe wins ties: order 0
     if constexpr (K32) {
         // an area 8 wide searched whole (wave-uniform)
-        const bool whole = SVTME_FP_WHOLE && !WIDE && w == 8 && parts == 1; // WIDE: areas >= 24 wide
+        const bool whole = !WIDE && w == 8 && parts == 1; // WIDE: areas >= 24 wide
         if ((SUB ? (WHOLE & 2) && (h == 3 || h == 4) : (WHOLE & 1) && h == 8) && whole)
             fp_rows32_whole<SUB>(M, g, P.stride >> 2, h, obase, src, by, bx);
         else
@@ -2847,10 +2838,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
                      // search rows of a 16-lane read group (hr = 0, 1) fall on disjoint bank halves
 #define FPW_BOFF 40  // fw_b within the row: one base address serves both copies
 #define FPW_ROWS 96  // window rows per workgroup (4 bands + 62; the host bounds the band height)
-#ifndef FPW_TQ
 #define FPW_TQ 4 // position quads per set (2 quad pairs, 16 positions; 6 wastes a third of the
                // last set at 64 positions, 8 measures the same as 4)
-#endif
 
 struct FpW {
     uint32_t b8t, b8b, b16, b32, b64; // K32 keys: 8x8 / 16x16 (sad << 16 | order), 32x32 / 64x64 (sad << 12 | order)
@@ -2916,12 +2905,7 @@ __device__ __forceinline__ uint32_t fpw_rebase(uint32_t b, uint32_t m, uint32_t 
     return min_u32(b, m == 0xFFFFFFFFu ? m : m + base);
 }
 
-#ifndef FPW_W0
-#define FPW_W0 1 // the per-(SB, reference) prologue by wave 0 only
-#endif
-#ifndef FPW_WAVES
 #define FPW_WAVES 5 // waves per SIMD: 5 workgroups of 30 KB LDS per CU
-#endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WAVES, FPW_WAVES))) k_fp_wide(const DevBatch B) {
     __shared__ __attribute__((aligned(16))) uint32_t fw[FPW_ROWS * FPW_PITCH]; // rows: fw_a | fw_b
     constexpr int ROWS = 4, RSTEP = 2; // sub-sampled rows
@@ -2964,7 +2948,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
     const int sdw          = P.stride >> 2;
     FpW b{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     // search centre, area and centre probe: the same for the workgroup's 4 bands,
-    // made by wave 0 and handed to the others through LDS (FPW_W0 = 0: every wave)
+    // made by wave 0 and handed to the others through LDS
     auto prologue = [&](FpArea &A) -> bool {
         const SlotCentre scv   = final_centre(job, dj.bst + sb_local, valid_mask(job));
         const uint64_t hme_sad = rl64(scv.hme_sad, s);
@@ -3018,7 +3002,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
         return true;
     };
     FpArea A;
-#if FPW_W0
     __shared__ FpArea fx_area;
     __shared__ uint32_t fx_keys[5][64], fx_run;
     if (wid == 0) {
@@ -3036,10 +3019,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
     A     = fx_area;
     b.b8t = fx_keys[0][lane], b.b8b = fx_keys[1][lane], b.b16 = fx_keys[2][lane];
     b.b32 = fx_keys[3][lane], b.b64 = fx_keys[4][lane];
-#else
-    if (!prologue(A))
-        return;
-#endif
     const int w = A.w, h = A.h;
 
     // stage the rows [Y0, Y1 + 62) of the 4 bands: fw_a[row][j] = window dword j
@@ -3296,7 +3275,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         using A8 = std::integral_constant<uint32_t, 8u>;
         using A2 = std::integral_constant<uint32_t, 2u>;
         using AF = std::integral_constant<uint32_t, (1u << PR) - 1u>;
-        // head: t < PR - 1 (position rows j <= t)
+        if constexpr (PR == 4) {
+            if (bhs == 2) { // an 8-row SB: block rows t - j in {0, 1} only
+                using A6 = std::integral_constant<uint32_t, 6u>;
+                row(0, A1(), FW);
+                row(1, A3(), FW);
+                row(2, A6(), FW);
+                row(3, AC(), FW);
+                row(4, A8(), FW);
+                return;
+            }
+        }
+        // head: t < PR - 1 (position rows j <= t; bhs >= PR - 1 from here)
         row(0, A1(), FW);
         if constexpr (PR == 4) {
             row(1, A3(), FW);
@@ -3351,9 +3341,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
 }
 
-#ifndef SVTME_L1_LDS // 0: k_l1_full's rows from global memory, realigned per row (A/B builds)
-#define SVTME_L1_LDS 1
-#endif
 #define L1W_PITCH 12                  // dwords per staged window row (16 positions + 31 columns + 1)
 #define L1W_HALF (48 * L1W_PITCH + 4) // 48 rows; + 4 dwords: the two halves' rows on different banks
 // ============================================================================
@@ -3428,7 +3415,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     const bool active  = search && sw > 0 && shh > 0;
     const bool any     = __ballot(active) != 0;
     uint32_t acc32[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-#if SVTME_L1_LDS
     // this half's window in LDS, realigned to position 0: rows 0 .. rlast (<= 47) x
     // 12 dwords (positions 0 .. 15 + 31 block columns + 1); every qsad pair is then
     // one 4-byte-aligned 8-byte LDS read (ds_read2_b32), with no v_alignbyte and no
@@ -3481,44 +3467,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 }
             }
         };
-#else
-    if (any) {
-        const DevPlane &Qc = dj.cur.lv[1];
-        const uint8_t *sp0 = uni_ptr(Qc.base + (ptrdiff_t)qy * Qc.stride + qx);
-        const int sst      = UNI(Qc.stride);
-        unsigned long long a0 = 0, a1 = 0; // position rows 2 pr, 2 pr + 1
-        // one reference row 2 pr + t of the window (raw dwords qd .. qd + 9, realigned to
-        // d[0 .. 8]): block row t of position row 2 pr (D0) and block row t - 1 of 2 pr + 1
-        // (D1). The row loop is peeled and chunked so that no qsad is predicated (uniform
-        // conditions inside the body became v_cndmask pairs); prefetching the next row one
-        // iteration ahead measured slower (66 VGPRs, 7 waves)
-        auto row = [&](int t, auto D0, auto D1, auto FW) {
-            constexpr bool do0 = decltype(D0)::value, do1 = decltype(D1)::value, fw = decltype(FW)::value;
-            const uint32_t off = (uint32_t)(wofs + min(2 * pr + t, rlast) * rowbytes + 4 * qcol);
-            const u32x4a4 ra = bld4(rs, off, 0), rb = bld4(rs, off + 16u, 0);
-            const uint32_t r8 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 32u), 0, 0);
-            const uint32_t r9 = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)(off + 36u), 0, 0);
-            const uint32_t raw[10] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w, r8, r9};
-            uint32_t d[9];
-#pragma unroll
-            for (int j = 0; j < 9; j++) d[j] = __builtin_amdgcn_alignbyte(raw[j + 1], raw[j], (uint32_t)sh);
-            // source rows t and t - 1: scalar loads (nothing carried between rows)
-            const uint8_t *s0 = sp0 + (ptrdiff_t)(do0 ? t : t - 1) * sst;
-            const uint4 c0 = sld4(s0), c1 = sld4(s0 + 16);
-            const uint4 p0 = do0 && do1 ? sld4(s0 - sst) : c0, p1 = do0 && do1 ? sld4(s0 - sst + 16) : c1;
-            const uint32_t sc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-            const uint32_t sp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                if (fw || k < nd) {
-                    if (do0)
-                        a0 = qsad(d[k], d[k + 1], sc[k], a0);
-                    if (do1)
-                        a1 = qsad(d[k], d[k + 1], do0 ? sp[k] : sc[k], a1);
-                }
-            }
-        };
-#endif
         auto flush = [&]() { // at most 8 block rows per u16 lane (8 x 32 x 255 < 2^16)
             qsad_unpack(a0, acc32[0]);
             qsad_unpack(a1, acc32[1]);
@@ -3812,19 +3760,9 @@ struct HmeSh {
 // per record, then k_stage_e); else the HME state goes to BState for them.
 // wave 0's serial phases (decisions, search tables, final centre) run at raised
 // issue priority: the workgroup's other waves wait for them at a barrier
-#ifndef HME_PRIO
-#define HME_PRIO 1
-#endif
-#if HME_PRIO
 #define HME_PRIO_HI() __builtin_amdgcn_s_setprio(2)
 #define HME_PRIO_LO() __builtin_amdgcn_s_setprio(0)
-#else
-#define HME_PRIO_HI()
-#define HME_PRIO_LO()
-#endif
-#ifndef HME_WAVES_PER_EU
 #define HME_WAVES_PER_EU 8 // 64 VGPRs: 8 workgroups per CU
-#endif
 template <bool FP, bool SUB_ME, bool K32, bool RT = false> // RT: the real-time tune's HME-L0 reduction (a1_table)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WAVES_PER_EU, HME_WAVES_PER_EU))) k_hme(const DevBatch B) {
     __shared__ HmeSh sh;
@@ -4269,7 +4207,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         }
         const int s         = k < gj.job.num_refs[0] ? k : 4 + (k - gj.job.num_refs[0]);
         const SlotCentre &v = sh.cen[s];
-        fp_slot<SUB_ME, K32, 2, false, SVTME_HME_WHOLE>(gj, G, s, src, by, bx, rl64(v.hme_sad, 0), (uint32_t)UNI(v.zz), (uint32_t)UNI(v.reduce_div),
+        fp_slot<SUB_ME, K32, 2, false, HME_WHOLE>(gj, G, s, src, by, bx, rl64(v.hme_sad, 0), (uint32_t)UNI(v.zz), (uint32_t)UNI(v.reduce_div),
                                 (int16_t)UNI(v.sc_x), (int16_t)UNI(v.sc_y), (uint8_t)UNI(v.do_ref),
                                 (uint8_t)UNI(sh.tf_exit), 0, 1u, &sh.u.st.keys[k][0], &sh.cin[k]);
     }
@@ -4402,9 +4340,10 @@ extern "C" void svtme_hme_prepare(DevJob *dj) {
 // k_hme applies: every SB 64 wide, sub-sampled HME rows
 extern "C" bool svtme_hme_fused(const svtme_job *job) {
     const svtme_controls &c = job->ctrl;
-    return (job->width % 64) == 0 && c.hme_search_method != SVTME_FULL_SAD_SEARCH &&
-           getenv("SVTME_NO_FUSED_HME") == nullptr;
+    return (job->width % 64) == 0 && c.hme_search_method != SVTME_FULL_SAD_SEARCH;
 }
+// the same with the context's path selection (svtme_set_paths) applied
+static bool hme_fused(const DevJob &dj) { return svtme_hme_fused(&dj.job) && !(dj.paths & SVTME_PATH_NO_FUSED_HME); }
 
 // the real-time tune's HME-L0 reduction is on (get_hme_l0_search_area,
 // motion_estimation.c:1811-1819): k_hme<..., RT = true> only
@@ -4417,9 +4356,9 @@ extern "C" bool svtme_hme_rt(const svtme_controls *c) {
 // 16 x 16 positions (TF-ME levels 0-2)
 extern "C" bool svtme_l1_full(const svtme_controls *c) {
     return c->hme_search_method == SVTME_FULL_SAD_SEARCH && c->enable_hme_flag && c->enable_hme_level1_flag &&
-           !c->enable_hme_level2_flag && c->hme_l1_sa.width <= 16 && c->hme_l1_sa.height <= 16 &&
-           !getenv("SVTME_NO_L1_FULL");
+           !c->enable_hme_level2_flag && c->hme_l1_sa.width <= 16 && c->hme_l1_sa.height <= 16;
 }
+static bool l1_full(const DevJob &dj) { return svtme_l1_full(&dj.job.ctrl) && !(dj.paths & SVTME_PATH_NO_L1_FULL); }
 
 // k_l0_full applies: full-SAD HME rows, HME-L0 on, no pre-HME, HME-L0 quadrants of
 // at most 16 x 8 positions for every slot, whole source dwords on partial SBs
@@ -4427,7 +4366,7 @@ extern "C" bool svtme_l0_full(const DevJob *dj) {
     const svtme_controls &c = dj->job.ctrl;
     if (c.hme_search_method != SVTME_FULL_SAD_SEARCH || c.prehme_enable || !c.enable_hme_flag ||
         !c.enable_hme_level0_flag || svtme_hme_rt(&c) || (dj->job.width % 64) % 16 != 0 ||
-        getenv("SVTME_NO_L0_FULL"))
+        (dj->paths & SVTME_PATH_NO_L0_FULL))
         return false;
     for (int s = 0; s < 8; s++)
         if (dj->l0_sa[s][0] > 16 || dj->l0_sa[s][1] > 16)
@@ -4467,7 +4406,7 @@ extern "C" bool svtme_fp_wide(const svtme_controls *c) {
 // at most 8 rows with up to 16 parts)
 extern "C" bool svtme_fp_wide_lds(const svtme_controls *c) {
     if (c->me_search_method == SVTME_FULL_SAD_SEARCH || c->enable_me_sr_adjustment == 2 || !svtme_fp_k32(c) ||
-        !svtme_fp_wide(c) || getenv("SVTME_NO_FP_WIDE"))
+        !svtme_fp_wide(c))
         return false;
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
@@ -4475,28 +4414,36 @@ extern "C" bool svtme_fp_wide_lds(const svtme_controls *c) {
     return (w * h) / 512 >= 2 && 14 + nsets * FPW_TQ + 2 + 1 <= FPW_BOFF && h <= 8 * 16;
 }
 
-extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) {
+static bool fp_wide_lds(const svtme_controls *c, uint32_t paths) {
+    return svtme_fp_wide_lds(c) && !(paths & SVTME_PATH_NO_FP_WIDE);
+}
+static bool fp_wide_lds(const DevJob &dj) { return fp_wide_lds(&dj.job.ctrl, dj.paths); }
+
+// search-row bands per (SB, reference) of the wide full-pel stage under path selection `paths`
+extern "C" uint32_t svtme_fp_parts_paths(const svtme_controls *c, uint32_t paths) {
     if (c->enable_me_sr_adjustment == 2)
         return 0; // slot 0's 64x64 SAD feeds the other slots' areas: per-SB k_stage_c
     uint32_t w, h;
     fp_area_bound(c, &w, &h);
     uint32_t parts = (w * h) / 512;
-    if (svtme_fp_wide_lds(c)) { // workgroups of 4 bands of <= 8 rows
+    if (fp_wide_lds(c, paths)) { // workgroups of 4 bands of <= 8 rows
         parts = parts > (h + 7) / 8 ? parts : (h + 7) / 8;
         parts = (parts + 3) & ~3u;
     }
     return parts < 1 ? 1 : (parts > 16 ? 16 : parts);
 }
+extern "C" uint32_t svtme_fp_parts(const svtme_controls *c) { return svtme_fp_parts_paths(c, 0); }
 
 // Batch launch key: jobs launched together must agree on it (svtme_host.cpp
 // splits a batch into groups by it).
 extern "C" uint32_t svtme_launch_key(const DevJob *dj) {
     const bool full = dj->job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     return (uint32_t)full | (uint32_t)(dj->parts != 0) << 1 | (uint32_t)svtme_fp_k32(&dj->job.ctrl) << 2 |
-           (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)svtme_hme_fused(&dj->job) << 4 |
+           (uint32_t)(dj->job.ctrl.enable_hme_level2_flag != 0) << 3 | (uint32_t)hme_fused(*dj) << 4 |
            (uint32_t)(dj->parts == 1) << 5 | (uint32_t)svtme_fp_wide(&dj->job.ctrl) << 6 |
-           (uint32_t)svtme_hme_rt(&dj->job.ctrl) << 7 | (uint32_t)svtme_fp_wide_lds(&dj->job.ctrl) << 8 |
-           (uint32_t)svtme_l1_full(&dj->job.ctrl) << 9 | (uint32_t)svtme_l0_full(dj) << 10;
+           (uint32_t)svtme_hme_rt(&dj->job.ctrl) << 7 | (uint32_t)fp_wide_lds(*dj) << 8 |
+           (uint32_t)l1_full(*dj) << 9 | (uint32_t)svtme_l0_full(dj) << 10 |
+           (uint32_t)((dj->paths & SVTME_PATH_SPLIT_PASS) != 0) << 11;
 }
 
 static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, uint32_t (*units)(const DevJob &)) {
@@ -4518,7 +4465,8 @@ static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, ui
 // counts). ev (optional, timing): ten events, start / stop of stage k in
 // ev[2k], ev[2k+1] (k = A, D, B, C1|C, E), attached to the dispatch packets
 // themselves (hipExtLaunchKernelGGL: no extra packets, no gaps); *mask gets
-// bit k for every stage launched.
+// bit k for every stage launched. With the real-time tune on the split path,
+// stage A spans both stage-A rounds and the k_stage_d<true> between them.
 #define SVTME_LAUNCH(K, grid, k, ...)                                                                               \
     do {                                                                                                           \
         if (ev) {                                                                                                  \
@@ -4538,7 +4486,7 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     const DevBatch bd = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count; });
     const bool full = h0.job.ctrl.me_search_method == SVTME_FULL_SAD_SEARCH;
     const bool k32  = svtme_fp_k32(&h0.job.ctrl);
-    // the whole pass in one launch; SVTME_SPLIT_PASS=1 keeps k_hme -> k_stage_c1 -> k_stage_e (diagnostics)
+    // the whole pass in one launch; SVTME_PATH_SPLIT_PASS keeps k_hme -> k_stage_c1 -> k_stage_e (diagnostics)
     const bool rt = svtme_hme_rt(&h0.job.ctrl); // the real-time tune's HME-L0 reduction
 #define SVTME_HME(FP, SUB, K32)                                                                                     \
     do {                                                                                                           \
@@ -4547,7 +4495,7 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
         else                                                                                                       \
             SVTME_LAUNCH((svtme::k_hme<FP, SUB, K32, false>), dim3(bd.total), 0, bd);                              \
     } while (0)
-    if (svtme_hme_fused(&h0.job) && h0.parts == 1 && !getenv("SVTME_SPLIT_PASS")) {
+    if (hme_fused(h0) && h0.parts == 1 && !(h0.paths & SVTME_PATH_SPLIT_PASS)) {
         if (full && k32)
             SVTME_HME(true, false, true);
         else if (full)
@@ -4558,7 +4506,7 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
             SVTME_HME(true, true, false);
         return hipGetLastError();
     }
-    if (svtme_hme_fused(&h0.job)) {
+    if (hme_fused(h0)) {
         SVTME_HME(false, true, true);
     } else {
     const DevBatch ba = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta_count; });
@@ -4574,13 +4522,18 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
     if (rt) { // the real-time tune: slot 0's HME-L0 centre, then the other slots' HME-L0
         const DevBatch ba1 =
             make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.ta1_count; });
-        hipLaunchKernelGGL(svtme::k_stage_d<true>, dim3((bd.total + 3) / 4), dim3(256), 0, s, bd);
+        // timed as part of stage 0: the last of these launches re-records stage 0's stop event
+        hipEvent_t stop_d = ev && !ba1.total ? ev[1] : nullptr, stop_a = ev ? ev[1] : nullptr;
+        hipExtLaunchKernelGGL(svtme::k_stage_d<true>, dim3((bd.total + 3) / 4), dim3(256), 0, s, nullptr, stop_d, 0, bd);
         if (ba1.total)
-            hipLaunchKernelGGL(svtme::k_stage_a<true>, dim3((ba1.total + 3) / 4), dim3(256), 0, s, ba1);
+            hipExtLaunchKernelGGL(svtme::k_stage_a<true>, dim3((ba1.total + 3) / 4), dim3(256), 0, s, nullptr, stop_a, 0,
+                                  ba1);
+        if (ev)
+            *mask |= 1u;
     }
     SVTME_LAUNCH(svtme::k_stage_d<false>, dim3((bd.total + 3) / 4), 1, bd);
     const DevBatch bb = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.tb_count; });
-    if (bb.total && svtme_l1_full(&h0.job.ctrl)) { // two quadrants per wavefront
+    if (bb.total && l1_full(h0)) { // two quadrants per wavefront
         const DevBatch b2 =
             make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * (j.tb_count / 2); });
         SVTME_LAUNCH(svtme::k_l1_full, dim3((b2.total + 3) / 4), 2, b2);
@@ -4596,7 +4549,7 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
         const DevBatch bc = make_batch(d_jobs, h_jobs, n, [](const DevJob &j) { return j.job.sb_count * j.R * j.parts; });
         const dim3 grid((bc.total + 3) / 4);
         const bool wide = svtme_fp_wide(&h0.job.ctrl);
-        if (svtme_fp_wide_lds(&h0.job.ctrl))
+        if (fp_wide_lds(h0))
             SVTME_LAUNCH(svtme::k_fp_wide, grid, 3, bc);
         else if (full && k32 && wide)
             SVTME_LAUNCH((svtme::k_stage_c1<false, true, true>), grid, 3, bc);
@@ -4613,7 +4566,7 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
         bool direct = true; // every record made by k_stage_c1 (direct_records)
         for (uint32_t k = 0; k < n; k++)
             direct = direct && h_jobs[k].job.me_type == SVTME_ME_MCTF && h_jobs[k].parts == 1 && !h_jobs[k].out_sb &&
-                     !svtme_fp_wide_lds(&h_jobs[k].job.ctrl);
+                     !fp_wide_lds(h_jobs[k]);
         if (!direct)
             SVTME_LAUNCH(svtme::k_stage_e, dim3(be.total), 4, be);
     } else if (full)

@@ -25,6 +25,8 @@ MAX_SAD_VALUE = 128 * 128 * 255
 PAD_FULL, PAD_QUARTER, PAD_SIXTEENTH = 72, 32, 16
 SUB_SAD_SEARCH, FULL_SAD_SEARCH = 0, 1
 ME_MCTF, ME_OPEN_LOOP = 1, 3  # EbMeType (me_context.h:44-51)
+# kernel-path selection bits (include/svtme.h SVTME_PATH_*)
+PATH_NO_FUSED_HME, PATH_NO_L1_FULL, PATH_NO_L0_FULL, PATH_NO_FP_WIDE, PATH_SPLIT_PASS = 1, 2, 4, 8, 16
 # EbInputResolution (definitions.h:2079-2085)
 RES_240P, RES_360P, RES_480P, RES_720P, RES_1080P, RES_4K, RES_8K = range(7)
 
@@ -537,6 +539,8 @@ def load_product():
         lib.svtme_fetch.restype = C.c_int32
         lib.svtme_submit_picture_device.argtypes = [vp, C.POINTER(Job), vp, vp]
         lib.svtme_submit_picture_device.restype = C.c_int32
+        lib.svtme_set_paths.argtypes = [vp, C.c_uint32]
+        lib.svtme_set_paths.restype = C.c_int32
         lib.svtme_set_timing.argtypes = [vp, C.c_int]
         lib.svtme_set_timing.restype = C.c_int32
         lib.svtme_timing_read.argtypes = [vp, C.POINTER(C.c_float)]
@@ -651,6 +655,10 @@ class GpuME:
     def submit_device(self, job: Job, d_records: int, d_sb: int | None = None):
         self._check(self.lib.svtme_submit_picture_device(self.ctx, C.byref(job), d_records, d_sb),
                     "svtme_submit_picture_device")
+
+    def set_paths(self, paths: int):
+        """Kernel-path selection (SVTME_PATH_* bits; 0 = every specialised kernel)."""
+        self._check(self.lib.svtme_set_paths(self.ctx, paths), "svtme_set_paths")
 
     def set_timing(self, enable: bool = True):
         self._check(self.lib.svtme_set_timing(self.ctx, 1 if enable else 0), "svtme_set_timing")

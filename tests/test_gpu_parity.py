@@ -128,6 +128,10 @@ MCTF_CASES = [  # content, w, h, tf hme_me_level, qp_opt, cur, ref, tl, tf_me_ex
     ("hpan", 264, 200, 1, 0, 8, 9, 1, 0),
     ("sat", 192, 128, 2, 1, 8, 6, 2, 0),
     ("pan", 72, 40, 1, 0, 8, 7, 1, 0),
+    # k_l0_full<4> (HME-L0 quadrants taller than 8 rows) on a last SB row of 8 lines
+    # (height 8 mod 64) with whole 16-pixel source dwords: level 1, and level 2 above 480p
+    ("pan", 256, 200, 1, 0, 8, 7, 1, 0),
+    ("hpan", 1280, 712, 2, 1, 8, 9, 1, 0),
 ]
 
 
@@ -411,12 +415,15 @@ def test_picture_vs_reference_golden(svtme, gpu, case):
 
 
 @pytest.mark.parametrize("case", [c for c in GOLD_ME_CASES if "_rt" in c["name"]], ids=lambda c: c["name"])
-def test_realtime_split_path_vs_reference_golden(svtme, gpu, case, monkeypatch):
+def test_realtime_split_path_vs_reference_golden(svtme, gpu, case):
     """The real-time tune's HME-L0 reduction on the split HME path (k_stage_a ->
     k_stage_d<true> -> k_stage_a<true> -> k_stage_d), forced for widths k_hme
-    would take, against the reference's outputs."""
-    monkeypatch.setenv("SVTME_NO_FUSED_HME", "1")
-    test_picture_vs_reference_golden(svtme, gpu, case)
+    would take (svtme_set_paths), against the reference's outputs."""
+    gpu.set_paths(svtme.PATH_NO_FUSED_HME)
+    try:
+        test_picture_vs_reference_golden(svtme, gpu, case)
+    finally:
+        gpu.set_paths(0)
 
 
 def test_job_validation_errors(svtme, gpu):
