@@ -333,21 +333,24 @@ def main():
         me_ms = ms_per_step / P * world
         # pipelined: each step uploads a new current picture asynchronously
         # (svtme_picture_upload_async, pinned source) and searches it against the
-        # resident references; the upload stream overlaps the previous searches
+        # resident references on the next submission lane; 8 pictures rotate, so an
+        # upload waits only for the search of the picture it replaces, 8 steps back
+        # (scripts/upload_probe.py: 4 rotating pictures on one lane serialise more)
+        NP = 8
         pjobs = []
-        for k in range(4):
+        for k in range(NP):
             pj = W.workload_job(name)
             pj.picture_number = 910000 + k
             pjobs.append(pj)
-        pbuf = torch.zeros(n_sb * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        pbuf = [torch.zeros(n_sb * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device=dev) for _ in range(2)]
 
         def pipe(i):
-            gpu.upload_async(910000 + (i & 3), pinned.data_ptr(), Wd, Ht)
-            gpu.submit_batch_device([pjobs[i & 3]], [pbuf.data_ptr()])
-        for i in range(8):
+            gpu.upload_async(910000 + i % NP, pinned.data_ptr(), Wd, Ht)
+            gpu.submit_batch_device([pjobs[i % NP]], [pbuf[i & 1].data_ptr()], lane=i & 1)
+        for i in range(2 * NP):
             pipe(i)
         gpu.sync()
-        reps = 40
+        reps = 80
         t0p = time.perf_counter()
         for i in range(reps):
             pipe(i)
@@ -356,10 +359,10 @@ def main():
         # the same loop with the uploads only (the copy engine's rate)
         t0p = time.perf_counter()
         for i in range(reps):
-            gpu.upload_async(910000 + (i & 3), pinned.data_ptr(), Wd, Ht)
+            gpu.upload_async(910000 + i % NP, pinned.data_ptr(), Wd, Ht)
         gpu.sync()
         up_only_ms = (time.perf_counter() - t0p) / reps * 1e3
-        for k in range(4):
+        for k in range(NP):
             gpu.release(910000 + k)
         upload = {"pageable_ms_per_picture": round(pageable_ms, 4), "pinned_ms_per_picture": round(pinned_ms, 4),
                   "picture_bytes": int(frame.nbytes),
@@ -369,7 +372,7 @@ def main():
                   "async_upload_only_ms_per_picture": round(up_only_ms, 4),
                   "note": "upload + pyramid build of one picture from host memory, synchronous; pipelined: "
                           "asynchronous upload of each step's current picture (pinned) overlapped with the "
-                          "searches, one picture per launch"}
+                          "searches, one picture per launch on alternating lanes, 8 pictures rotating"}
 
     # roofline of the ME pass on this rank (one batched launch per stage)
     sbs_launch = count * P
@@ -423,6 +426,20 @@ def main():
                 "note": "measured HBM bytes per launch (traffic) / the kernel's average duration: the share of "
                         "the 8 TB/s the kernel really draws; the algorithmic frac counts every search window "
                         "as read from HBM, most of which neighbouring SBs' workgroups find in L2 / MALL"}
+
+    # what bounds the dominant kernel, from the evidence: the measured DRAM rate and the SAD-unit rate
+    dram_frac = dram["frac"] if dram else None
+    sad_frac = sad_rate / SAD_PEAK_T
+    if dram_frac is not None and dram_frac >= 0.5:
+        bound, limiter = "hbm", "measured HBM traffic at >= half of the 8 TB/s peak"
+    elif sad_frac >= 0.5:
+        bound, limiter = "valu", "SAD instructions (v_qsad / v_sad) at >= half of their measured roof"
+    else:
+        bound = "issue"
+        limiter = ("issue / latency: neither HBM (dram.frac " + (f"{dram_frac:.2f}" if dram_frac is not None else "n/a")
+                   + f") nor the SAD units (valu_sad.frac {sad_frac:.2f}) are at half their roof; frac is the "
+                   "SURVEY.md 8(d) algorithmic-bytes rate")
+    chip_gbps = bps * count * P / (ms_per_step * 1e-3) / 1e9  # this rank's algorithmic bytes per step / step time
 
     band = None
     if args.band_steps > 0:
@@ -492,7 +509,7 @@ def main():
             "upload": upload,
             "sb_ref_per_s": round(value * R, 1),
             "algorithmic_hbm_gbps": round(bps * value / 1e9, 1),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "roofline": {"bound": bound, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel": "ME pass: " + " -> ".join(n for k, n in enumerate(names) if stage_ms[k] > 0) +
                                    " (one launch each, back to back on the library stream)",
@@ -507,8 +524,11 @@ def main():
                          "valu_sad": valu_sad,
                          "algorithmic_frac": round(achieved / HBM_PEAK_GBPS, 4),
                          "dram": dram,
-                         "limiter": "issue / latency: neither HBM (dram.frac) nor the SAD units (valu_sad.frac) "
-                                    "are saturated; frac is the SURVEY.md 8(d) algorithmic-bytes rate"},
+                         "chip": {"gbps": round(chip_gbps, 1), "frac": round(chip_gbps / HBM_PEAK_GBPS, 4),
+                                  "note": "algorithmic bytes of one step / ms_per_step: the chip-level rate of the "
+                                          "timed steps, whose launches overlap on the two lanes (frac above is one "
+                                          "lane's launch alone, a lower bound on chip use)"},
+                         "limiter": limiter},
             "band_8k": band,
             "cpu_baseline": cpu_baseline,
             "parity_vs_cpu": parity,

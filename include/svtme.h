@@ -213,6 +213,49 @@ typedef struct svtme_sb_result {
     uint8_t pad2[6];
 } svtme_sb_result;
 
+/* The last 24 bytes of svtme_ref_record: the per-reference state an encoder
+ * keeps after the SB (search_results[l][r], zz_sad[l][r], me_context.h:459). */
+typedef struct svtme_record_tail {
+    uint64_t hme_sad;
+    int16_t hme_sc_x;
+    int16_t hme_sc_y;
+    uint32_t zz_sad;
+    uint8_t searched;
+    uint8_t do_ref;
+    uint8_t tf_early_exit;
+    uint8_t pad[5];
+} svtme_record_tail;
+
+/* Packed host output of svtme_submit_picture_packed_async: per SB, only what the
+ * encoder's consumer reads, sized by its MeSbResults allocation (pcs.c:91-117),
+ * so the device-to-host copy carries no unused candidate slots. SB k of the job
+ * starts at byte k * svtme_packed_sb_bytes(layout, R):
+ *   R records: svtme_ref_record (full_records = 1) or svtme_record_tail (0)
+ *   when sb_results = 1:
+ *     uint32 me_8x8_cost_variance, rc_me_distortion, me_64x64_distortion,
+ *            me_32x32_distortion, me_16x16_distortion, me_8x8_distortion
+ *     uint32 me_distortion[85]
+ *     uint32 me_mv_array[n_pus][max_refs]
+ *     uint8  stationary_block_present, rc_me_allow_gm, 0, 0
+ *     uint8  total_me_candidate_index[n_pus]
+ *     uint8  me_candidate_array[n_pus][max_cand]
+ *   zero bytes up to the next multiple of 16. */
+typedef struct svtme_pack_layout {
+    uint16_t n_pus;       /* PUs with candidates: 85, 21 (no 8x8) or 5 (no 16x16) */
+    uint8_t max_cand;     /* pa_me_data->max_cand, 1 .. SVTME_MAX_PA_ME_CAND */
+    uint8_t max_refs;     /* pa_me_data->max_refs, 1 .. SVTME_MAX_PA_ME_MV */
+    uint8_t full_records; /* 1: whole records (TF-ME reads the 85-PU winners), 0: tails */
+    uint8_t sb_results;   /* 1: the SB-result fields (PA-ME) */
+    uint8_t pad[2];
+} svtme_pack_layout;
+
+static inline uint32_t svtme_packed_sb_bytes(const svtme_pack_layout *L, uint32_t R) {
+    uint32_t b = R * (L->full_records ? (uint32_t)sizeof(svtme_ref_record) : (uint32_t)sizeof(svtme_record_tail));
+    if (L->sb_results)
+        b += 4u * (6u + SVTME_PU_COUNT) + 4u * L->n_pus * L->max_refs + 4u + L->n_pus * (1u + L->max_cand);
+    return (b + 15u) & ~15u;
+}
+
 /* ---------------------------------------------------------------------------
  * Picture-level job API (the performance boundary)
  * ------------------------------------------------------------------------- */
@@ -300,6 +343,25 @@ svtme_status svtme_submit_batch_device_lane(svtme_ctx *ctx, uint32_t lane, const
                                             svtme_sb_result *const *d_sb_results);
 /* The hipStream_t of a lane (created on first use), NULL on a bad lane. */
 void *svtme_lane_stream(svtme_ctx *ctx, uint32_t lane);
+
+/* Asynchronous job with packed HOST output, for an encoder's ME threads (the
+ * reference runs several pictures' ME at once, me_process.c:97-104). The job
+ * runs on lane `lane` into device buffers the context keeps per ticket, is
+ * packed on the device (svtme_pack_layout) and copied into host_out
+ * (sb_count x svtme_packed_sb_bytes(layout, R) bytes) on the context's download
+ * stream, overlapping later jobs. Returns at once with *ticket. host_out should
+ * be page-locked (svtme_host_alloc): a pageable destination makes the copy
+ * synchronous. At most SVTME_MAX_TICKETS tickets are outstanding; a submission
+ * beyond that is refused. */
+#define SVTME_MAX_TICKETS 16
+svtme_status svtme_submit_picture_packed_async(svtme_ctx *ctx, uint32_t lane, const svtme_job *job,
+                                               const svtme_pack_layout *layout, void *host_out, uint64_t *ticket);
+/* Block until ticket's packed output is in host memory, then retire the ticket.
+ * Safe to call from any thread, without holding anything the submitter holds. */
+svtme_status svtme_ticket_wait(svtme_ctx *ctx, uint64_t ticket);
+/* Page-locked host memory for packed outputs (NULL on failure), and its release. */
+void *svtme_host_alloc(uint64_t bytes);
+void svtme_host_free(void *p);
 /* Kernel timing with HIP events on the context's stream, recorded around every
  * stage launch of every submission while enabled (enable = 1). svtme_timing_read
  * waits for the recorded launch groups and returns the milliseconds of stage 0

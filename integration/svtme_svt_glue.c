@@ -17,7 +17,13 @@
  *                                  3169) runs ONE job over every SB of the
  *                                  picture; every call then scatters its SB's
  *                                  results exactly where the reference function
- *                                  leaves them. Pictures are uploaded on first
+ *                                  leaves them. Jobs are asynchronous: the
+ *                                  thread that starts one submits it on the next
+ *                                  submission lane and waits for its packed
+ *                                  output outside every glue lock, so the ME
+ *                                  threads of several pictures keep several
+ *                                  jobs in flight (uploads, searches and copies
+ *                                  overlap). Pictures are uploaded on first
  *                                  use and re-uploaded after the encoder rebuilds
  *                                  their 1/4 and 1/16 planes
  *                                  (svtme_picture_changed). Pictures the job API
@@ -45,14 +51,19 @@
  * Environment (read once): SVTME_DEVICE (HIP device, default 0);
  * SVTME_GLUE_STRICT=1 aborts instead of falling back; SVTME_GLUE_VERIFY=1
  * compares every uploaded pyramid with the encoder's own planes;
- * SVTME_GLUE_STATS=<file> appends the counters at exit; SVTME_GLUE_RESIDENT
- * caps the resident pictures (default 64).
+ * SVTME_GLUE_STATS=<file> appends the counters at exit (jobs, SBs, uploads,
+ * timing: upload / submit / wait milliseconds, mean job latency, the busy time
+ * with a job in flight and served_sb_per_s = SBs of the jobs / busy time; and
+ * the rtcd check: how many of the pointers parity mode replaces changed since
+ * the first SB call, and how many point at this file's HIP wrappers);
+ * SVTME_GLUE_RESIDENT caps the resident pictures (default 64).
  */
 #include <pthread.h>
 #include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "aom_dsp_rtcd.h"
 #include "mcomp.h"
@@ -73,8 +84,8 @@ void svtme_job_from_pcs(svtme_job *job, const PictureParentControlSet *pcs, cons
 void svtme_job_from_tf(svtme_job *job, const PictureParentControlSet *centre, const MeContext *me,
                        const EbPictureBufferDesc *input_ptr);
 void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_index, uint32_t b64_origin_x,
-                      uint32_t b64_origin_y, const svtme_job *job, const svtme_ref_record *recs,
-                      const svtme_sb_result *s);
+                      uint32_t b64_origin_y, const svtme_job *job, const svtme_pack_layout *layout,
+                      const uint8_t *packed_sb);
 
 #ifdef SVTME_GLUE_WRAP
 EbErrorType __real_svt_aom_motion_estimation_b64(PictureParentControlSet *, uint32_t, uint32_t, uint32_t,
@@ -197,6 +208,24 @@ static void glue_pme(const struct svt_mv_cost_param *p, uint8_t *src, uint32_t s
                    step, mvx, mvy);
 }
 
+/* the rtcd pointers parity mode replaces (aom_dsp_rtcd.h:779, 841-856, 863, 868) */
+#define GLUE_RTCD_N 10
+static void rtcd_snapshot(void *out[GLUE_RTCD_N]) {
+    out[0] = (void *)svt_sad_loop_kernel;
+    out[1] = (void *)svt_nxm_sad_kernel;
+    out[2] = (void *)svt_ext_sad_calculation_8x8_16x16;
+    out[3] = (void *)svt_ext_sad_calculation_32x32_64x64;
+    out[4] = (void *)svt_ext_all_sad_calculation_8x8_16x16;
+    out[5] = (void *)svt_ext_eight_sad_calculation_32x32_64x64;
+    out[6] = (void *)svt_initialize_buffer_32bits;
+    out[7] = (void *)downsample_2d;
+    out[8] = (void *)sad_16b_kernel;
+    out[9] = (void *)svt_pme_sad_loop_kernel;
+}
+/* the HIP wrappers parity mode registered (NULL until it runs): the exit stats
+ * count the pointers that hold them */
+static void *g_hip_wrappers[GLUE_RTCD_N];
+
 /* Parity / debug only: call right after svt_aom_setup_rtcd_internal(); the
  * pointers it set become the fallbacks, the HIP variants the active ones. Never
  * call it in picture-job mode: every rtcd call would become a GPU round trip. */
@@ -222,6 +251,7 @@ void svt_aom_setup_rtcd_hip_parity(void) {
     downsample_2d                             = glue_downsample;              /* :841 */
     sad_16b_kernel                            = glue_sad16b;                  /* :863 */
     svt_pme_sad_loop_kernel                   = glue_pme;                     /* :868 */
+    rtcd_snapshot(g_hip_wrappers);
 }
 
 /* ==========================================================================
@@ -358,11 +388,32 @@ void svtme_job_from_tf(svtme_job *job, const PictureParentControlSet *centre, co
 
 /* ==========================================================================
  * Outputs of one SB back into the reference's storage, exactly where
- * svt_aom_motion_estimation_b64 leaves them
+ * svt_aom_motion_estimation_b64 leaves them, from the SB's packed bytes
+ * (svtme_pack_layout, include/svtme.h)
  * ======================================================================== */
+/* The pack layout a job's consumer reads: TF-ME takes whole records (the 85-PU
+ * winners of its reference, temporal_filtering.c:1867-1869, 2232-2233); PA-ME
+ * takes the record tails and the SB results sized by its MeSbResults
+ * allocation (pcs.c:91-117; 85, 21 without 8x8, 5 without 16x16 PUs, the
+ * use_me_pu rule of motion_estimation.c:2561-2563). */
+static svtme_pack_layout layout_of(const PictureParentControlSet *pcs, const svtme_job *job) {
+    svtme_pack_layout L;
+    memset(&L, 0, sizeof(L));
+    if (job->me_type == SVTME_ME_MCTF) {
+        L.full_records = 1;
+        return L;
+    }
+    L.n_pus      = (uint16_t)(pcs->enable_me_16x16
+                                  ? (pcs->enable_me_8x8 ? pcs->max_number_of_pus_per_sb : MAX_SB64_PU_COUNT_NO_8X8)
+                                  : MAX_SB64_PU_COUNT_WO_16X16);
+    L.max_cand   = pcs->pa_me_data->max_cand;
+    L.max_refs   = pcs->pa_me_data->max_refs;
+    L.sb_results = 1;
+    return L;
+}
+
 void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_index, uint32_t b64_origin_x,
-                      uint32_t b64_origin_y, const svtme_job *job, const svtme_ref_record *recs,
-                      const svtme_sb_result *s) {
+                      uint32_t b64_origin_y, const svtme_job *job, const svtme_pack_layout *L, const uint8_t *p) {
     /* :3093-3100 */
     me->b64_width  = (job->width - b64_origin_x) < 64 ? job->width - b64_origin_x : 64;
     me->b64_height = (job->height - b64_origin_y) < 64 ? job->height - b64_origin_y : 64;
@@ -378,20 +429,26 @@ void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_
             me->reduce_me_sr_divisor[l][r]  = 1;
             me->zz_sad[l][r]                = (uint32_t)~0;
         }
-    /* per-reference state after the SB (search_results, me_context.h:459; the
-     * integer-search winners p_sb_best_* and the p_best_* views of the last
-     * searched reference, :1368-1384, which TF reads) */
-    const svtme_ref_record *rec = recs;
+    /* per-reference state after the SB (search_results, me_context.h:459); with
+     * whole records also the integer-search winners p_sb_best_* and the p_best_*
+     * views of the last searched reference (:1368-1384), which TF reads. PA-ME's
+     * consumer reads only MeSbResults and the PCS arrays below (me_process.c:
+     * 266-290), so its jobs carry the record tails alone. */
+    const uint32_t rsz = L->full_records ? (uint32_t)sizeof(svtme_ref_record) : (uint32_t)sizeof(svtme_record_tail);
+    const uint8_t *rp  = p;
     for (int l = 0; l < job->num_lists; l++)
-        for (int r = 0; r < job->num_refs[l]; r++, rec++) {
+        for (int r = 0; r < job->num_refs[l]; r++, rp += rsz) {
+            svtme_record_tail t;
+            memcpy(&t, L->full_records ? rp + offsetof(svtme_ref_record, hme_sad) : rp, sizeof(t));
             SearchResults *sr = &me->search_results[l][r];
-            sr->hme_sc_x      = rec->hme_sc_x;
-            sr->hme_sc_y      = rec->hme_sc_y;
-            sr->hme_sad       = rec->hme_sad;
-            sr->do_ref        = rec->do_ref;
-            me->zz_sad[l][r]  = rec->zz_sad;
-            if (!rec->searched)
+            sr->hme_sc_x      = t.hme_sc_x;
+            sr->hme_sc_y      = t.hme_sc_y;
+            sr->hme_sad       = t.hme_sad;
+            sr->do_ref        = t.do_ref;
+            me->zz_sad[l][r]  = t.zz_sad;
+            if (!t.searched || !L->full_records)
                 continue; /* the reference leaves p_sb_best_sad untouched and p_sb_best_mv zero */
+            const svtme_ref_record *rec = (const svtme_ref_record *)rp;
             memcpy(me->p_sb_best_sad[l][r], rec->best_sad, sizeof(rec->best_sad));
             memcpy(me->p_sb_best_mv[l][r], rec->best_mv, sizeof(rec->best_mv));
             me->p_best_sad_64x64 = &me->p_sb_best_sad[l][r][ME_TIER_ZERO_PU_64x64];
@@ -404,47 +461,66 @@ void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_
             me->p_best_mv8x8     = &me->p_sb_best_mv[l][r][ME_TIER_ZERO_PU_8x8_0];
         }
     if (job->me_type == SVTME_ME_MCTF) {
-        if (recs[0].tf_early_exit) /* :3109-3112 */
+        svtme_record_tail t0;
+        memcpy(&t0, p + offsetof(svtme_ref_record, hme_sad), sizeof(t0));
+        if (t0.tf_early_exit) /* :3109-3112 */
             me->tf_use_pred_64x64_only_th = (uint8_t)~0;
         return;
     }
-    /* candidates (:2532-2835) into MeSbResults (me_sb_results.h:44), whose arrays
-     * hold only the PUs ME produces candidates for (pcs.c:108-117): 85, 21
-     * without 8x8, 5 without 16x16 (the use_me_pu rule, :2561-2563); the
+    /* the SB results, packed (svtme_pack_layout) */
+    uint32_t v[6];
+    memcpy(v, rp, sizeof(v));
+    rp += sizeof(v);
+    /* compute_distortion (:2964-3007) and perform_gm_detection (:2838-2961) */
+    memcpy(me->me_distortion, rp, sizeof(me->me_distortion));
+    rp += sizeof(me->me_distortion);
+    const uint8_t *mvs = rp;
+    rp += 4u * L->n_pus * L->max_refs;
+    const uint8_t stationary = rp[0], allow_gm = rp[1];
+    rp += 4;
+    const uint8_t *total = rp, *cand = rp + L->n_pus;
+    /* candidates (:2532-2835) into MeSbResults (me_sb_results.h:44); the
      * candidates past total_me_candidate_index are not written */
     MeSbResults *res  = pcs->pa_me_data->me_results[b64_index];
-    const uint32_t mc = pcs->pa_me_data->max_cand, mr = pcs->pa_me_data->max_refs;
-    const uint32_t n_pus = pcs->enable_me_16x16
-        ? (pcs->enable_me_8x8 ? pcs->max_number_of_pus_per_sb : MAX_SB64_PU_COUNT_NO_8X8)
-        : MAX_SB64_PU_COUNT_WO_16X16;
-    for (uint32_t pu = 0; pu < n_pus; pu++) {
-        const uint32_t n = s->total_me_candidate_index[pu] < mc ? s->total_me_candidate_index[pu] : mc;
-        res->total_me_candidate_index[pu] = s->total_me_candidate_index[pu];
-        memcpy(&res->me_candidate_array[pu * mc], s->me_candidate_array[pu], n);
-        for (uint32_t k = 0; k < mr; k++) res->me_mv_array[pu * mr + k].as_int = s->me_mv_array[pu][k];
+    const uint32_t mc = L->max_cand, mr = L->max_refs;
+    for (uint32_t pu = 0; pu < L->n_pus; pu++) {
+        const uint32_t n = total[pu] < mc ? total[pu] : mc;
+        res->total_me_candidate_index[pu] = total[pu];
+        memcpy(&res->me_candidate_array[pu * mc], cand + pu * mc, n);
+        memcpy(&res->me_mv_array[pu * mr], mvs + 4u * pu * mr, 4u * mr);
     }
-    /* compute_distortion (:2964-3007) and perform_gm_detection (:2838-2961) */
-    memcpy(me->me_distortion, s->me_distortion, sizeof(me->me_distortion));
-    pcs->me_8x8_cost_variance[b64_index]        = s->me_8x8_cost_variance;
-    pcs->rc_me_distortion[b64_index]            = s->rc_me_distortion;
-    pcs->me_64x64_distortion[b64_index]         = s->me_64x64_distortion;
-    pcs->me_32x32_distortion[b64_index]         = s->me_32x32_distortion;
-    pcs->me_16x16_distortion[b64_index]         = s->me_16x16_distortion;
-    pcs->me_8x8_distortion[b64_index]           = s->me_8x8_distortion;
-    pcs->stationary_block_present_sb[b64_index] = s->stationary_block_present;
-    pcs->rc_me_allow_gm[b64_index]              = s->rc_me_allow_gm;
+    pcs->me_8x8_cost_variance[b64_index]        = v[0];
+    pcs->rc_me_distortion[b64_index]            = v[1];
+    pcs->me_64x64_distortion[b64_index]         = v[2];
+    pcs->me_32x32_distortion[b64_index]         = v[3];
+    pcs->me_16x16_distortion[b64_index]         = v[4];
+    pcs->me_8x8_distortion[b64_index]           = v[5];
+    pcs->stationary_block_present_sb[b64_index] = stationary;
+    pcs->rc_me_allow_gm[b64_index]              = allow_gm;
 }
 
 /* ==========================================================================
  * Picture-job service of the SB function
+ *
+ * The encoder's ME threads take the SB segments of whichever pictures are ready
+ * (me_process.c:97-174, several pictures at once). The first SB call of a
+ * picture (or of a TF reference) makes its pictures resident (asynchronous
+ * uploads), submits ONE job over all of its SBs on the next submission lane and
+ * waits for the job's packed output outside every glue lock, so the threads of
+ * other pictures upload and submit meanwhile: several jobs are in flight, their
+ * uploads, searches and copies overlapping on the GPU's copy engines and CUs.
+ * Every other SB call of the picture waits for that job and scatters its SB.
  * ======================================================================== */
 typedef struct GlueJob {
     svtme_job job;
-    uint32_t n_sb, R;
-    svtme_ref_record *recs;
-    svtme_sb_result *sbr;
+    svtme_pack_layout layout;
+    uint32_t n_sb, R, stride;
+    uint8_t *packed;   /* page-locked host buffer (pool) */
+    size_t packed_cap;
     uint32_t served;
-    int state; /* 0 running, 1 done, -1 failed (its SBs run on the encoder's function) */
+    uint32_t users;    /* threads between finding the job and the end of their scatter */
+    int state;         /* 0 running, 1 done, -1 failed (its SBs run on the encoder's function) */
+    int stale;         /* a picture it reads was re-decimated after it ran: later calls start a new job */
     struct GlueJob *next;
 } GlueJob;
 
@@ -452,13 +528,25 @@ typedef struct GluePic {
     uint64_t pn;
     uint32_t w, h;
     uint64_t last_use;
+    int dirty; /* the encoder rebuilt its planes: the next job re-uploads it in place */
 } GluePic;
+
+typedef struct GlueBuf {
+    uint8_t *p;
+    size_t cap;
+} GlueBuf;
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 static struct {
     pthread_once_t once;
-    pthread_mutex_t mu;  /* job list, residency table, counters */
+    pthread_mutex_t mu;  /* job list, buffer pool, counters */
     pthread_cond_t cv;   /* a job finished */
-    pthread_mutex_t gpu; /* one thread drives the backend at a time */
+    pthread_mutex_t gpu; /* one thread uploads / submits at a time (not held while waiting) */
     svtme_ctx *ctx;
     int strict, verify, max_resident;
     const char *stats_path;
@@ -466,8 +554,16 @@ static struct {
     GluePic *pics;
     uint32_t n_pics, cap_pics;
     uint64_t tick;
+    uint32_t next_lane;
+    GlueBuf pool[2 * SVTME_MAX_TICKETS];
+    uint32_t n_pool;
+    void *rtcd0[GLUE_RTCD_N]; /* the rtcd pointers at the first SB call (after svt_aom_setup_rtcd_internal) */
+    uint32_t inflight;        /* jobs between their submission and their output in host memory */
+    double busy_t0;
     struct {
-        unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified;
+        unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
+        unsigned long long job_sbs, max_inflight;
+        double upload_s, submit_s, wait_s, job_s, busy_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER};
 
@@ -475,16 +571,32 @@ static void glue_stats_at_exit(void) {
     FILE *f = fopen(G.stats_path, "a");
     if (!f)
         return;
+    /* rtcd check: every pointer parity mode replaces, against its value at the first SB call,
+     * and how many point at this file's HIP wrappers */
+    void *rt[GLUE_RTCD_N];
+    rtcd_snapshot(rt);
+    int changed = 0;
+    for (int i = 0; i < GLUE_RTCD_N; i++) changed += G.rtcd0[i] != NULL && rt[i] != G.rtcd0[i];
+    int hip = 0;
+    for (int i = 0; i < GLUE_RTCD_N; i++) hip += g_hip_wrappers[i] != NULL && rt[i] == g_hip_wrappers[i];
+    const double rate = G.n.busy_s > 0 ? (double)G.n.job_sbs / G.n.busy_s : 0.0;
+    const unsigned long long jobs = G.n.pa_jobs + G.n.tf_jobs;
     fprintf(f,
             "{\"backend\": %d, \"pa_jobs\": %llu, \"tf_jobs\": %llu, \"sbs\": %llu, \"fallback_sbs\": %llu, "
-            "\"uploads\": %llu, \"invalidations\": %llu, \"evictions\": %llu, \"verified_planes\": %llu}\n",
+            "\"uploads\": %llu, \"invalidations\": %llu, \"evictions\": %llu, \"verified_planes\": %llu, "
+            "\"stale_jobs\": %llu, \"rtcd_checked\": %d, \"rtcd_changed\": %d, \"rtcd_hip\": %d, "
+            "\"job_sbs\": %llu, \"max_inflight\": %llu, \"upload_ms\": %.3f, \"submit_ms\": %.3f, \"wait_ms\": %.3f, "
+            "\"job_latency_ms\": %.4f, \"busy_ms\": %.3f, \"served_sb_per_s\": %.1f}\n",
             G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
-            G.n.evictions, G.n.verified);
+            G.n.evictions, G.n.verified, G.n.stale, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
+            G.n.max_inflight, 1e3 * G.n.upload_s, 1e3 * G.n.submit_s, 1e3 * G.n.wait_s,
+            jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate);
     fclose(f);
 }
 
 static void glue_init(void) {
     const char *e;
+    rtcd_snapshot(G.rtcd0);
     G.strict       = (e = getenv("SVTME_GLUE_STRICT")) && atoi(e);
     G.verify       = (e = getenv("SVTME_GLUE_VERIFY")) && atoi(e);
     G.max_resident = (e = getenv("SVTME_GLUE_RESIDENT")) ? atoi(e) : 64;
@@ -506,6 +618,33 @@ static void glue_fallback(const char *what) {
     fprintf(stderr, "svtme glue: %s (%s); the SB runs on the encoder's ME\n", what, svtme_last_error());
     if (G.strict)
         abort();
+}
+
+/* ---- page-locked output buffers (G.mu held) */
+static int buf_take(GlueJob *j, size_t need) {
+    int best = -1;
+    for (uint32_t i = 0; i < G.n_pool; i++)
+        if (G.pool[i].cap >= need && (best < 0 || G.pool[i].cap < G.pool[best].cap))
+            best = (int)i;
+    if (best >= 0) {
+        j->packed = G.pool[best].p, j->packed_cap = G.pool[best].cap;
+        G.pool[best] = G.pool[--G.n_pool];
+        return 0;
+    }
+    j->packed     = (uint8_t *)svtme_host_alloc(need);
+    j->packed_cap = need;
+    return j->packed ? 0 : -1;
+}
+
+static void buf_give(GlueJob *j) {
+    if (!j->packed)
+        return;
+    if (G.n_pool < sizeof(G.pool) / sizeof(G.pool[0])) {
+        G.pool[G.n_pool].p = j->packed, G.pool[G.n_pool].cap = j->packed_cap;
+        G.n_pool++;
+    } else
+        svtme_host_free(j->packed);
+    j->packed = NULL;
 }
 
 /* ---- residency (G.gpu held) */
@@ -537,11 +676,13 @@ static int verify_level(uint64_t pn, int level, const EbPictureBufferDesc *d) {
     return bad;
 }
 
-/* Make picture pn resident with the encoder's current planes of it. */
+/* Make picture pn resident with the encoder's current planes of it: an
+ * asynchronous upload (the library stages the rows, the pyramid is built on its
+ * upload stream, and the first job reading the picture waits for it on the GPU). */
 static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPictureBufferDesc *quarter,
                       const EbPictureBufferDesc *sixteenth, uint32_t w, uint32_t h, uint64_t pin[9], int npin) {
     GluePic *p = pic_find(pn);
-    if (p && p->w == w && p->h == h) {
+    if (p && p->w == w && p->h == h && !p->dirty) {
         p->last_use = ++G.tick;
         return 0;
     }
@@ -559,9 +700,11 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
             G.n.evictions++;
         }
     }
+    const double t0 = now_s();
     const uint8_t *y = full->buffer_y + (size_t)full->org_y * full->stride_y + full->org_x;
-    if (svtme_picture_upload(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
+    if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
         return -1;
+    G.n.upload_s += now_s() - t0;
     if (G.verify && (verify_level(pn, 0, full) || (quarter && verify_level(pn, 1, quarter)) ||
                      (sixteenth && verify_level(pn, 2, sixteenth)))) {
         fprintf(stderr, "svtme glue: picture %llu: the ME pyramid differs from the encoder's planes\n",
@@ -578,9 +721,30 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
         }
         p = &G.pics[G.n_pics++];
     }
-    p->pn = pn, p->w = w, p->h = h, p->last_use = ++G.tick;
+    p->pn = pn, p->w = w, p->h = h, p->last_use = ++G.tick, p->dirty = 0;
     G.n.uploads++;
     return 0;
+}
+
+static int job_names(const svtme_job *job, uint64_t pn) {
+    if (job->picture_number == pn)
+        return 1;
+    for (int l = 0; l < job->num_lists; l++)
+        for (int r = 0; r < job->num_refs[l]; r++)
+            if (job->ref_picture_number[l][r] == pn)
+                return 1;
+    return 0;
+}
+
+static void job_free(GlueJob *j) { /* G.mu held, j already unlinked */
+    buf_give(j);
+    free(j);
+}
+
+static void job_unlink(GlueJob *j) { /* G.mu held */
+    GlueJob **pp = &G.jobs;
+    while (*pp != j) pp = &(*pp)->next;
+    *pp = j->next;
 }
 
 /* The encoder rebuilt a picture's 1/4 and 1/16 planes from its (possibly
@@ -588,27 +752,41 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
  * pad_and_decimate_filtered_pic (temporal_filtering.c:3895-3931), or picture
  * decision (pd_process.c:2720-2739). Jobs read it again from the new planes;
  * jobs already computed read the old ones, as the encoder's SB calls made
- * before the rebuild did. */
+ * before the rebuild did, and are no longer matched by later calls. */
 void svtme_picture_changed(PictureParentControlSet *pcs) {
     pthread_once(&G.once, glue_init);
     if (!G.ctx)
         return;
+    /* the resident planes stay until the next job re-uploads the picture in place
+     * (svtme_picture_upload_async orders that after the jobs still reading them) */
     pthread_mutex_lock(&G.gpu);
     GluePic *p = pic_find(pcs->picture_number);
-    if (p) {
-        svtme_picture_release(G.ctx, p->pn);
-        *p = G.pics[--G.n_pics];
+    if (p && !p->dirty) {
+        p->dirty = 1;
         G.n.invalidations++;
     }
     pthread_mutex_unlock(&G.gpu);
+    pthread_mutex_lock(&G.mu);
+    for (GlueJob *j = G.jobs, *nx; j; j = nx) {
+        nx = j->next;
+        if (j->stale || !job_names(&j->job, pcs->picture_number))
+            continue;
+        j->stale = 1;
+        G.n.stale++;
+        if (j->users == 0 && j->state != 0) {
+            job_unlink(j);
+            job_free(j);
+        }
+    }
+    pthread_mutex_unlock(&G.mu);
 }
 
 static EbPaReferenceObject *pa_object(const PictureParentControlSet *pcs) {
     return (EbPaReferenceObject *)pcs->pa_ref_pic_wrapper->object_ptr;
 }
 
-/* run one job (G.gpu held): make its pictures resident, submit, keep the results */
-static int run_job(GlueJob *j, const PictureParentControlSet *pcs, const MeContext *me) {
+/* make the job's pictures resident and submit it (G.gpu held); *ticket on success */
+static int submit_job(GlueJob *j, const PictureParentControlSet *pcs, const MeContext *me, uint64_t *ticket) {
     const svtme_job *job = &j->job;
     uint64_t pin[9];
     int npin = 0;
@@ -626,17 +804,11 @@ static int run_job(GlueJob *j, const PictureParentControlSet *pcs, const MeConte
                            job->width, job->height, pin, npin))
                 return -1;
         }
-    j->recs = (svtme_ref_record *)malloc((size_t)j->n_sb * j->R * sizeof(svtme_ref_record));
-    j->sbr  = job->me_type == SVTME_ME_MCTF ? NULL : (svtme_sb_result *)malloc((size_t)j->n_sb * sizeof(svtme_sb_result));
-    if (!j->recs || (job->me_type != SVTME_ME_MCTF && !j->sbr))
-        return -1;
-    return svtme_submit_picture(G.ctx, job, j->recs, j->sbr) == SVTME_OK ? 0 : -1;
-}
-
-static void job_free(GlueJob *j) {
-    free(j->recs);
-    free(j->sbr);
-    free(j);
+    const double t0 = now_s();
+    const svtme_status st =
+        svtme_submit_picture_packed_async(G.ctx, G.next_lane++ % SVTME_LANES, job, &j->layout, j->packed, ticket);
+    G.n.submit_s += now_s() - t0;
+    return st == SVTME_OK ? 0 : -1;
 }
 
 EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
@@ -659,31 +831,55 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
     /* find or start the picture's job (one per picture, or per TF reference) */
     pthread_mutex_lock(&G.mu);
     GlueJob *j = G.jobs;
-    while (j && memcmp(&j->job, &job, sizeof(job)) != 0) j = j->next;
-    if (!j) {
+    while (j && (j->stale || memcmp(&j->job, &job, sizeof(job)) != 0)) j = j->next;
+    if (j) {
+        j->users++;
+        while (j->state == 0) pthread_cond_wait(&G.cv, &G.mu);
+    } else {
         j = (GlueJob *)calloc(1, sizeof(GlueJob));
         if (!j)
             abort();
-        j->job  = job;
-        j->n_sb = svtme_sb_total(job.width, job.height);
-        j->R    = svtme_job_ref_slots(&job);
-        j->next = G.jobs;
-        G.jobs  = j;
+        j->job    = job;
+        j->layout = layout_of(pcs, &job);
+        j->n_sb   = svtme_sb_total(job.width, job.height);
+        j->R      = svtme_job_ref_slots(&job);
+        j->stride = svtme_packed_sb_bytes(&j->layout, j->R);
+        j->users  = 1;
+        j->next   = G.jobs;
+        G.jobs    = j;
         if (job.me_type == SVTME_ME_MCTF)
             G.n.tf_jobs++;
         else
             G.n.pa_jobs++;
+        int rc = buf_take(j, (size_t)j->n_sb * j->stride);
+        const double t_start = now_s();
+        if (G.inflight++ == 0)
+            G.busy_t0 = t_start;
+        if (G.inflight > G.n.max_inflight)
+            G.n.max_inflight = G.inflight;
         pthread_mutex_unlock(&G.mu);
-        pthread_mutex_lock(&G.gpu);
-        const int rc = run_job(j, pcs, me_ctx);
-        pthread_mutex_unlock(&G.gpu);
+        uint64_t ticket = 0;
+        if (!rc) {
+            pthread_mutex_lock(&G.gpu);
+            rc = submit_job(j, pcs, me_ctx, &ticket);
+            pthread_mutex_unlock(&G.gpu);
+        }
+        double t_wait = now_s();
+        if (!rc) /* no glue lock held: other pictures' threads upload and submit meanwhile */
+            rc = svtme_ticket_wait(G.ctx, ticket) == SVTME_OK ? 0 : -1;
+        const double t_done = now_s();
         pthread_mutex_lock(&G.mu);
+        G.n.wait_s += t_done - t_wait;
+        G.n.job_s += t_done - t_start;
+        if (--G.inflight == 0)
+            G.n.busy_s += t_done - G.busy_t0;
+        if (!rc)
+            G.n.job_sbs += j->n_sb;
         j->state = rc ? -1 : 1;
         if (rc)
             glue_fallback("picture job failed");
         pthread_cond_broadcast(&G.cv);
     }
-    while (j->state == 0) pthread_cond_wait(&G.cv, &G.mu);
     const int ok = j->state == 1 && b64_index < j->n_sb;
     if (ok)
         G.n.sbs++;
@@ -693,17 +889,16 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
 
     EbErrorType ret = EB_ErrorNone;
     if (ok)
-        svtme_scatter_sb(pcs, me_ctx, b64_index, b64_origin_x, b64_origin_y, &j->job,
-                         &j->recs[(size_t)b64_index * j->R], j->sbr ? &j->sbr[b64_index] : NULL);
+        svtme_scatter_sb(pcs, me_ctx, b64_index, b64_origin_x, b64_origin_y, &j->job, &j->layout,
+                         j->packed + (size_t)b64_index * j->stride);
     else
         ret = SVTME_ENCODER_ME_B64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
 
-    /* the job is dropped once every SB of the picture has been served */
+    /* the job is dropped once every SB of the picture has been served (or it went stale) */
     pthread_mutex_lock(&G.mu);
-    if (++j->served == j->n_sb) {
-        GlueJob **pp = &G.jobs;
-        while (*pp != j) pp = &(*pp)->next;
-        *pp = j->next;
+    j->served++;
+    if (--j->users == 0 && (j->served >= j->n_sb || j->stale)) {
+        job_unlink(j);
         job_free(j);
     }
     pthread_mutex_unlock(&G.mu);

@@ -204,3 +204,78 @@ svtme_status svtme_submit_picture(svtme_ctx *c, const svtme_job *job, svtme_ref_
     pthread_mutex_unlock(&c->mu);
     return st;
 }
+
+/* ---- asynchronous forms, run synchronously here (the glue's fast path) ---- */
+svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, const uint8_t *y, uint32_t stride, uint32_t width,
+                                        uint32_t height) {
+    return svtme_picture_upload(c, pn, y, stride, width, height);
+}
+
+void *svtme_host_alloc(uint64_t bytes) { return malloc(bytes ? (size_t)bytes : 1); }
+void svtme_host_free(void *p) { free(p); }
+
+/* the packed layout of include/svtme.h (svtme_pack_layout), as svtme_pack.hip writes it */
+static void pack_sb(const svtme_ref_record *rec, const svtme_sb_result *s, uint32_t R, const svtme_pack_layout *L,
+                    uint8_t *o) {
+    const uint32_t stride = svtme_packed_sb_bytes(L, R);
+    uint8_t *p = o;
+    memset(o, 0, stride);
+    for (uint32_t r = 0; r < R; r++) {
+        if (L->full_records) {
+            memcpy(p, &rec[r], sizeof(svtme_ref_record));
+            p += sizeof(svtme_ref_record);
+        } else {
+            memcpy(p, &rec[r].hme_sad, sizeof(svtme_record_tail));
+            p += sizeof(svtme_record_tail);
+        }
+    }
+    if (!L->sb_results)
+        return;
+    const uint32_t v[6] = {s->me_8x8_cost_variance, s->rc_me_distortion, s->me_64x64_distortion,
+                           s->me_32x32_distortion, s->me_16x16_distortion, s->me_8x8_distortion};
+    memcpy(p, v, sizeof(v));
+    p += sizeof(v);
+    memcpy(p, s->me_distortion, sizeof(s->me_distortion));
+    p += sizeof(s->me_distortion);
+    for (uint32_t pu = 0; pu < L->n_pus; pu++) {
+        memcpy(p, s->me_mv_array[pu], 4u * L->max_refs);
+        p += 4u * L->max_refs;
+    }
+    p[0] = s->stationary_block_present;
+    p[1] = s->rc_me_allow_gm;
+    p += 4;
+    memcpy(p, s->total_me_candidate_index, L->n_pus);
+    p += L->n_pus;
+    for (uint32_t pu = 0; pu < L->n_pus; pu++) {
+        memcpy(p, s->me_candidate_array[pu], L->max_cand);
+        p += L->max_cand;
+    }
+}
+
+svtme_status svtme_submit_picture_packed_async(svtme_ctx *c, uint32_t lane, const svtme_job *job,
+                                               const svtme_pack_layout *L, void *host_out, uint64_t *ticket) {
+    (void)lane;
+    if (!c || !job || !L || !host_out || !ticket)
+        return ora_fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_picture_packed_async: null argument");
+    const uint32_t total = svtme_sb_total(job->width, job->height);
+    const uint32_t count = job->sb_count ? job->sb_count : total - job->sb_begin;
+    const uint32_t R     = svtme_job_ref_slots(job);
+    svtme_ref_record *recs = (svtme_ref_record *)malloc((size_t)count * R * sizeof(svtme_ref_record));
+    svtme_sb_result *sbr   = L->sb_results ? (svtme_sb_result *)malloc((size_t)count * sizeof(svtme_sb_result)) : NULL;
+    svtme_status st        = (!recs || (L->sb_results && !sbr))
+        ? ora_fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "out of memory")
+        : svtme_submit_picture(c, job, recs, sbr);
+    if (!st) {
+        const uint32_t stride = svtme_packed_sb_bytes(L, R);
+        for (uint32_t k = 0; k < count; k++)
+            pack_sb(recs + (size_t)k * R, sbr ? sbr + k : NULL, R, L, (uint8_t *)host_out + (size_t)k * stride);
+        *ticket = 1;
+    }
+    free(recs);
+    free(sbr);
+    return st;
+}
+
+svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
+    return c && ticket ? SVTME_OK : ora_fail(SVTME_ERR_BAD_PARAMETER, "svtme_ticket_wait: bad arguments");
+}

@@ -1,0 +1,43 @@
+"""The ME rate the encoder gets through the glue (integration/svtme_svt_glue.c):
+whole encodes with svtav1enc_gpu (SVTME_GLUE_STRICT, no pyramid verification,
+which would download every pyramid), their bitstreams checked against the
+unmodified reference encoder, and the glue's exit stats: served_sb_per_s = SBs
+of the GPU jobs / the wall time with at least one job in flight (upload,
+search and the packed copy back included), mean job latency, jobs in flight.
+
+usage: python scripts/glue_rate.py OUT.json [case ...]   (default: 4k_p8_16f 4k_p8 1080p_p8)
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
+
+import encoder_harness as E  # noqa: E402
+
+
+def main():
+    out = sys.argv[1]
+    cases = sys.argv[2:] or ["4k_p8_16f", "4k_p8", "1080p_p8"]
+    wd = os.path.join("/tmp", "svtme_glue_rate")
+    res = []
+    for case in cases:
+        ref = E.encode("ref", case, wd)
+        got = E.encode("gpu", case, wd, env_extra={"SVTME_GLUE_VERIFY": "0"})
+        g = got["glue"]
+        w, h, frames, preset = E.CASES[case][:4]
+        r = {"case": case, "size": f"{w}x{h}", "frames": frames, "preset": preset,
+             "identical": got["md5"] == ref["md5"], "md5": got["md5"], "ref_seconds": ref["seconds"],
+             "gpu_encoder_seconds": got["seconds"], **g}
+        print(json.dumps(r), flush=True)
+        res.append(r)
+        if not r["identical"]:
+            raise SystemExit(f"{case}: bitstream differs from the reference encoder")
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,12 @@
+# round 4: the asynchronous glue (packed outputs, tickets, lanes) and the cleanup on the GPU:
+# smoke + the whole -m gpu suite, the glue-served ME rate of whole encodes, the default bench line
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r04b; mkdir -p $O
+export TMPDIR=/tmp
+bash scripts/gpu_tests.sh > $O/gpu_tests_summary.txt 2>&1; rc=$?
+cp gpurun_out/gpu_tests.log gpurun_out/smoke.log $O/ 2>/dev/null
+tail -6 $O/gpu_tests_summary.txt; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 scripts/glue_rate.py $O/glue_rate.json > $O/glue_rate.log 2>&1 || { tail -20 $O/glue_rate.log; exit 1; }
+cat $O/glue_rate.log
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $O/bench_default.json 2> $O/bench_default.err || { tail -20 $O/bench_default.err; exit 1; }
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('default', d['value'], d['roofline']['frac'], d['roofline']['bound'], d['roofline']['chip'], d['upload'])" $O/bench_default.json

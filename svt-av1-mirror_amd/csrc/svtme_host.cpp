@@ -28,6 +28,8 @@
 extern "C" hipError_t svtme_launch_build_full(const void *src, uint32_t src_stride, int w, int h, int ten_bit,
                                               DevPlane dst, int left, int top, int rows, hipStream_t s);
 extern "C" hipError_t svtme_launch_copy_words(const void *src, void *dst, uint32_t nwords, hipStream_t s);
+extern "C" hipError_t svtme_launch_pack(const svtme_ref_record *d_recs, const svtme_sb_result *d_sb, uint32_t n_sb,
+                                        uint32_t R, const svtme_pack_layout *L, void *d_out, hipStream_t s);
 extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int left, int top, int rows,
                                               hipStream_t s);
 extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
@@ -107,6 +109,18 @@ struct Lane {
     size_t cslot_cap           = 0;
 };
 
+// An outstanding packed host-output job (svtme_submit_picture_packed_async):
+// its device outputs stay allocated with the ticket slot and are reused by the
+// next job that takes the slot after svtme_ticket_wait retired it.
+struct Ticket {
+    uint64_t id = 0;               // 0: the slot is free
+    bool waiting = false;          // a thread is blocked on `done`
+    hipEvent_t launched = nullptr; // end of the job's launches on its lane
+    hipEvent_t done = nullptr;     // end of the copy into host memory (download stream)
+    void *d_mem = nullptr;         // records | SB results | packed bytes
+    size_t d_cap = 0;
+};
+
 struct svtme_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -143,6 +157,9 @@ struct svtme_ctx {
     uint32_t t_dropped = 0;
     Lane lanes[SVTME_LANES]; // lanes[0].s == stream
     uint32_t paths = 0;      // SVTME_PATH_* (svtme_set_paths; the environment at creation)
+    Ticket tickets[SVTME_MAX_TICKETS];
+    uint64_t ticket_seq = 0;
+    hipStream_t dstream = nullptr; // packed outputs to host memory, created on first use
     std::mutex mu;
 };
 
@@ -222,6 +239,18 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
     for (int k = 0; k < svtme_ctx::kRing; k++)
         if (c->ring_copied[k])
             (void)hipEventDestroy(c->ring_copied[k]);
+    if (c->dstream)
+        (void)hipStreamSynchronize(c->dstream);
+    for (auto &t : c->tickets) {
+        if (t.d_mem)
+            (void)hipFree(t.d_mem);
+        if (t.launched)
+            (void)hipEventDestroy(t.launched);
+        if (t.done)
+            (void)hipEventDestroy(t.done);
+    }
+    if (c->dstream)
+        (void)hipStreamDestroy(c->dstream);
     if (c->d_table)
         (void)hipFree(c->d_table);
     if (c->h_table)
@@ -794,6 +823,103 @@ extern "C" svtme_status svtme_submit_batch_device_lane(svtme_ctx *c, uint32_t la
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_batch_device_lane: null ctx, jobs or outputs");
     std::lock_guard<std::mutex> lk(c->mu);
     return submit_batch_locked(c, jobs, n, d_recs, d_sb, d_sb != nullptr, lane);
+}
+
+// ----------------------------------------------------------------------------
+// packed host output, asynchronous (tickets)
+// ----------------------------------------------------------------------------
+extern "C" void *svtme_host_alloc(uint64_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes ? (size_t)bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        svtme_set_error_internal("svtme_host_alloc: hipHostMalloc failed");
+        return nullptr;
+    }
+    return p;
+}
+
+extern "C" void svtme_host_free(void *p) {
+    if (p)
+        (void)hipHostFree(p);
+}
+
+extern "C" svtme_status svtme_submit_picture_packed_async(svtme_ctx *c, uint32_t lane, const svtme_job *job,
+                                                          const svtme_pack_layout *L, void *host_out,
+                                                          uint64_t *ticket) {
+    if (!c || !job || !L || !host_out || !ticket)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_picture_packed_async: null argument");
+    if (L->sb_results && (L->n_pus == 0 || L->n_pus > SVTME_PU_COUNT || L->max_cand == 0 ||
+                          L->max_cand > SVTME_MAX_PA_ME_CAND || L->max_refs == 0 || L->max_refs > SVTME_MAX_PA_ME_MV))
+        return fail(SVTME_ERR_BAD_PARAMETER, "pack layout: %u PUs, %u candidates, %u MVs", L->n_pus, L->max_cand,
+                    L->max_refs);
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    Ticket *t = nullptr;
+    for (auto &x : c->tickets)
+        if (!x.id) {
+            t = &x;
+            break;
+        }
+    if (!t)
+        return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "%d packed jobs outstanding (svtme_ticket_wait retires them)",
+                    SVTME_MAX_TICKETS);
+    if (!c->dstream)
+        HIP_TRY(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
+    if (!t->done) {
+        HIP_TRY(hipEventCreateWithFlags(&t->launched, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&t->done, hipEventDisableTiming));
+    }
+    const uint32_t total = svtme_sb_total(job->width, job->height);
+    const uint32_t count = job->sb_count ? job->sb_count : (job->sb_begin < total ? total - job->sb_begin : 0);
+    const uint32_t R     = svtme_job_ref_slots(job);
+    const size_t rb      = (size_t)count * R * sizeof(svtme_ref_record);
+    const size_t sbb     = L->sb_results ? (size_t)count * sizeof(svtme_sb_result) : 0;
+    const size_t stride = svtme_packed_sb_bytes(L, R), pb = (size_t)count * stride;
+    const size_t o_sb = (rb + 255) & ~(size_t)255, o_pk = (o_sb + sbb + 255) & ~(size_t)255;
+    svtme_status st;
+    if ((st = ensure_buf(&t->d_mem, &t->d_cap, o_pk + pb))) // the slot is free: nothing reads the old buffer
+        return st;
+    svtme_ref_record *d_recs = (svtme_ref_record *)t->d_mem;
+    svtme_sb_result *d_sb    = L->sb_results ? (svtme_sb_result *)((uint8_t *)t->d_mem + o_sb) : nullptr;
+    void *d_pack             = (uint8_t *)t->d_mem + o_pk;
+    if ((st = submit_batch_locked(c, job, 1, &d_recs, &d_sb, d_sb != nullptr, lane)))
+        return st;
+    hipStream_t ls = c->lanes[lane].s;
+    HIP_TRY(svtme_launch_pack(d_recs, d_sb, count, R, L, d_pack, ls));
+    HIP_TRY(hipEventRecord(t->launched, ls));
+    HIP_TRY(hipStreamWaitEvent(c->dstream, t->launched, 0));
+    HIP_TRY(hipMemcpyAsync(host_out, d_pack, pb, hipMemcpyDeviceToHost, c->dstream));
+    HIP_TRY(hipEventRecord(t->done, c->dstream));
+    t->id   = ++c->ticket_seq;
+    *ticket = t->id;
+    return SVTME_OK;
+}
+
+extern "C" svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
+    if (!c || !ticket)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_ticket_wait: null ctx or ticket");
+    hipEvent_t done = nullptr;
+    Ticket *t       = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        for (auto &x : c->tickets)
+            if (x.id == ticket && !x.waiting) {
+                t = &x;
+                break;
+            }
+        if (!t)
+            return fail(SVTME_ERR_BAD_PARAMETER, "svtme_ticket_wait: ticket %llu is not outstanding",
+                        (unsigned long long)ticket);
+        t->waiting = true;
+        done       = t->done;
+    }
+    HIP_TRY(hipSetDevice(c->device));
+    const hipError_t e = hipEventSynchronize(done); // without the context lock: other threads submit meanwhile
+    std::lock_guard<std::mutex> lk(c->mu);
+    t->waiting = false;
+    t->id      = 0;
+    if (e != hipSuccess)
+        return fail(SVTME_ERR_UNDEFINED, "svtme_ticket_wait: %s", hipGetErrorString(e));
+    return SVTME_OK;
 }
 
 extern "C" svtme_status svtme_set_timing(svtme_ctx *c, int enable) {

@@ -201,6 +201,52 @@ SB_RESULT_DTYPE = np.dtype(
 )
 
 
+class PackLayout(C.Structure):
+    """svtme_pack_layout (include/svtme.h): the packed host output of a job."""
+    _fields_ = [("n_pus", C.c_uint16), ("max_cand", C.c_uint8), ("max_refs", C.c_uint8),
+                ("full_records", C.c_uint8), ("sb_results", C.c_uint8), ("pad", C.c_uint8 * 2)]
+
+
+TAIL_BYTES = 24  # svtme_record_tail: the last 24 bytes of svtme_ref_record
+
+
+def packed_sb_bytes(L: PackLayout, R: int) -> int:
+    """svtme_packed_sb_bytes (include/svtme.h)."""
+    b = R * (REF_RECORD_DTYPE.itemsize if L.full_records else TAIL_BYTES)
+    if L.sb_results:
+        b += 4 * (6 + PU_COUNT) + 4 * L.n_pus * L.max_refs + 4 + L.n_pus * (1 + L.max_cand)
+    return (b + 15) & ~15
+
+
+def pack_outputs(recs: np.ndarray, sbr, L: PackLayout) -> bytes:
+    """The packed bytes of a job's outputs (records [n_sb][R], SB results [n_sb]),
+    restated in numpy from the layout include/svtme.h documents."""
+    n_sb, R = recs.shape
+    stride = packed_sb_bytes(L, R)
+    out = bytearray(n_sb * stride)
+    raw = recs.tobytes()
+    rs = REF_RECORD_DTYPE.itemsize
+    for k in range(n_sb):
+        o = k * stride
+        for r in range(R):
+            rec = raw[(k * R + r) * rs:(k * R + r + 1) * rs]
+            part = rec if L.full_records else rec[rs - TAIL_BYTES:]
+            out[o:o + len(part)] = part
+            o += len(part)
+        if L.sb_results:
+            s = sbr[k]
+            v = np.array([s["me_8x8_cost_variance"], s["rc_me_distortion"], s["me_64x64_distortion"],
+                          s["me_32x32_distortion"], s["me_16x16_distortion"], s["me_8x8_distortion"]], "<u4")
+            for part in (v.tobytes(), s["me_distortion"].astype("<u4").tobytes(),
+                         np.ascontiguousarray(s["me_mv_array"][:L.n_pus, :L.max_refs]).astype("<u4").tobytes(),
+                         bytes([int(s["stationary_block_present"]), int(s["rc_me_allow_gm"]), 0, 0]),
+                         s["total_me_candidate_index"][:L.n_pus].tobytes(),
+                         np.ascontiguousarray(s["me_candidate_array"][:L.n_pus, :L.max_cand]).tobytes()):
+                out[o:o + len(part)] = part
+                o += len(part)
+    return bytes(out)
+
+
 def sb_total(width: int, height: int) -> int:
     return ((width + 63) // 64) * ((height + 63) // 64)
 
@@ -507,65 +553,85 @@ def product_lib_path() -> str:
 
 
 def load_product():
-    lib = _load(product_lib_path(), "HIP product library libsvtme.so")
+    return _job_api_protos(_load(product_lib_path(), "HIP product library libsvtme.so"))
+
+
+def load_oracle_job():
+    """oracle/liboraclejob.so: the job API over the CPU oracle (test infrastructure,
+    the encoder tests' backend); the entry points it implements get prototypes."""
+    return _job_api_protos(_load(os.path.join(REPO_DIR, "oracle", "liboraclejob.so"), "oracle job API"))
+
+
+def _proto(lib, name, attr, val):
+    if hasattr(lib, name):  # (the oracle job API implements a subset)
+        setattr(getattr(lib, name), attr, val)
+
+
+def _job_api_protos(lib):
     if not hasattr(lib, "_svtme_protos"):
         vp = C.c_void_p
-        lib.svtme_ctx_create.argtypes = [C.c_int, C.POINTER(vp)]
-        lib.svtme_ctx_create.restype = C.c_int32
-        lib.svtme_ctx_destroy.argtypes = [vp]
-        lib.svtme_ctx_destroy.restype = None
-        lib.svtme_picture_upload.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
-        lib.svtme_picture_upload.restype = C.c_int32
-        lib.svtme_picture_upload_10bit.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
-        lib.svtme_picture_upload_10bit.restype = C.c_int32
-        lib.svtme_picture_upload_async.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
-        lib.svtme_picture_upload_async.restype = C.c_int32
-        lib.svtme_picture_upload_device.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
-        lib.svtme_picture_upload_device.restype = C.c_int32
-        lib.svtme_picture_invalidate.argtypes = [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32]
-        lib.svtme_picture_invalidate.restype = C.c_int32
-        lib.svtme_picture_release.argtypes = [vp, C.c_uint64]
-        lib.svtme_picture_release.restype = C.c_int32
-        lib.svtme_picture_download.argtypes = [vp, C.c_uint64, C.c_int, vp, C.POINTER(C.c_uint32),
-                                               C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
-        lib.svtme_picture_download.restype = C.c_int32
-        lib.svtme_submit_picture.argtypes = [vp, C.POINTER(Job), vp, vp]
-        lib.svtme_submit_picture.restype = C.c_int32
-        lib.svtme_submit_picture_async.argtypes = [vp, C.POINTER(Job)]
-        lib.svtme_submit_picture_async.restype = C.c_int32
-        lib.svtme_sync.argtypes = [vp]
-        lib.svtme_sync.restype = C.c_int32
-        lib.svtme_fetch.argtypes = [vp, vp, vp]
-        lib.svtme_fetch.restype = C.c_int32
-        lib.svtme_submit_picture_device.argtypes = [vp, C.POINTER(Job), vp, vp]
-        lib.svtme_submit_picture_device.restype = C.c_int32
-        lib.svtme_set_paths.argtypes = [vp, C.c_uint32]
-        lib.svtme_set_paths.restype = C.c_int32
-        lib.svtme_set_timing.argtypes = [vp, C.c_int]
-        lib.svtme_set_timing.restype = C.c_int32
-        lib.svtme_timing_read.argtypes = [vp, C.POINTER(C.c_float)]
-        lib.svtme_timing_read.restype = C.c_uint32
-        lib.svtme_submit_batch_device.argtypes = [vp, C.POINTER(Job), C.c_uint32, C.POINTER(vp), C.POINTER(vp)]
-        lib.svtme_submit_batch_device.restype = C.c_int32
-        lib.svtme_submit_batch_device_lane.argtypes = [vp, C.c_uint32, C.POINTER(Job), C.c_uint32, C.POINTER(vp),
-                                                       C.POINTER(vp)]
-        lib.svtme_submit_batch_device_lane.restype = C.c_int32
-        lib.svtme_lane_stream.argtypes = [vp, C.c_uint32]
-        lib.svtme_lane_stream.restype = vp
-        lib.svtme_device_records.argtypes = [vp, C.POINTER(C.c_uint64)]
-        lib.svtme_device_records.restype = vp
-        lib.svtme_stream.argtypes = [vp]
-        lib.svtme_stream.restype = vp
-        lib.svtme_rtcd_failed.argtypes = []
-        lib.svtme_rtcd_failed.restype = C.c_int
-        lib.svtme_last_error.argtypes = []
-        lib.svtme_last_error.restype = C.c_char_p
-        lib.svtme_derive_controls.argtypes = [C.c_int] * 6 + [C.POINTER(Controls)]
-        lib.svtme_derive_controls.restype = None
-        lib.svtme_derive_controls_tf.argtypes = [C.c_int] * 4 + [C.POINTER(Controls)]
-        lib.svtme_derive_controls_tf.restype = None
-        lib.svtme_sb_total.argtypes = [C.c_uint32, C.c_uint32]
-        lib.svtme_sb_total.restype = C.c_uint32
+        _proto(lib, "svtme_ctx_create", "argtypes", [C.c_int, C.POINTER(vp)])
+        _proto(lib, "svtme_ctx_create", "restype", C.c_int32)
+        _proto(lib, "svtme_ctx_destroy", "argtypes", [vp])
+        _proto(lib, "svtme_ctx_destroy", "restype", None)
+        _proto(lib, "svtme_picture_upload", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
+        _proto(lib, "svtme_picture_upload", "restype", C.c_int32)
+        _proto(lib, "svtme_picture_upload_10bit", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
+        _proto(lib, "svtme_picture_upload_10bit", "restype", C.c_int32)
+        _proto(lib, "svtme_picture_upload_async", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
+        _proto(lib, "svtme_picture_upload_async", "restype", C.c_int32)
+        _proto(lib, "svtme_picture_upload_device", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
+        _proto(lib, "svtme_picture_upload_device", "restype", C.c_int32)
+        _proto(lib, "svtme_picture_invalidate", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
+        _proto(lib, "svtme_picture_invalidate", "restype", C.c_int32)
+        _proto(lib, "svtme_picture_release", "argtypes", [vp, C.c_uint64])
+        _proto(lib, "svtme_picture_release", "restype", C.c_int32)
+        _proto(lib, "svtme_picture_download", "argtypes", [vp, C.c_uint64, C.c_int, vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)])
+        _proto(lib, "svtme_picture_download", "restype", C.c_int32)
+        _proto(lib, "svtme_submit_picture", "argtypes", [vp, C.POINTER(Job), vp, vp])
+        _proto(lib, "svtme_submit_picture", "restype", C.c_int32)
+        _proto(lib, "svtme_submit_picture_async", "argtypes", [vp, C.POINTER(Job)])
+        _proto(lib, "svtme_submit_picture_async", "restype", C.c_int32)
+        _proto(lib, "svtme_sync", "argtypes", [vp])
+        _proto(lib, "svtme_sync", "restype", C.c_int32)
+        _proto(lib, "svtme_fetch", "argtypes", [vp, vp, vp])
+        _proto(lib, "svtme_fetch", "restype", C.c_int32)
+        _proto(lib, "svtme_submit_picture_device", "argtypes", [vp, C.POINTER(Job), vp, vp])
+        _proto(lib, "svtme_submit_picture_device", "restype", C.c_int32)
+        _proto(lib, "svtme_submit_picture_packed_async", "argtypes", [vp, C.c_uint32, C.POINTER(Job), C.POINTER(PackLayout), vp, C.POINTER(C.c_uint64)])
+        _proto(lib, "svtme_submit_picture_packed_async", "restype", C.c_int32)
+        _proto(lib, "svtme_ticket_wait", "argtypes", [vp, C.c_uint64])
+        _proto(lib, "svtme_ticket_wait", "restype", C.c_int32)
+        _proto(lib, "svtme_host_alloc", "argtypes", [C.c_uint64])
+        _proto(lib, "svtme_host_alloc", "restype", vp)
+        _proto(lib, "svtme_host_free", "argtypes", [vp])
+        _proto(lib, "svtme_host_free", "restype", None)
+        _proto(lib, "svtme_set_paths", "argtypes", [vp, C.c_uint32])
+        _proto(lib, "svtme_set_paths", "restype", C.c_int32)
+        _proto(lib, "svtme_set_timing", "argtypes", [vp, C.c_int])
+        _proto(lib, "svtme_set_timing", "restype", C.c_int32)
+        _proto(lib, "svtme_timing_read", "argtypes", [vp, C.POINTER(C.c_float)])
+        _proto(lib, "svtme_timing_read", "restype", C.c_uint32)
+        _proto(lib, "svtme_submit_batch_device", "argtypes", [vp, C.POINTER(Job), C.c_uint32, C.POINTER(vp), C.POINTER(vp)])
+        _proto(lib, "svtme_submit_batch_device", "restype", C.c_int32)
+        _proto(lib, "svtme_submit_batch_device_lane", "argtypes", [vp, C.c_uint32, C.POINTER(Job), C.c_uint32, C.POINTER(vp), C.POINTER(vp)])
+        _proto(lib, "svtme_submit_batch_device_lane", "restype", C.c_int32)
+        _proto(lib, "svtme_lane_stream", "argtypes", [vp, C.c_uint32])
+        _proto(lib, "svtme_lane_stream", "restype", vp)
+        _proto(lib, "svtme_device_records", "argtypes", [vp, C.POINTER(C.c_uint64)])
+        _proto(lib, "svtme_device_records", "restype", vp)
+        _proto(lib, "svtme_stream", "argtypes", [vp])
+        _proto(lib, "svtme_stream", "restype", vp)
+        _proto(lib, "svtme_rtcd_failed", "argtypes", [])
+        _proto(lib, "svtme_rtcd_failed", "restype", C.c_int)
+        _proto(lib, "svtme_last_error", "argtypes", [])
+        _proto(lib, "svtme_last_error", "restype", C.c_char_p)
+        _proto(lib, "svtme_derive_controls", "argtypes", [C.c_int] * 6 + [C.POINTER(Controls)])
+        _proto(lib, "svtme_derive_controls", "restype", None)
+        _proto(lib, "svtme_derive_controls_tf", "argtypes", [C.c_int] * 4 + [C.POINTER(Controls)])
+        _proto(lib, "svtme_derive_controls_tf", "restype", None)
+        _proto(lib, "svtme_sb_total", "argtypes", [C.c_uint32, C.c_uint32])
+        _proto(lib, "svtme_sb_total", "restype", C.c_uint32)
         lib._svtme_protos = True
     return lib
 
@@ -573,8 +639,8 @@ def load_product():
 class GpuME:
     """The picture-level job API on one HIP device (no CPU fallback)."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load_product()
+    def __init__(self, device: int = 0, lib=None):
+        self.lib = lib or load_product()
         self.ctx = C.c_void_p()
         self._check(self.lib.svtme_ctx_create(device, C.byref(self.ctx)), "svtme_ctx_create")
 
@@ -655,6 +721,32 @@ class GpuME:
     def submit_device(self, job: Job, d_records: int, d_sb: int | None = None):
         self._check(self.lib.svtme_submit_picture_device(self.ctx, C.byref(job), d_records, d_sb),
                     "svtme_submit_picture_device")
+
+    def submit_packed(self, job: Job, layout: PackLayout, lane: int = 0, wait: bool = True):
+        """svtme_submit_picture_packed_async into a page-locked buffer (svtme_host_alloc);
+        returns (ticket, pointer, bytes), or the packed bytes when `wait`."""
+        total = sb_total(job.width, job.height)
+        count = job.sb_count if job.sb_count else total - job.sb_begin
+        nbytes = count * packed_sb_bytes(layout, ref_slots(job))
+        ptr = self.lib.svtme_host_alloc(nbytes)
+        if not ptr:
+            raise RuntimeError("svtme_host_alloc failed")
+        t = C.c_uint64()
+        st = self.lib.svtme_submit_picture_packed_async(self.ctx, lane, C.byref(job), C.byref(layout), ptr,
+                                                        C.byref(t))
+        if st != 0:
+            self.lib.svtme_host_free(ptr)
+            self._check(st, "svtme_submit_picture_packed_async")
+        if not wait:
+            return t.value, ptr, nbytes
+        return self.wait_packed(t.value, ptr, nbytes)
+
+    def wait_packed(self, ticket: int, ptr: int, nbytes: int) -> bytes:
+        try:
+            self._check(self.lib.svtme_ticket_wait(self.ctx, ticket), "svtme_ticket_wait")
+            return C.string_at(ptr, nbytes)
+        finally:
+            self.lib.svtme_host_free(ptr)
 
     def set_paths(self, paths: int):
         """Kernel-path selection (SVTME_PATH_* bits; 0 = every specialised kernel)."""

@@ -18,6 +18,7 @@ HEADER = os.path.join(ROOT, "include", "svtme.h")
 def declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"^static inline[^\n]*", "", text, flags=re.M)  # header-only helpers (svtme_packed_sb_bytes)
     names = set(re.findall(r"^\s*[A-Za-z_][\w \*]*?\b(svt\w+)\s*\(", text, flags=re.M))
     return sorted(names)
 

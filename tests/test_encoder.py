@@ -33,6 +33,15 @@ def test_bitstream_identical_oracle_backend(case, workdir):
     r = E.check(case, "ora", workdir)
     assert r["sbs"] > 0 and r["fallback_sbs"] == 0
     assert r["verified_planes"] == 3 * r["uploads"]
+    _no_rtcd_registered(r)
+
+
+def _no_rtcd_registered(r):
+    """Picture-job mode leaves every rtcd pointer to the encoder: the running
+    encoder's pointers (the ten parity mode would replace, aom_dsp_rtcd.h:779,
+    841-856, 863, 868) equal at exit what svt_aom_setup_rtcd_internal set before
+    the first SB call (aom_dsp_rtcd.c:188, 501-528), and none is a HIP wrapper."""
+    assert r["rtcd_checked"] == 10 and r["rtcd_changed"] == 0 and r["rtcd_hip"] == 0, r
 
 
 @pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
@@ -49,5 +58,8 @@ def test_tf_jobs_and_redecimation_exercised(workdir):
 def test_bitstream_identical_gpu(case, workdir):
     r = E.check(case, "gpu", workdir)
     assert r["backend"] == 1 and r["sbs"] > 0 and r["fallback_sbs"] == 0
+    _no_rtcd_registered(r)
     print(f"\n{case}: ref {r['ref_seconds']} s, GPU-ME encoder {r['glue_seconds']} s, {r['pa_jobs']} PA + "
-          f"{r['tf_jobs']} TF jobs, {r['sbs']} SBs, md5 {r['md5']}")
+          f"{r['tf_jobs']} TF jobs, {r['sbs']} SBs, served {r['served_sb_per_s'] / 1e6:.2f} M SB/s "
+          f"(busy {r['busy_ms']} ms, mean job {r['job_latency_ms']} ms, up to {r['max_inflight']} in flight), "
+          f"md5 {r['md5']}")
