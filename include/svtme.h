@@ -290,6 +290,16 @@ svtme_status svtme_picture_upload_async(svtme_ctx *ctx, uint64_t picture_number,
 /* Same, from a DEVICE pointer already in HBM (no PCIe). */
 svtme_status svtme_picture_upload_device(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *d_y,
                                          uint32_t stride, uint32_t width, uint32_t height);
+/* Asynchronous form of svtme_picture_upload_device (the input distribution of a
+ * picture split over GPUs, SURVEY.md 8(e): the plane arrives in HBM by an RCCL
+ * broadcast): the pyramid is built from d_y on the context's upload stream
+ * (svtme_upload_stream) and the first job reading the picture waits for it on
+ * the GPU. The caller makes the upload stream wait for d_y's producer before the
+ * call and keeps d_y unchanged until the work queued on that stream has run. */
+svtme_status svtme_picture_upload_device_async(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *d_y,
+                                               uint32_t stride, uint32_t width, uint32_t height);
+/* The hipStream_t of the asynchronous uploads (created on first use). */
+void *svtme_upload_stream(svtme_ctx *ctx);
 svtme_status svtme_picture_release(svtme_ctx *ctx, uint64_t picture_number);
 /* The resident picture's source planes were replaced (temporal filtering
  * re-decimates the filtered picture, temporal_filtering.c:3895-3931

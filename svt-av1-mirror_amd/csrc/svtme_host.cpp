@@ -421,16 +421,61 @@ static svtme_status upload_host(svtme_ctx *c, uint64_t pn, const void *y, uint32
 // first job that reads the picture waits for it on the job stream. Jobs
 // already queued that read an earlier version of the picture finish before
 // its planes are rewritten.
+static svtme_status ensure_ustream(svtme_ctx *c) {
+    if (!c->ustream) { // high priority: its small pyramid kernels go ahead of queued search workgroups
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, hi));
+    }
+    return SVTME_OK;
+}
+
+extern "C" void *svtme_upload_stream(svtme_ctx *c) {
+    if (!c)
+        return nullptr;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess || ensure_ustream(c))
+        return nullptr;
+    return (void *)c->ustream;
+}
+
+// Device-resident form of svtme_picture_upload_async: the pyramid is built from
+// d_y on the upload stream (the caller orders d_y's producer before it, e.g. an
+// RCCL broadcast of the plane, and keeps d_y until the build has run).
+extern "C" svtme_status svtme_picture_upload_device_async(svtme_ctx *c, uint64_t pn, const uint8_t *d_y,
+                                                          uint32_t stride, uint32_t w, uint32_t h) {
+    if (!c || !d_y || w == 0 || h == 0 || stride < w)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_upload_device_async: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    svtme_status st;
+    if ((st = ensure_ustream(c)))
+        return st;
+    const bool resident = c->pics.count(pn) != 0;
+    PicBuf *pb;
+    if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
+        return st;
+    if (resident && (st = after_readers(c, *pb, c->ustream))) // queued jobs may still read the old planes
+        return st;
+    if (!pb->ready)
+        HIP_TRY(hipEventCreateWithFlags(&pb->ready, hipEventDisableTiming));
+    if ((st = build_pyramid(c, pb, d_y, stride, w, h, 0, c->ustream)))
+        return st;
+    HIP_TRY(hipEventRecord(pb->ready, c->ustream));
+    pb->pending = (1u << SVTME_LANES) - 1u;
+    return SVTME_OK;
+}
+
 extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, const uint8_t *y, uint32_t stride,
                                                    uint32_t w, uint32_t h) {
     if (!c || !y || w == 0 || h == 0 || stride < w)
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_upload_async: bad arguments");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    if (!c->ustream) { // high priority: its small pyramid kernels go ahead of queued search workgroups
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(&c->ustream, hipStreamNonBlocking, hi));
+    {
+        const svtme_status us = ensure_ustream(c);
+        if (us)
+            return us;
     }
     const bool resident = c->pics.count(pn) != 0;
     PicBuf *pb;

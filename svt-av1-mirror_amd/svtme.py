@@ -582,6 +582,11 @@ def _job_api_protos(lib):
         _proto(lib, "svtme_picture_upload_async", "restype", C.c_int32)
         _proto(lib, "svtme_picture_upload_device", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
         _proto(lib, "svtme_picture_upload_device", "restype", C.c_int32)
+        _proto(lib, "svtme_picture_upload_device_async", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32,
+                                                                      C.c_uint32])
+        _proto(lib, "svtme_picture_upload_device_async", "restype", C.c_int32)
+        _proto(lib, "svtme_upload_stream", "argtypes", [vp])
+        _proto(lib, "svtme_upload_stream", "restype", vp)
         _proto(lib, "svtme_picture_invalidate", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
         _proto(lib, "svtme_picture_invalidate", "restype", C.c_int32)
         _proto(lib, "svtme_picture_release", "argtypes", [vp, C.c_uint64])
@@ -684,6 +689,14 @@ class GpuME:
     def upload_device(self, picture_number: int, dev_ptr: int, stride: int, w: int, h: int):
         self._check(self.lib.svtme_picture_upload_device(self.ctx, picture_number, dev_ptr, stride, w, h),
                     "svtme_picture_upload_device")
+
+    def upload_device_async(self, picture_number: int, dev_ptr: int, stride: int, w: int, h: int):
+        """svtme_picture_upload_device_async: the pyramid built on the upload stream."""
+        self._check(self.lib.svtme_picture_upload_device_async(self.ctx, picture_number, dev_ptr, stride, w, h),
+                    "svtme_picture_upload_device_async")
+
+    def upload_stream(self) -> int:
+        return self.lib.svtme_upload_stream(self.ctx) or 0
 
     def invalidate(self, picture_number: int, y: np.ndarray):
         """The resident picture's planes were replaced (TF re-decimation): rebuild."""

@@ -65,6 +65,21 @@ class BandSplit:
         return d_out[: self.picture_bytes]
 
 
+def broadcast_plane(plane, dist, src: int = 0, group=None, stream=None):
+    """SURVEY.md 8(e) input distribution: the current picture's 8-bit luma plane
+    (uint8 tensor) from rank `src` to every rank of the split, one broadcast
+    (RCCL over xGMI on GPUs, on `stream`; gloo in the CPU tests). Every rank
+    then builds the picture's pyramid from it (svtme_picture_upload_device_async)."""
+    import torch
+
+    if stream is not None:
+        with torch.cuda.stream(stream):
+            dist.broadcast(plane, src=src, group=group)
+    else:
+        dist.broadcast(plane, src=src, group=group)
+    return plane
+
+
 def gather_chunks_device(d_local, d_out, dist, group=None, stream=None):
     """All-gather the ranks' record chunks between device buffers.
 

@@ -195,3 +195,67 @@ def test_owner_exchange_equals_single_rank(svtme, tmp_path, world, k):
                                     nthreads=2)
         full = np.load(f"{out}.{p}.npy").view(S.REF_RECORD_DTYPE).reshape(ref.shape)
         assert not S.compare_records(ref, full)
+
+
+def _bcast_worker(rank, world, port, out_path, n_pics):
+    """bench.py's band_8k step on CPU: rank 0 holds the current picture's luma
+    plane, one broadcast (svtme_dist.broadcast_plane) gives it to every rank,
+    every rank builds the pyramid from what it received, searches its equal SB
+    chunk against its resident references and one all_gather_into_tensor
+    assembles the picture's records on every rank."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "svt-av1-mirror_amd"))
+    import torch
+    import torch.distributed as dist
+
+    import svtme as S
+    import svtme_dist as D
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w, h = 264, 200  # 5 x 4 = 20 SBs, ragged width and height
+    n_sb = S.sb_total(w, h)
+    R = 3
+    split = D.BandSplit(n_sb, R, S.REF_RECORD_DTYPE.itemsize, world, rank)
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    outs = []
+    for p in range(n_pics):
+        cur = 8 + 3 * p
+        frames = S.test_frames("pan", w, h, [cur - 1, cur - 2, cur, cur + 1])
+        refs = {(0, 0): S.build_host_pyramid(frames[cur - 1]), (0, 1): S.build_host_pyramid(frames[cur - 2]),
+                (1, 0): S.build_host_pyramid(frames[cur + 1])}  # resident: distributed with earlier pictures
+        plane = torch.from_numpy(frames[cur].copy()) if rank == 0 else torch.zeros((h, w), dtype=torch.uint8)
+        D.broadcast_plane(plane, dist, src=0)
+        local = torch.zeros(split.chunk_bytes, dtype=torch.uint8)
+        if split.count:
+            job = S.case_job(ctrl, w, h, cur, (cur - 1, cur - 2), (cur + 1,), 1, sb_begin=split.begin,
+                             sb_count=split.count)
+            recs, _ = S.run_checker(job, S.build_host_pyramid(plane.numpy()), refs, "oracle", nthreads=1,
+                                    with_sb_results=False)
+            local[: recs.nbytes] = torch.from_numpy(recs.view(np.uint8).reshape(-1).copy())
+        out = torch.empty(world * split.chunk_bytes, dtype=torch.uint8)
+        split.exchange(local, out, dist)
+        outs.append(split.picture(out).numpy().copy())
+    np.save(f"{out_path}.{rank}.npy", np.stack(outs))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_broadcast_chunked_search_allgather_equals_single_rank(svtme, tmp_path, world):
+    S = svtme
+    out = str(tmp_path / "bcast")
+    mp.spawn(_bcast_worker, args=(world, _free_port(), out, 2), nprocs=world, join=True)
+    w, h = 264, 200
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    for rank in range(world):  # every rank holds every picture's records
+        got = np.load(f"{out}.{rank}.npy")
+        for p in range(2):
+            cur = 8 + 3 * p
+            ref, _ = S.run_case_checker("pan", w, h, ctrl, cur, (cur - 1, cur - 2), (cur + 1,), 1, checker="oracle",
+                                        nthreads=2)
+            full = got[p].view(S.REF_RECORD_DTYPE).reshape(ref.shape)
+            assert not S.compare_records(ref, full)
