@@ -536,6 +536,13 @@ typedef struct GlueBuf {
     size_t cap;
 } GlueBuf;
 
+typedef struct GlueTrace { /* one job (SVTME_GLUE_TRACE) */
+    uint64_t pn;
+    int tf;
+    uint32_t n_sb, inflight;
+    double t_create, t_submitted, t_done;
+} GlueTrace;
+
 static double now_s(void) {
     struct timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -549,7 +556,10 @@ static struct {
     pthread_mutex_t gpu; /* one thread uploads / submits at a time (not held while waiting) */
     svtme_ctx *ctx;
     int strict, verify, max_resident;
-    const char *stats_path;
+    const char *stats_path, *trace_path;
+    GlueTrace *trace;
+    uint32_t n_trace, cap_trace;
+    double t0;
     GlueJob *jobs;
     GluePic *pics;
     uint32_t n_pics, cap_pics;
@@ -566,6 +576,20 @@ static struct {
         double upload_s, submit_s, wait_s, job_s, busy_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER};
+
+static void glue_trace_at_exit(void) {
+    FILE *f = fopen(G.trace_path, "w");
+    if (!f)
+        return;
+    for (uint32_t i = 0; i < G.n_trace; i++) {
+        const GlueTrace *t = &G.trace[i];
+        fprintf(f, "{\"pn\": %llu, \"tf\": %d, \"sbs\": %u, \"inflight\": %u, \"create_ms\": %.4f, "
+                   "\"submitted_ms\": %.4f, \"done_ms\": %.4f}\n",
+                (unsigned long long)t->pn, t->tf, t->n_sb, t->inflight, 1e3 * (t->t_create - G.t0),
+                1e3 * (t->t_submitted - G.t0), 1e3 * (t->t_done - G.t0));
+    }
+    fclose(f);
+}
 
 static void glue_stats_at_exit(void) {
     FILE *f = fopen(G.stats_path, "a");
@@ -605,6 +629,10 @@ static void glue_init(void) {
     G.stats_path = getenv("SVTME_GLUE_STATS");
     if (G.stats_path)
         atexit(glue_stats_at_exit);
+    G.trace_path = getenv("SVTME_GLUE_TRACE");
+    if (G.trace_path)
+        atexit(glue_trace_at_exit);
+    G.t0 = now_s();
     const int dev = (e = getenv("SVTME_DEVICE")) ? atoi(e) : 0;
     if (svtme_ctx_create(dev, &G.ctx) != SVTME_OK) {
         fprintf(stderr, "svtme glue: no ME device (%s); motion estimation runs on the CPU\n", svtme_last_error());
@@ -851,12 +879,13 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
             G.n.tf_jobs++;
         else
             G.n.pa_jobs++;
-        int rc = buf_take(j, (size_t)j->n_sb * j->stride);
         const double t_start = now_s();
+        int rc = buf_take(j, (size_t)j->n_sb * j->stride);
         if (G.inflight++ == 0)
             G.busy_t0 = t_start;
         if (G.inflight > G.n.max_inflight)
             G.n.max_inflight = G.inflight;
+        const uint32_t inflight = G.inflight;
         pthread_mutex_unlock(&G.mu);
         uint64_t ticket = 0;
         if (!rc) {
@@ -875,6 +904,17 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
             G.n.busy_s += t_done - G.busy_t0;
         if (!rc)
             G.n.job_sbs += j->n_sb;
+        if (G.trace_path) {
+            if (G.n_trace == G.cap_trace) {
+                G.cap_trace = G.cap_trace ? 2 * G.cap_trace : 256;
+                G.trace     = (GlueTrace *)realloc(G.trace, G.cap_trace * sizeof(GlueTrace));
+                if (!G.trace)
+                    abort();
+            }
+            const GlueTrace t = {job.picture_number, job.me_type == SVTME_ME_MCTF, j->n_sb, inflight, t_start, t_wait,
+                                 t_done};
+            G.trace[G.n_trace++] = t;
+        }
         j->state = rc ? -1 : 1;
         if (rc)
             glue_fallback("picture job failed");

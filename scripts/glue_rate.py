@@ -25,13 +25,20 @@ def main():
     res = []
     for case in cases:
         ref = E.encode("ref", case, wd)
-        got = E.encode("gpu", case, wd, env_extra={"SVTME_GLUE_VERIFY": "0"})
+        trace = os.path.join(wd, f"{case}.trace.jsonl")
+        got = E.encode("gpu", case, wd, env_extra={"SVTME_GLUE_VERIFY": "0", "SVTME_GLUE_TRACE": trace})
         g = got["glue"]
+        with open(trace) as fh:
+            jobs = [json.loads(line) for line in fh if line.strip()]
         w, h, frames, preset = E.CASES[case][:4]
         r = {"case": case, "size": f"{w}x{h}", "frames": frames, "preset": preset,
              "identical": got["md5"] == ref["md5"], "md5": got["md5"], "ref_seconds": ref["seconds"],
-             "gpu_encoder_seconds": got["seconds"], **g}
-        print(json.dumps(r), flush=True)
+             "gpu_encoder_seconds": got["seconds"], **g, "jobs": jobs}
+        lat = sorted(j["done_ms"] - j["create_ms"] for j in jobs)
+        print(json.dumps({k: v for k, v in r.items() if k != "jobs"}), flush=True)
+        print(f"  job latency ms: min {lat[0]:.3f} median {lat[len(lat) // 2]:.3f} max {lat[-1]:.3f}; "
+              f"submit part median {sorted(j['submitted_ms'] - j['create_ms'] for j in jobs)[len(jobs) // 2]:.3f}",
+              flush=True)
         res.append(r)
         if not r["identical"]:
             raise SystemExit(f"{case}: bitstream differs from the reference encoder")

@@ -35,6 +35,9 @@ extern "C" hipError_t svtme_launch_build_down(DevPlane prev, DevPlane dst, int l
 extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
                                           hipEvent_t *ev, uint32_t *mask);
 extern "C" uint32_t svtme_launch_key(const DevJob *dj);
+extern "C" hipError_t svtme_prime_pyramid(void);
+extern "C" hipError_t svtme_prime_pack(void);
+extern "C" hipError_t svtme_prime_stages(void);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_b_list(const svtme_job *job, uint8_t *list, uint32_t *count);
 extern "C" void svtme_stage_a1_list(const svtme_job *job, uint8_t *list, uint32_t *count);
@@ -187,6 +190,13 @@ extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
         return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "hipStreamCreate: %s", hipGetErrorString(e));
     }
     c->lanes[0].s = c->stream;
+    // the code objects of the kernels, loaded now rather than at a first job's launches
+    if ((e = svtme_prime_pyramid()) != hipSuccess || (e = svtme_prime_pack()) != hipSuccess ||
+        (e = svtme_prime_stages()) != hipSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return fail(SVTME_ERR_UNDEFINED, "svtme_ctx_create: loading the kernels: %s", hipGetErrorString(e));
+    }
     // kernel-path selection from the environment, read once (diagnostic A/B runs)
     static const struct {
         const char *var;
@@ -486,17 +496,17 @@ extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, co
         return st;
     if (!pb->ready)
         HIP_TRY(hipEventCreateWithFlags(&pb->ready, hipEventDisableTiming));
-    const size_t need = (size_t)w * h;
+    // one linear copy of the span from the first to the last sample (rows keep their
+    // stride; a padded encoder plane's margins ride along): a 2D copy out of
+    // pageable memory goes row by row
+    const size_t need = (size_t)(h - 1) * stride + w;
     if (c->ustaging_cap < need) { // only between uploads: nothing queued reads the old buffer
         HIP_TRY(hipStreamSynchronize(c->ustream));
         if ((st = ensure_buf(&c->ustaging, &c->ustaging_cap, need)))
             return st;
     }
-    if (stride == w)
-        HIP_TRY(hipMemcpyAsync(c->ustaging, y, need, hipMemcpyHostToDevice, c->ustream));
-    else
-        HIP_TRY(hipMemcpy2DAsync(c->ustaging, w, y, stride, w, h, hipMemcpyHostToDevice, c->ustream));
-    if ((st = build_pyramid(c, pb, c->ustaging, w, w, h, 0, c->ustream)))
+    HIP_TRY(hipMemcpyAsync(c->ustaging, y, need, hipMemcpyHostToDevice, c->ustream));
+    if ((st = build_pyramid(c, pb, c->ustaging, stride, w, h, 0, c->ustream)))
         return st;
     HIP_TRY(hipEventRecord(pb->ready, c->ustream));
     pb->pending = (1u << SVTME_LANES) - 1u;

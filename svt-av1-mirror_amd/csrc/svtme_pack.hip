@@ -76,3 +76,8 @@ extern "C" hipError_t svtme_launch_pack(const svtme_ref_record *d_recs, const sv
     hipLaunchKernelGGL(k_pack, dim3(n_sb), dim3(256), 0, s, d_recs, d_sb, R, *L, stride, (uint8_t *)d_out);
     return hipGetLastError();
 }
+
+extern "C" hipError_t svtme_prime_pack(void) { // (see svtme_prime_pyramid)
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_pack);
+}

@@ -96,3 +96,10 @@ extern "C" hipError_t svtme_launch_copy_words(const void *src, void *dst, uint32
     hipLaunchKernelGGL(k_copy_words, dim3(blocks), dim3(256), 0, s, (const uint32_t *)src, (uint32_t *)dst, nwords);
     return hipGetLastError();
 }
+
+// Load this translation unit's code object now (HIP loads it lazily at the first
+// launch of one of its kernels, which would otherwise land in a job's latency)
+extern "C" hipError_t svtme_prime_pyramid(void) {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_build_down);
+}

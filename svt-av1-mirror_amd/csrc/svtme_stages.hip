@@ -4476,6 +4476,11 @@ static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, ui
             hipLaunchKernelGGL(K, grid, dim3(256), 0, s, __VA_ARGS__);                                             \
     } while (0)
 
+extern "C" hipError_t svtme_prime_stages(void) { // (see svtme_prime_pyramid)
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)svtme::k_hme<true, true, true, false>);
+}
+
 extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
                                           hipEvent_t *ev, uint32_t *mask) {
     if (n == 0 || n > SVTME_MAX_BATCH)
