@@ -539,8 +539,8 @@ typedef struct GlueBuf {
 typedef struct GlueTrace { /* one job (SVTME_GLUE_TRACE) */
     uint64_t pn;
     int tf;
-    uint32_t n_sb, inflight;
-    double t_create, t_submitted, t_done;
+    uint32_t n_sb, inflight, uploads;
+    double t_create, t_submitted, t_done, upload_s;
 } GlueTrace;
 
 static double now_s(void) {
@@ -583,10 +583,10 @@ static void glue_trace_at_exit(void) {
         return;
     for (uint32_t i = 0; i < G.n_trace; i++) {
         const GlueTrace *t = &G.trace[i];
-        fprintf(f, "{\"pn\": %llu, \"tf\": %d, \"sbs\": %u, \"inflight\": %u, \"create_ms\": %.4f, "
-                   "\"submitted_ms\": %.4f, \"done_ms\": %.4f}\n",
-                (unsigned long long)t->pn, t->tf, t->n_sb, t->inflight, 1e3 * (t->t_create - G.t0),
-                1e3 * (t->t_submitted - G.t0), 1e3 * (t->t_done - G.t0));
+        fprintf(f, "{\"pn\": %llu, \"tf\": %d, \"sbs\": %u, \"inflight\": %u, \"uploads\": %u, "
+                   "\"upload_ms\": %.4f, \"create_ms\": %.4f, \"submitted_ms\": %.4f, \"done_ms\": %.4f}\n",
+                (unsigned long long)t->pn, t->tf, t->n_sb, t->inflight, t->uploads, 1e3 * t->upload_s,
+                1e3 * (t->t_create - G.t0), 1e3 * (t->t_submitted - G.t0), 1e3 * (t->t_done - G.t0));
     }
     fclose(f);
 }
@@ -888,9 +888,13 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
         const uint32_t inflight = G.inflight;
         pthread_mutex_unlock(&G.mu);
         uint64_t ticket = 0;
+        unsigned long long up_n = 0;
+        double up_s = 0;
         if (!rc) {
             pthread_mutex_lock(&G.gpu);
-            rc = submit_job(j, pcs, me_ctx, &ticket);
+            up_n = G.n.uploads, up_s = G.n.upload_s;
+            rc   = submit_job(j, pcs, me_ctx, &ticket);
+            up_n = G.n.uploads - up_n, up_s = G.n.upload_s - up_s;
             pthread_mutex_unlock(&G.gpu);
         }
         double t_wait = now_s();
@@ -911,8 +915,8 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
                 if (!G.trace)
                     abort();
             }
-            const GlueTrace t = {job.picture_number, job.me_type == SVTME_ME_MCTF, j->n_sb, inflight, t_start, t_wait,
-                                 t_done};
+            const GlueTrace t = {job.picture_number, job.me_type == SVTME_ME_MCTF, j->n_sb, inflight, (uint32_t)up_n,
+                                 t_start, t_wait, t_done, up_s};
             G.trace[G.n_trace++] = t;
         }
         j->state = rc ? -1 : 1;

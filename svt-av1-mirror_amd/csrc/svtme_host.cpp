@@ -174,6 +174,8 @@ extern "C" uint32_t svtme_job_ref_slots(const svtme_job *job) {
     return job->num_refs[0] + (job->num_lists == 2 ? job->num_refs[1] : 0);
 }
 
+static svtme_status prepare(svtme_ctx *c);
+
 extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
     if (!out)
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_ctx_create: null out");
@@ -208,6 +210,11 @@ extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
         if (const char *v = getenv(e.var))
             if (*v && strcmp(v, "0") != 0)
                 c->paths |= e.bit;
+    const svtme_status ps = prepare(c);
+    if (ps) {
+        svtme_ctx_destroy(c);
+        return ps;
+    }
     *out = c;
     return SVTME_OK;
 }
@@ -674,6 +681,23 @@ static svtme_status ensure_ring(svtme_ctx *c) {
     HIP_TRY(hipHostGetDevicePointer((void **)&c->h_table_dev, c->h_table, 0)); // read by k_copy_words
     for (int k = 0; k < svtme_ctx::kRing; k++)
         HIP_TRY(hipEventCreateWithFlags(&c->ring_copied[k], hipEventDisableTiming));
+    return SVTME_OK;
+}
+
+// The streams, events and job-table ring of a context, made at creation so
+// that no job's latency carries them
+static svtme_status prepare(svtme_ctx *c) {
+    svtme_status st;
+    for (uint32_t l = 0; l < SVTME_LANES; l++)
+        if ((st = ensure_lane(c, l)))
+            return st;
+    if ((st = ensure_ustream(c)) || (st = ensure_ring(c)))
+        return st;
+    HIP_TRY(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
+    for (auto &t : c->tickets) {
+        HIP_TRY(hipEventCreateWithFlags(&t.launched, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+    }
     return SVTME_OK;
 }
 
