@@ -659,6 +659,11 @@ static int buf_take(GlueJob *j, size_t need) {
         G.pool[best] = G.pool[--G.n_pool];
         return 0;
     }
+    /* a new buffer holds the largest output seen so far (rounded to 1 MB): the
+     * pool then serves every later job whatever its layout */
+    static size_t largest;
+    largest       = need > largest ? need : largest;
+    need          = (largest + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
     j->packed     = (uint8_t *)svtme_host_alloc(need);
     j->packed_cap = need;
     return j->packed ? 0 : -1;

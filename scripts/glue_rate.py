@@ -5,7 +5,7 @@ unmodified reference encoder, and the glue's exit stats: served_sb_per_s = SBs
 of the GPU jobs / the wall time with at least one job in flight (upload,
 search and the packed copy back included), mean job latency, jobs in flight.
 
-usage: python scripts/glue_rate.py OUT.json [case ...]   (default: 4k_p8_16f 4k_p8 1080p_p8)
+usage: python scripts/glue_rate.py OUT.json [case ...]   (default: 4k_p8_64f 4k_p8_16f 1080p_p8)
 """
 import json
 import os
@@ -20,7 +20,7 @@ import encoder_harness as E  # noqa: E402
 
 def main():
     out = sys.argv[1]
-    cases = sys.argv[2:] or ["4k_p8_16f", "4k_p8", "1080p_p8"]
+    cases = sys.argv[2:] or ["4k_p8_64f", "4k_p8_16f", "1080p_p8"]
     wd = os.path.join("/tmp", "svtme_glue_rate")
     res = []
     for case in cases:

@@ -52,6 +52,7 @@ CASES = {
     "4k_p8": (3840, 2160, 8, 8, False, [], True),
     # the glue-served ME rate of a longer 4K encode (several pictures' jobs in flight)
     "4k_p8_16f": (3840, 2160, 16, 8, False, [], True),
+    "4k_p8_64f": (3840, 2160, 64, 8, False, [], True),  # (scripts/glue_rate.py only)
     "4k10_p6": (3840, 2160, 4, 6, True, [], True),
     # low-delay prediction (real-time tune): reduce_hme_l0_sr_th at presets >= 8
     # (enc_mode_config.c:692-704); p10 also runs without pre-HME
