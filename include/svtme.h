@@ -372,6 +372,11 @@ svtme_status svtme_ticket_wait(svtme_ctx *ctx, uint64_t ticket);
 /* Page-locked host memory for packed outputs (NULL on failure), and its release. */
 void *svtme_host_alloc(uint64_t bytes);
 void svtme_host_free(void *p);
+/* Page-lock an existing host range (e.g. an encoder's picture buffer) so that
+ * svtme_picture_upload_async copies it by DMA without staging it through the
+ * CPU; svtme_host_unregister undoes it once the copies reading it have run. */
+svtme_status svtme_host_register(void *p, uint64_t bytes);
+svtme_status svtme_host_unregister(void *p);
 /* Kernel timing with HIP events on the context's stream, recorded around every
  * stage launch of every submission while enabled (enable = 1). svtme_timing_read
  * waits for the recorded launch groups and returns the milliseconds of stage 0

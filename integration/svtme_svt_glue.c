@@ -513,6 +513,8 @@ void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_
  * ======================================================================== */
 typedef struct GlueJob {
     svtme_job job;
+    void *pinned[9]; /* encoder buffers page-locked for this job's uploads */
+    int n_pinned;
     svtme_pack_layout layout;
     uint32_t n_sb, R, stride;
     uint8_t *packed;   /* page-locked host buffer (pool) */
@@ -572,7 +574,7 @@ static struct {
     double busy_t0;
     struct {
         unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
-        unsigned long long job_sbs, max_inflight;
+        unsigned long long job_sbs, max_inflight, unpinned;
         double upload_s, submit_s, wait_s, job_s, busy_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER};
@@ -608,11 +610,11 @@ static void glue_stats_at_exit(void) {
     fprintf(f,
             "{\"backend\": %d, \"pa_jobs\": %llu, \"tf_jobs\": %llu, \"sbs\": %llu, \"fallback_sbs\": %llu, "
             "\"uploads\": %llu, \"invalidations\": %llu, \"evictions\": %llu, \"verified_planes\": %llu, "
-            "\"stale_jobs\": %llu, \"rtcd_checked\": %d, \"rtcd_changed\": %d, \"rtcd_hip\": %d, "
+            "\"stale_jobs\": %llu, \"unpinned_uploads\": %llu, \"rtcd_checked\": %d, \"rtcd_changed\": %d, \"rtcd_hip\": %d, "
             "\"job_sbs\": %llu, \"max_inflight\": %llu, \"upload_ms\": %.3f, \"submit_ms\": %.3f, \"wait_ms\": %.3f, "
             "\"job_latency_ms\": %.4f, \"busy_ms\": %.3f, \"served_sb_per_s\": %.1f}\n",
             G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
-            G.n.evictions, G.n.verified, G.n.stale, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
+            G.n.evictions, G.n.verified, G.n.stale, G.n.unpinned, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
             G.n.max_inflight, 1e3 * G.n.upload_s, 1e3 * G.n.submit_s, 1e3 * G.n.wait_s,
             jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate);
     fclose(f);
@@ -712,7 +714,7 @@ static int verify_level(uint64_t pn, int level, const EbPictureBufferDesc *d) {
 /* Make picture pn resident with the encoder's current planes of it: an
  * asynchronous upload (the library stages the rows, the pyramid is built on its
  * upload stream, and the first job reading the picture waits for it on the GPU). */
-static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPictureBufferDesc *quarter,
+static int pic_ensure(GlueJob *j, uint64_t pn, const EbPictureBufferDesc *full, const EbPictureBufferDesc *quarter,
                       const EbPictureBufferDesc *sixteenth, uint32_t w, uint32_t h, uint64_t pin[9], int npin) {
     GluePic *p = pic_find(pn);
     if (p && p->w == w && p->h == h && !p->dirty) {
@@ -735,6 +737,13 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
     }
     const double t0 = now_s();
     const uint8_t *y = full->buffer_y + (size_t)full->org_y * full->stride_y + full->org_x;
+    /* the span the upload reads, page-locked for the job's duration: the copy is then
+     * one DMA with no staging pass through the CPU (busy with the encoder's threads) */
+    const uint64_t span = (uint64_t)(h - 1) * full->stride_y + w;
+    if (svtme_host_register((void *)y, span) == SVTME_OK)
+        j->pinned[j->n_pinned++] = (void *)y;
+    else
+        G.n.unpinned++;
     if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
         return -1;
     G.n.upload_s += now_s() - t0;
@@ -827,13 +836,13 @@ static int submit_job(GlueJob *j, const PictureParentControlSet *pcs, const MeCo
     for (int l = 0; l < job->num_lists; l++)
         for (int r = 0; r < job->num_refs[l]; r++) pin[npin++] = job->ref_picture_number[l][r];
     const EbPaReferenceObject *cur = pa_object(pcs);
-    if (pic_ensure(job->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
+    if (pic_ensure(j, job->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
                    cur->sixteenth_downsampled_picture_ptr, job->width, job->height, pin, npin))
         return -1;
     for (int l = 0; l < job->num_lists; l++)
         for (int r = 0; r < job->num_refs[l]; r++) {
             const EbDownScaledBufDescPtrArray *d = &me->me_ds_ref_array[l][r];
-            if (pic_ensure(d->picture_number, d->picture_ptr, d->quarter_picture_ptr, d->sixteenth_picture_ptr,
+            if (pic_ensure(j, d->picture_number, d->picture_ptr, d->quarter_picture_ptr, d->sixteenth_picture_ptr,
                            job->width, job->height, pin, npin))
                 return -1;
         }
@@ -905,6 +914,10 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
         double t_wait = now_s();
         if (!rc) /* no glue lock held: other pictures' threads upload and submit meanwhile */
             rc = svtme_ticket_wait(G.ctx, ticket) == SVTME_OK ? 0 : -1;
+        else if (j->n_pinned) /* the uploads this job queued have run before their pages unlock */
+            svtme_sync(G.ctx);
+        for (int k = 0; k < j->n_pinned; k++) svtme_host_unregister(j->pinned[k]);
+        j->n_pinned = 0;
         const double t_done = now_s();
         pthread_mutex_lock(&G.mu);
         G.n.wait_s += t_done - t_wait;

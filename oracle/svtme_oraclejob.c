@@ -213,6 +213,8 @@ svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, const uint8_t
 
 void *svtme_host_alloc(uint64_t bytes) { return malloc(bytes ? (size_t)bytes : 1); }
 void svtme_host_free(void *p) { free(p); }
+svtme_status svtme_host_register(void *p, uint64_t bytes) { return p && bytes ? SVTME_OK : SVTME_ERR_BAD_PARAMETER; }
+svtme_status svtme_host_unregister(void *p) { return p ? SVTME_OK : SVTME_ERR_BAD_PARAMETER; }
 
 /* the packed layout of include/svtme.h (svtme_pack_layout), as svtme_pack.hip writes it */
 static void pack_sb(const svtme_ref_record *rec, const svtme_sb_result *s, uint32_t R, const svtme_pack_layout *L,
@@ -275,6 +277,8 @@ svtme_status svtme_submit_picture_packed_async(svtme_ctx *c, uint32_t lane, cons
     free(sbr);
     return st;
 }
+
+svtme_status svtme_sync(svtme_ctx *c) { return c ? SVTME_OK : SVTME_ERR_BAD_PARAMETER; }
 
 svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
     return c && ticket ? SVTME_OK : ora_fail(SVTME_ERR_BAD_PARAMETER, "svtme_ticket_wait: bad arguments");

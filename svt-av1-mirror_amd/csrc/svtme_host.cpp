@@ -921,6 +921,20 @@ extern "C" void svtme_host_free(void *p) {
         (void)hipHostFree(p);
 }
 
+extern "C" svtme_status svtme_host_register(void *p, uint64_t bytes) {
+    if (!p || !bytes)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_host_register: bad arguments");
+    HIP_TRY(hipHostRegister(p, (size_t)bytes, hipHostRegisterDefault));
+    return SVTME_OK;
+}
+
+extern "C" svtme_status svtme_host_unregister(void *p) {
+    if (!p)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_host_unregister: null pointer");
+    HIP_TRY(hipHostUnregister(p));
+    return SVTME_OK;
+}
+
 extern "C" svtme_status svtme_submit_picture_packed_async(svtme_ctx *c, uint32_t lane, const svtme_job *job,
                                                           const svtme_pack_layout *L, void *host_out,
                                                           uint64_t *ticket) {
