@@ -140,11 +140,16 @@ def main():
     ap.add_argument("--band-steps", type=int, default=30,
                     help="steps of the band_8k sub-measurement (one 8K p8 picture split over the N GPUs, SURVEY.md "
                          "8(e)); 0 skips it")
+    ap.add_argument("--backend", default="nccl", choices=("nccl", "gloo"),
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; gloo: a rehearsal of the "
+                         "multi-rank code paths, e.g. several ranks on one GPU with --shared-device)")
+    ap.add_argument("--shared-device", action="store_true",
+                    help="every rank on HIP device 0 (rehearsal of the N > 1 path on a one-GPU box, with gloo)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_rank = 0 if args.shared_device else int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
 
@@ -153,7 +158,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
 
     import svtme as S
     import svtme_dist as D

@@ -78,6 +78,7 @@
 EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
                                         uint32_t b64_origin_y, MeContext *me_ctx, EbPictureBufferDesc *input_ptr);
 void svtme_picture_changed(PictureParentControlSet *pcs);
+void svtme_glue_release(void);
 void svt_aom_setup_rtcd_hip_parity(void);
 void svtme_controls_from_me_context(svtme_controls *c, const MeContext *m);
 void svtme_job_from_pcs(svtme_job *job, const PictureParentControlSet *pcs, const MeContext *me);
@@ -513,8 +514,6 @@ void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_
  * ======================================================================== */
 typedef struct GlueJob {
     svtme_job job;
-    void *pinned[9]; /* encoder buffers page-locked for this job's uploads */
-    int n_pinned;
     svtme_pack_layout layout;
     uint32_t n_sb, R, stride;
     uint8_t *packed;   /* page-locked host buffer (pool) */
@@ -537,6 +536,11 @@ typedef struct GlueBuf {
     uint8_t *p;
     size_t cap;
 } GlueBuf;
+
+typedef struct GlueReg { /* an encoder picture span page-locked for uploads */
+    const void *p;
+    uint64_t bytes;
+} GlueReg;
 
 typedef struct GlueTrace { /* one job (SVTME_GLUE_TRACE) */
     uint64_t pn;
@@ -569,6 +573,8 @@ static struct {
     uint32_t next_lane;
     GlueBuf pool[2 * SVTME_MAX_TICKETS];
     uint32_t n_pool;
+    GlueReg *regs; /* (G.gpu) */
+    uint32_t n_regs, cap_regs;
     void *rtcd0[GLUE_RTCD_N]; /* the rtcd pointers at the first SB call (after svt_aom_setup_rtcd_internal) */
     uint32_t inflight;        /* jobs between their submission and their output in host memory */
     double busy_t0;
@@ -714,7 +720,48 @@ static int verify_level(uint64_t pn, int level, const EbPictureBufferDesc *d) {
 /* Make picture pn resident with the encoder's current planes of it: an
  * asynchronous upload (the library stages the rows, the pyramid is built on its
  * upload stream, and the first job reading the picture waits for it on the GPU). */
-static int pic_ensure(GlueJob *j, uint64_t pn, const EbPictureBufferDesc *full, const EbPictureBufferDesc *quarter,
+/* Page-lock the span an upload reads, once per encoder buffer (G.gpu held): the
+ * encoder keeps its input picture buffers from svt_av1_enc_init to
+ * svt_av1_enc_deinit and recycles them, so a buffer is locked on its first
+ * upload and every later upload from it is one DMA with no staging pass through
+ * the CPU (busy with the encoder's threads). svtme_glue_release (called by the
+ * svt_av1_enc_deinit wrap) unlocks them all before the encoder frees them. */
+static void pin_span(const void *p, uint64_t bytes) {
+    for (uint32_t i = 0; i < G.n_regs; i++)
+        if (G.regs[i].p == p) {
+            if (G.regs[i].bytes >= bytes)
+                return;
+            svtme_sync(G.ctx); /* the uploads queued from the old span have run */
+            svtme_host_unregister((void *)p);
+            G.regs[i] = G.regs[--G.n_regs];
+            break;
+        }
+    if (G.n_regs == G.cap_regs) {
+        G.cap_regs = G.cap_regs ? 2 * G.cap_regs : 64;
+        G.regs     = (GlueReg *)realloc(G.regs, G.cap_regs * sizeof(GlueReg));
+        if (!G.regs)
+            abort();
+    }
+    if (svtme_host_register((void *)p, bytes) == SVTME_OK) {
+        G.regs[G.n_regs].p = p, G.regs[G.n_regs].bytes = bytes;
+        G.n_regs++;
+    } else
+        G.n.unpinned++;
+}
+
+/* Unlock every page-locked encoder buffer (after the uploads reading them have run) */
+void svtme_glue_release(void) {
+    if (!G.ctx)
+        return;
+    pthread_mutex_lock(&G.gpu);
+    if (G.n_regs)
+        svtme_sync(G.ctx);
+    for (uint32_t i = 0; i < G.n_regs; i++) svtme_host_unregister((void *)G.regs[i].p);
+    G.n_regs = 0;
+    pthread_mutex_unlock(&G.gpu);
+}
+
+static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPictureBufferDesc *quarter,
                       const EbPictureBufferDesc *sixteenth, uint32_t w, uint32_t h, uint64_t pin[9], int npin) {
     GluePic *p = pic_find(pn);
     if (p && p->w == w && p->h == h && !p->dirty) {
@@ -737,13 +784,7 @@ static int pic_ensure(GlueJob *j, uint64_t pn, const EbPictureBufferDesc *full, 
     }
     const double t0 = now_s();
     const uint8_t *y = full->buffer_y + (size_t)full->org_y * full->stride_y + full->org_x;
-    /* the span the upload reads, page-locked for the job's duration: the copy is then
-     * one DMA with no staging pass through the CPU (busy with the encoder's threads) */
-    const uint64_t span = (uint64_t)(h - 1) * full->stride_y + w;
-    if (svtme_host_register((void *)y, span) == SVTME_OK)
-        j->pinned[j->n_pinned++] = (void *)y;
-    else
-        G.n.unpinned++;
+    pin_span(y, (uint64_t)(h - 1) * full->stride_y + w);
     if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
         return -1;
     G.n.upload_s += now_s() - t0;
@@ -836,13 +877,13 @@ static int submit_job(GlueJob *j, const PictureParentControlSet *pcs, const MeCo
     for (int l = 0; l < job->num_lists; l++)
         for (int r = 0; r < job->num_refs[l]; r++) pin[npin++] = job->ref_picture_number[l][r];
     const EbPaReferenceObject *cur = pa_object(pcs);
-    if (pic_ensure(j, job->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
+    if (pic_ensure(job->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
                    cur->sixteenth_downsampled_picture_ptr, job->width, job->height, pin, npin))
         return -1;
     for (int l = 0; l < job->num_lists; l++)
         for (int r = 0; r < job->num_refs[l]; r++) {
             const EbDownScaledBufDescPtrArray *d = &me->me_ds_ref_array[l][r];
-            if (pic_ensure(j, d->picture_number, d->picture_ptr, d->quarter_picture_ptr, d->sixteenth_picture_ptr,
+            if (pic_ensure(d->picture_number, d->picture_ptr, d->quarter_picture_ptr, d->sixteenth_picture_ptr,
                            job->width, job->height, pin, npin))
                 return -1;
         }
@@ -914,10 +955,6 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
         double t_wait = now_s();
         if (!rc) /* no glue lock held: other pictures' threads upload and submit meanwhile */
             rc = svtme_ticket_wait(G.ctx, ticket) == SVTME_OK ? 0 : -1;
-        else if (j->n_pinned) /* the uploads this job queued have run before their pages unlock */
-            svtme_sync(G.ctx);
-        for (int k = 0; k < j->n_pinned; k++) svtme_host_unregister(j->pinned[k]);
-        j->n_pinned = 0;
         const double t_done = now_s();
         pthread_mutex_lock(&G.mu);
         G.n.wait_s += t_done - t_wait;
@@ -972,6 +1009,12 @@ EbErrorType __wrap_svt_aom_motion_estimation_b64(PictureParentControlSet *pcs, u
                                                  uint32_t b64_origin_x, uint32_t b64_origin_y, MeContext *me_ctx,
                                                  EbPictureBufferDesc *input_ptr) {
     return svtme_motion_estimation_b64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
+}
+
+EbErrorType __real_svt_av1_enc_deinit(EbComponentType *svt_enc_component);
+EbErrorType __wrap_svt_av1_enc_deinit(EbComponentType *svt_enc_component) {
+    svtme_glue_release(); /* before the encoder frees the buffers the glue page-locked */
+    return __real_svt_av1_enc_deinit(svt_enc_component);
 }
 
 void __wrap_svt_aom_downsample_filtering_input_picture(PictureParentControlSet *pcs, EbPictureBufferDesc *full,

@@ -69,7 +69,8 @@ liboraclejob.so: svtme_oraclejob.c svtme_oracle.c svtme_oracle_kernels.c svtme_o
 	$(CC) -O3 -fPIC -std=gnu11 -Wall -Wextra -Wno-unused-parameter -shared -o $@ svtme_oraclejob.c \
 	    svtme_oracle.c svtme_oracle_kernels.c -lpthread
 
-WRAP = -Wl,--wrap=svt_aom_motion_estimation_b64 -Wl,--wrap=svt_aom_downsample_filtering_input_picture
+WRAP = -Wl,--wrap=svt_aom_motion_estimation_b64 -Wl,--wrap=svt_aom_downsample_filtering_input_picture \
+       -Wl,--wrap=svt_av1_enc_deinit
 
 $(O)/svtav1enc_ora: $(APP_OBJ) $(O)/obj/glue.o $(O)/libsvtenc.a liboraclejob.so
 	$(CC) -o $@ $(APP_OBJ) $(O)/obj/glue.o $(O)/libsvtenc.a $(WRAP) -L. -loraclejob \

@@ -52,7 +52,8 @@ def test_glue_wrap_build_exports_wrappers(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     syms = subprocess.run(["nm", obj], capture_output=True, text=True).stdout
     for s in ("T __wrap_svt_aom_motion_estimation_b64", "T __wrap_svt_aom_downsample_filtering_input_picture",
-              "U __real_svt_aom_motion_estimation_b64", "U __real_svt_aom_downsample_filtering_input_picture"):
+              "U __real_svt_aom_motion_estimation_b64", "U __real_svt_aom_downsample_filtering_input_picture",
+              "T __wrap_svt_av1_enc_deinit", "U __real_svt_av1_enc_deinit"):
         assert s in syms, s
 
 
