@@ -1,0 +1,65 @@
+"""8K p8 search time (one picture per launch, lane 0) for different current
+pictures: (a) the resident picture uploaded from host memory, searched every
+step; (b) a copy built by svtme_picture_upload_device_async; (c) two such
+copies alternating step by step (what band_8k's pipelined step searches).
+Prints ms per search."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
+
+import torch  # noqa: E402
+
+import svtme as S  # noqa: E402
+import workloads as W  # noqa: E402
+
+
+def main():
+    name = "8k_p8"
+    wl = W.WORKLOADS[name]
+    Wd, Ht = wl["w"], wl["h"]
+    dev = torch.device("cuda", 0)
+    gpu = S.GpuME(0)
+    base = 800000
+    frames = W.workload_frames(name)
+    for t, f in frames.items():
+        gpu.upload(base + t, f)
+    n_sb = S.sb_total(Wd, Ht)
+    out = torch.zeros(n_sb * 4 * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    planes = [torch.from_numpy(frames[8].reshape(-1)).to(dev) for _ in range(2)]
+    for k, pn in enumerate((base + 900, base + 901)):
+        gpu.upload_device_async(pn, planes[k].data_ptr(), Wd, Wd, Ht)
+    gpu.sync()
+
+    def job(pn):
+        j = W.workload_job(name, base=base)
+        j.picture_number = pn
+        return j
+    ja, jb, jc = job(base + 8), job(base + 900), job(base + 901)
+
+    def timed(fn, n=30):
+        for i in range(3):
+            fn(i)
+        gpu.sync()
+        t0 = time.perf_counter()
+        for i in range(n):
+            fn(i)
+        gpu.sync()
+        return round((time.perf_counter() - t0) / n * 1e3, 4)
+
+    res = {
+        "resident_host_upload": timed(lambda i: gpu.submit_batch_device([ja], [out.data_ptr()], lane=0)),
+        "device_built": timed(lambda i: gpu.submit_batch_device([jb], [out.data_ptr()], lane=0)),
+        "device_built_alternating": timed(lambda i: gpu.submit_batch_device([jb if i & 1 else jc], [out.data_ptr()],
+                                                                             lane=0)),
+        "resident_host_upload_again": timed(lambda i: gpu.submit_batch_device([ja], [out.data_ptr()], lane=0)),
+    }
+    print(json.dumps(res), flush=True)
+    gpu.close()
+
+
+if __name__ == "__main__":
+    main()
