@@ -344,16 +344,19 @@ def main():
         # resident references on the next submission lane; 8 pictures rotate, so an
         # upload waits only for the search of the picture it replaces, 8 steps back
         # (scripts/upload_probe.py: 4 rotating pictures on one lane serialise more)
+        # (each rotating picture has its own resident references at the workload's distances:
+        # picture numbers set the reference distances, and so the search areas)
         NP = 8
-        pjobs = []
-        for k in range(NP):
-            pj = W.workload_job(name)
-            pj.picture_number = 910000 + k
-            pjobs.append(pj)
+        pbase = [910000 + 64 * k for k in range(NP)]
+        pjobs = [W.workload_job(name, base=b) for b in pbase]
+        for b in pbase:
+            for t in offs:
+                if t != 0:
+                    gpu.upload(b + 8 + t, W.workload_frame(name, syn, 8 + t))
         pbuf = [torch.zeros(n_sb * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device=dev) for _ in range(2)]
 
         def pipe(i):
-            gpu.upload_async(910000 + i % NP, pinned.data_ptr(), Wd, Ht)
+            gpu.upload_async(pbase[i % NP] + 8, pinned.data_ptr(), Wd, Ht)
             gpu.submit_batch_device([pjobs[i % NP]], [pbuf[i & 1].data_ptr()], lane=i & 1)
         for i in range(2 * NP):
             pipe(i)
@@ -367,11 +370,12 @@ def main():
         # the same loop with the uploads only (the copy engine's rate)
         t0p = time.perf_counter()
         for i in range(reps):
-            gpu.upload_async(910000 + i % NP, pinned.data_ptr(), Wd, Ht)
+            gpu.upload_async(pbase[i % NP] + 8, pinned.data_ptr(), Wd, Ht)
         gpu.sync()
         up_only_ms = (time.perf_counter() - t0p) / reps * 1e3
-        for k in range(NP):
-            gpu.release(910000 + k)
+        for b in pbase:
+            for t in offs:
+                gpu.release(b + 8 + t)
         upload = {"pageable_ms_per_picture": round(pageable_ms, 4), "pinned_ms_per_picture": round(pinned_ms, 4),
                   "picture_bytes": int(frame.nbytes),
                   "pcie_inclusive_sb_per_s": round(n_sb / ((pinned_ms + me_ms) * 1e-3), 1),
@@ -566,21 +570,20 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, steps, fence):
     name = "8k_p8"
     wl = W.WORKLOADS[name]
     Wd, Ht = wl["w"], wl["h"]
-    base = 800000
+    # two sets of resident references (the previous pictures); the current picture of step i is
+    # set i & 1's picture 8, so distributing the next one waits only for the search two steps
+    # back, and every job keeps the workload's reference distances
+    bases = [800000, 800064]
     frames = W.workload_frames(name)
-    for t, f in frames.items():  # every rank holds the full pyramids (pre-HME reaches ~1400 rows)
-        gpu.upload(base + t, f)
+    for b in bases:
+        for t, f in frames.items():  # every rank holds the full pyramids (pre-HME reaches ~1400 rows)
+            if t != 8:
+                gpu.upload(b + t, f)
     n_sb = S.sb_total(Wd, Ht)
     R = len(wl["l0"]) + len(wl["l1"])
     split = D.BandSplit(n_sb, R, S.REF_RECORD_DTYPE.itemsize, world, rank)
-    # the current picture alternates between two picture numbers, so distributing the next one
-    # waits only for the search two steps back
-    cur = [base + 900, base + 901]
-    jobs = []
-    for pn in cur:
-        j = W.workload_job(name, base=base, sb_begin=split.begin, sb_count=split.count)
-        j.picture_number = pn
-        jobs.append(j)
+    cur = [b + 8 for b in bases]
+    jobs = [W.workload_job(name, base=b, sb_begin=split.begin, sb_count=split.count) for b in bases]
     local = torch.zeros(split.chunk_bytes, dtype=torch.uint8, device=dev)
     out = torch.empty(world * split.chunk_bytes, dtype=torch.uint8, device=dev) if world > 1 else None
     searched, gathered = torch.cuda.Event(), torch.cuda.Event()
@@ -653,10 +656,9 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, steps, fence):
             gather()
     pair_ms = timed(lambda i: (search(i), gather())) if world > 1 else search_ms
     step_ms = timed(step)
-    for t in frames:
-        gpu.release(base + t)
-    for pn in cur:
-        gpu.release(pn)
+    for b in bases:
+        for t in frames:
+            gpu.release(b + t)
     return {"workload": wl["desc"] + ", one picture per step split over the GPUs", "sbs_per_picture": n_sb,
             "sbs_per_rank": split.slots, "refs": R, "steps": steps, "picture_bytes": Wd * Ht,
             "distribute_ms": {m: round(v, 4) for m, v in dist_ms.items()}, "distribution": best,

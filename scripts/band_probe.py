@@ -50,7 +50,20 @@ def main():
         gpu.sync()
         return round((time.perf_counter() - t0) / n * 1e3, 4)
 
+    # the same content uploaded from host memory into a picture allocated after the device-built ones
+    gpu.upload(base + 902, frames[8])
+    jd = job(base + 902)
+    same = {lv: bool((gpu.download(base + 8, lv) == gpu.download(base + 900, lv)).all()) for lv in range(3)}
+    recs = {}
+    for nm, j in (("a", ja), ("b", jb), ("d", jd)):
+        gpu.submit_batch_device([j], [out.data_ptr()], lane=0)
+        gpu.sync()
+        recs[nm] = out.cpu().numpy().tobytes()
     res = {
+        "pyramid_equal_by_level": same,
+        "records_equal_device_built": recs["a"] == recs["b"],
+        "records_equal_late_host": recs["a"] == recs["d"],
+        "late_host_upload": timed(lambda i: gpu.submit_batch_device([jd], [out.data_ptr()], lane=0)),
         "resident_host_upload": timed(lambda i: gpu.submit_batch_device([ja], [out.data_ptr()], lane=0)),
         "device_built": timed(lambda i: gpu.submit_batch_device([jb], [out.data_ptr()], lane=0)),
         "device_built_alternating": timed(lambda i: gpu.submit_batch_device([jb if i & 1 else jc], [out.data_ptr()],

@@ -42,12 +42,14 @@ def main():
     dev = torch.device("cuda", 0)
     pbuf = [torch.zeros(n_sb * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device=dev) for _ in range(2)]
 
-    def jobs_for(base, n):
+    def jobs_for(base, n):  # picture set k at base + 64 k, its references resident (realistic distances)
         js = []
         for k in range(n):
-            j = W.workload_job(name)
-            j.picture_number = base + k
-            js.append(j)
+            b = base + 64 * k
+            for t, f in frames.items():
+                if t != 8:
+                    gpu.upload(b + t, f)
+            js.append(W.workload_job(name, base=b))
         return js
 
     def timed(fn, n=reps, warm=8):
@@ -64,29 +66,29 @@ def main():
 
     pj4 = jobs_for(910000, 4)
     pj8 = jobs_for(920000, 8)
-    for k in range(8):  # make the rotating pictures resident once (their references are t = 6, 7, 9, 10)
-        gpu.upload_async(920000 + k, pinned.data_ptr(), Wd, Ht)
+    for k in range(8):  # make the rotating pictures resident once
+        gpu.upload_async(920000 + 64 * k + 8, pinned.data_ptr(), Wd, Ht)
     for k in range(4):
-        gpu.upload_async(910000 + k, pinned.data_ptr(), Wd, Ht)
+        gpu.upload_async(910000 + 64 * k + 8, pinned.data_ptr(), Wd, Ht)
     gpu.sync()
     jme = W.workload_job(name)
 
-    out["upload_only"] = timed(lambda i: gpu.upload_async(910000 + (i & 3), pinned.data_ptr(), Wd, Ht))
+    out["upload_only"] = timed(lambda i: gpu.upload_async(910000 + 64 * (i & 3) + 8, pinned.data_ptr(), Wd, Ht))
     out["me_only"] = timed(lambda i: gpu.submit_batch_device([jme], [pbuf[0].data_ptr()]))
     out["me_only_lanes"] = timed(lambda i: gpu.submit_batch_device([jme], [pbuf[i & 1].data_ptr()], lane=i & 1))
 
     def pipe0(i):
-        gpu.upload_async(910000 + (i & 3), pinned.data_ptr(), Wd, Ht)
+        gpu.upload_async(910000 + 64 * (i & 3) + 8, pinned.data_ptr(), Wd, Ht)
         gpu.submit_batch_device([pj4[i & 3]], [pbuf[0].data_ptr()])
     out["pipe_lane0"] = timed(pipe0)
 
     def pipel(i):
-        gpu.upload_async(910000 + (i & 3), pinned.data_ptr(), Wd, Ht)
+        gpu.upload_async(910000 + 64 * (i & 3) + 8, pinned.data_ptr(), Wd, Ht)
         gpu.submit_batch_device([pj4[i & 3]], [pbuf[i & 1].data_ptr()], lane=i & 1)
     out["pipe_lanes"] = timed(pipel)
 
     def pipe8(i):
-        gpu.upload_async(920000 + (i & 7), pinned.data_ptr(), Wd, Ht)
+        gpu.upload_async(920000 + 64 * (i & 7) + 8, pinned.data_ptr(), Wd, Ht)
         gpu.submit_batch_device([pj8[i & 7]], [pbuf[i & 1].data_ptr()], lane=i & 1)
     out["pipe_depth8"] = timed(pipe8)
 
