@@ -23,20 +23,28 @@
  *                                  output outside every glue lock, so the ME
  *                                  threads of several pictures keep several
  *                                  jobs in flight (uploads, searches and copies
- *                                  overlap). Pictures are uploaded on first
- *                                  use and re-uploaded after the encoder rebuilds
- *                                  their 1/4 and 1/16 planes
- *                                  (svtme_picture_changed). Pictures the job API
+ *                                  overlap). A picture is uploaded as soon as
+ *                                  the encoder has decimated it (picture
+ *                                  analysis, pic_analysis_process.c:2151), so
+ *                                  its DMA and pyramid run while the picture
+ *                                  is still in the encoder's earlier stages,
+ *                                  and again whenever the encoder rebuilds its
+ *                                  1/4 and 1/16 planes (svtme_picture_changed);
+ *                                  a job uploads what is not resident yet (on
+ *                                  first use). Pictures the job API
  *                                  does not cover (super-resolution / resize
  *                                  scaled references, me_process.c:229-246;
  *                                  the DG detector's HME, me_process.c:115) and
  *                                  jobs that fail run on the encoder's own SB
  *                                  function (the fallback).
  *   Linking with -Wl,--wrap=svt_aom_motion_estimation_b64
- *   -Wl,--wrap=svt_aom_downsample_filtering_input_picture and
- *   -DSVTME_GLUE_WRAP routes both call sites of the SB function and every
- *   re-decimation outside pic_analysis_process.c through this file without
- *   editing the encoder's sources.
+ *   -Wl,--wrap=svt_aom_downsample_filtering_input_picture
+ *   -Wl,--wrap=svt_aom_picture_analysis_result_creator
+ *   -Wl,--wrap=svt_post_full_object -Wl,--wrap=svt_av1_enc_deinit and
+ *   -DSVTME_GLUE_WRAP routes both call sites of the SB function, every
+ *   re-decimation outside pic_analysis_process.c, the end of each picture's
+ *   analysis and the encoder's teardown through this file without editing the
+ *   encoder's sources.
  *
  * Parity / debug mode
  *   svt_aom_setup_rtcd_hip_parity() registers the per-kernel *_hip rtcd variants
@@ -50,13 +58,15 @@
  *
  * Environment (read once): SVTME_DEVICE (HIP device, default 0);
  * SVTME_GLUE_STRICT=1 aborts instead of falling back; SVTME_GLUE_VERIFY=1
- * compares every uploaded pyramid with the encoder's own planes;
+ * compares every uploaded pyramid with the encoder's own planes, and every
+ * picture a job names with the encoder's planes when the job is submitted;
+ * SVTME_GLUE_EAGER=0 leaves every upload to the first job that names the picture;
  * SVTME_GLUE_STATS=<file> appends the counters at exit (jobs, SBs, uploads,
  * timing: upload / submit / wait milliseconds, mean job latency, the busy time
  * with a job in flight and served_sb_per_s = SBs of the jobs / busy time; and
  * the rtcd check: how many of the pointers parity mode replaces changed since
  * the first SB call, and how many point at this file's HIP wrappers);
- * SVTME_GLUE_RESIDENT caps the resident pictures (default 64).
+ * SVTME_GLUE_RESIDENT caps the resident pictures (default 128).
  */
 #include <pthread.h>
 #include <stddef.h>
@@ -70,6 +80,7 @@
 #include "me_context.h"
 #include "me_sb_results.h"
 #include "pcs.h"
+#include "pic_analysis_results.h"
 #include "reference_object.h"
 #include "sequence_control_set.h"
 
@@ -77,7 +88,7 @@
 
 EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
                                         uint32_t b64_origin_y, MeContext *me_ctx, EbPictureBufferDesc *input_ptr);
-void svtme_picture_changed(PictureParentControlSet *pcs);
+void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDesc *full);
 void svtme_glue_release(void);
 void svt_aom_setup_rtcd_hip_parity(void);
 void svtme_controls_from_me_context(svtme_controls *c, const MeContext *m);
@@ -561,7 +572,7 @@ static struct {
     pthread_cond_t cv;   /* a job finished */
     pthread_mutex_t gpu; /* one thread uploads / submits at a time (not held while waiting) */
     svtme_ctx *ctx;
-    int strict, verify, max_resident;
+    int strict, verify, eager, max_resident;
     const char *stats_path, *trace_path;
     GlueTrace *trace;
     uint32_t n_trace, cap_trace;
@@ -580,8 +591,8 @@ static struct {
     double busy_t0;
     struct {
         unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
-        unsigned long long job_sbs, max_inflight, unpinned;
-        double upload_s, submit_s, wait_s, job_s, busy_s;
+        unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job;
+        double upload_s, submit_s, wait_s, job_s, busy_s, eager_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER};
 
@@ -612,17 +623,21 @@ static void glue_stats_at_exit(void) {
     int hip = 0;
     for (int i = 0; i < GLUE_RTCD_N; i++) hip += g_hip_wrappers[i] != NULL && rt[i] == g_hip_wrappers[i];
     const double rate = G.n.busy_s > 0 ? (double)G.n.job_sbs / G.n.busy_s : 0.0;
+    /* the same with the picture-analysis threads' upload calls counted as busy time */
+    const double rate_up = G.n.busy_s + G.n.eager_s > 0 ? (double)G.n.job_sbs / (G.n.busy_s + G.n.eager_s) : 0.0;
     const unsigned long long jobs = G.n.pa_jobs + G.n.tf_jobs;
     fprintf(f,
             "{\"backend\": %d, \"pa_jobs\": %llu, \"tf_jobs\": %llu, \"sbs\": %llu, \"fallback_sbs\": %llu, "
-            "\"uploads\": %llu, \"invalidations\": %llu, \"evictions\": %llu, \"verified_planes\": %llu, "
+            "\"uploads\": %llu, \"invalidations\": %llu, \"evictions\": %llu, \"verified_planes\": %llu, \"verified_job_planes\": %llu, "
             "\"stale_jobs\": %llu, \"unpinned_uploads\": %llu, \"rtcd_checked\": %d, \"rtcd_changed\": %d, \"rtcd_hip\": %d, "
             "\"job_sbs\": %llu, \"max_inflight\": %llu, \"upload_ms\": %.3f, \"submit_ms\": %.3f, \"wait_ms\": %.3f, "
-            "\"job_latency_ms\": %.4f, \"busy_ms\": %.3f, \"served_sb_per_s\": %.1f}\n",
+            "\"job_latency_ms\": %.4f, \"busy_ms\": %.3f, \"served_sb_per_s\": %.1f, \"eager_uploads\": %llu, "
+            "\"eager_upload_ms\": %.3f, \"served_sb_per_s_with_uploads\": %.1f}\n",
             G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
-            G.n.evictions, G.n.verified, G.n.stale, G.n.unpinned, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
+            G.n.evictions, G.n.verified, G.n.verified_job, G.n.stale, G.n.unpinned, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
             G.n.max_inflight, 1e3 * G.n.upload_s, 1e3 * G.n.submit_s, 1e3 * G.n.wait_s,
-            jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate);
+            jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate, G.n.eager_uploads, 1e3 * G.n.eager_s,
+            rate_up);
     fclose(f);
 }
 
@@ -631,7 +646,8 @@ static void glue_init(void) {
     rtcd_snapshot(G.rtcd0);
     G.strict       = (e = getenv("SVTME_GLUE_STRICT")) && atoi(e);
     G.verify       = (e = getenv("SVTME_GLUE_VERIFY")) && atoi(e);
-    G.max_resident = (e = getenv("SVTME_GLUE_RESIDENT")) ? atoi(e) : 64;
+    G.eager        = !(e = getenv("SVTME_GLUE_EAGER")) || atoi(e);
+    G.max_resident = (e = getenv("SVTME_GLUE_RESIDENT")) ? atoi(e) : 128;
     if (G.max_resident < 9)
         G.max_resident = 9; /* a job names at most 1 + 8 pictures */
     G.stats_path = getenv("SVTME_GLUE_STATS");
@@ -761,6 +777,18 @@ void svtme_glue_release(void) {
     pthread_mutex_unlock(&G.gpu);
 }
 
+/* SVTME_GLUE_VERIFY: the resident pyramid of pn equals the encoder's three planes (aborts if not) */
+static void verify_pic(uint64_t pn, const EbPictureBufferDesc *full, const EbPictureBufferDesc *quarter,
+                       const EbPictureBufferDesc *sixteenth, unsigned long long *count) {
+    if (verify_level(pn, 0, full) || (quarter && verify_level(pn, 1, quarter)) ||
+        (sixteenth && verify_level(pn, 2, sixteenth))) {
+        fprintf(stderr, "svtme glue: picture %llu: the ME pyramid differs from the encoder's planes\n",
+                (unsigned long long)pn);
+        abort();
+    }
+    *count += 1 + (quarter != NULL) + (sixteenth != NULL);
+}
+
 static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPictureBufferDesc *quarter,
                       const EbPictureBufferDesc *sixteenth, uint32_t w, uint32_t h, uint64_t pin[9], int npin) {
     GluePic *p = pic_find(pn);
@@ -788,13 +816,8 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
     if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
         return -1;
     G.n.upload_s += now_s() - t0;
-    if (G.verify && (verify_level(pn, 0, full) || (quarter && verify_level(pn, 1, quarter)) ||
-                     (sixteenth && verify_level(pn, 2, sixteenth)))) {
-        fprintf(stderr, "svtme glue: picture %llu: the ME pyramid differs from the encoder's planes\n",
-                (unsigned long long)pn);
-        abort();
-    }
-    G.n.verified += G.verify ? 3 : 0;
+    if (G.verify)
+        verify_pic(pn, full, quarter, sixteenth, &G.n.verified);
     if (!p) {
         if (G.n_pics == G.cap_pics) {
             G.cap_pics = G.cap_pics ? 2 * G.cap_pics : 16;
@@ -830,23 +853,47 @@ static void job_unlink(GlueJob *j) { /* G.mu held */
     *pp = j->next;
 }
 
-/* The encoder rebuilt a picture's 1/4 and 1/16 planes from its (possibly
- * replaced) full-resolution plane: temporal filtering's
- * pad_and_decimate_filtered_pic (temporal_filtering.c:3895-3931), or picture
- * decision (pd_process.c:2720-2739). Jobs read it again from the new planes;
- * jobs already computed read the old ones, as the encoder's SB calls made
- * before the rebuild did, and are no longer matched by later calls. */
-void svtme_picture_changed(PictureParentControlSet *pcs) {
+static EbPaReferenceObject *pa_object(const PictureParentControlSet *pcs) {
+    return (EbPaReferenceObject *)pcs->pa_ref_pic_wrapper->object_ptr;
+}
+
+/* The encoder decimated a picture into its 1/4 and 1/16 planes: picture
+ * analysis (pic_analysis_process.c:2151, the first time), temporal filtering's
+ * pad_and_decimate_filtered_pic (temporal_filtering.c:3895-3931, the filtered
+ * picture), or picture decision (pd_process.c:2720-2739, a re-copy). Jobs still
+ * to come read the new planes; jobs already computed read the old ones, as the
+ * encoder's SB calls made before the rebuild did, and are no longer matched by
+ * later calls.
+ *
+ * When `full` is the plane the jobs read (the picture's PA reference object's
+ * input_padded_pic, which is what submit_job uploads), it is uploaded here,
+ * ahead of the picture's jobs: every later change to it is again a decimation
+ * through this function, and the encoder's stages that write it (temporal
+ * filtering, picture decision) run after the jobs that read the earlier content
+ * have completed, which implies their upload has. Other planes (resize.c's
+ * scaled pictures) only mark the resident copy out of date. */
+void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDesc *full) {
     pthread_once(&G.once, glue_init);
     if (!G.ctx)
         return;
-    /* the resident planes stay until the next job re-uploads the picture in place
-     * (svtme_picture_upload_async orders that after the jobs still reading them) */
+    const EbPictureBufferDesc *pa = pcs->pa_ref_pic_wrapper ? pa_object(pcs)->input_padded_pic : NULL;
+    const int eager = G.eager && full && pa && full->buffer_y == pa->buffer_y && full->stride_y == pa->stride_y &&
+        full->org_x == pa->org_x && full->org_y == pa->org_y && pcs->aligned_width && pcs->aligned_height &&
+        !pcs->frame_superres_enabled && !pcs->frame_resize_enabled;
     pthread_mutex_lock(&G.gpu);
     GluePic *p = pic_find(pcs->picture_number);
     if (p && !p->dirty) {
         p->dirty = 1;
         G.n.invalidations++;
+    }
+    if (eager) {
+        const double t0 = now_s();
+        const EbPaReferenceObject *o = pa_object(pcs);
+        uint64_t pin[9] = {pcs->picture_number};
+        if (pic_ensure(pcs->picture_number, pa, o->quarter_downsampled_picture_ptr, o->sixteenth_downsampled_picture_ptr,
+                       pcs->aligned_width, pcs->aligned_height, pin, 1) == 0)
+            G.n.eager_uploads++;
+        G.n.eager_s += now_s() - t0;
     }
     pthread_mutex_unlock(&G.gpu);
     pthread_mutex_lock(&G.mu);
@@ -862,10 +909,6 @@ void svtme_picture_changed(PictureParentControlSet *pcs) {
         }
     }
     pthread_mutex_unlock(&G.mu);
-}
-
-static EbPaReferenceObject *pa_object(const PictureParentControlSet *pcs) {
-    return (EbPaReferenceObject *)pcs->pa_ref_pic_wrapper->object_ptr;
 }
 
 /* make the job's pictures resident and submit it (G.gpu held); *ticket on success */
@@ -887,6 +930,16 @@ static int submit_job(GlueJob *j, const PictureParentControlSet *pcs, const MeCo
                            job->width, job->height, pin, npin))
                 return -1;
         }
+    if (G.verify) { /* what the job reads is the encoder's current content, however it became resident */
+        verify_pic(job->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
+                   cur->sixteenth_downsampled_picture_ptr, &G.n.verified_job);
+        for (int l = 0; l < job->num_lists; l++)
+            for (int r = 0; r < job->num_refs[l]; r++) {
+                const EbDownScaledBufDescPtrArray *d = &me->me_ds_ref_array[l][r];
+                verify_pic(d->picture_number, d->picture_ptr, d->quarter_picture_ptr, d->sixteenth_picture_ptr,
+                           &G.n.verified_job);
+            }
+    }
     const double t0 = now_s();
     const svtme_status st =
         svtme_submit_picture_packed_async(G.ctx, G.next_lane++ % SVTME_LANES, job, &j->layout, j->packed, ticket);
@@ -1020,6 +1073,41 @@ EbErrorType __wrap_svt_av1_enc_deinit(EbComponentType *svt_enc_component) {
 void __wrap_svt_aom_downsample_filtering_input_picture(PictureParentControlSet *pcs, EbPictureBufferDesc *full,
                                                        EbPictureBufferDesc *quarter, EbPictureBufferDesc *sixteenth) {
     __real_svt_aom_downsample_filtering_input_picture(pcs, full, quarter, sixteenth);
-    svtme_picture_changed(pcs);
+    svtme_picture_changed(pcs, full);
+}
+
+/* Picture analysis decimates inside its own translation unit
+ * (pic_analysis_process.c:2151), out of reach of --wrap, and ends each picture
+ * by posting a PictureAnalysisResults object (pic_analysis_process.c:2180-2191).
+ * The wraps below record the objects the encoder creates for that FIFO (at
+ * svt_av1_enc_init, enc_handle.c) and upload the picture when one is posted:
+ * its PA reference planes are final then, until a later decimation. Objects
+ * beyond the table's size only lose the early upload (jobs upload on first use). */
+static void *g_pa_results[1024];
+static uint32_t g_n_pa_results;
+
+EbErrorType __real_svt_aom_picture_analysis_result_creator(EbPtr *object_dbl_ptr, EbPtr object_init_data_ptr);
+EbErrorType __wrap_svt_aom_picture_analysis_result_creator(EbPtr *object_dbl_ptr, EbPtr object_init_data_ptr) {
+    const EbErrorType e = __real_svt_aom_picture_analysis_result_creator(object_dbl_ptr, object_init_data_ptr);
+    const uint32_t n    = __atomic_load_n(&g_n_pa_results, __ATOMIC_RELAXED);
+    if (e == EB_ErrorNone && n < sizeof(g_pa_results) / sizeof(g_pa_results[0])) {
+        g_pa_results[n] = *object_dbl_ptr;
+        __atomic_store_n(&g_n_pa_results, n + 1, __ATOMIC_RELEASE);
+    }
+    return e;
+}
+
+EbErrorType __real_svt_post_full_object(EbObjectWrapper *object_ptr);
+EbErrorType __wrap_svt_post_full_object(EbObjectWrapper *object_ptr) {
+    const uint32_t n = __atomic_load_n(&g_n_pa_results, __ATOMIC_ACQUIRE);
+    for (uint32_t i = 0; object_ptr && i < n; i++)
+        if (g_pa_results[i] == object_ptr->object_ptr) {
+            const PictureAnalysisResults *r = (const PictureAnalysisResults *)object_ptr->object_ptr;
+            PictureParentControlSet *pcs    = (PictureParentControlSet *)r->pcs_wrapper->object_ptr;
+            if (!pcs->is_overlay && pcs->pa_ref_pic_wrapper) /* overlays skip the analysis (:2122) */
+                svtme_picture_changed(pcs, pa_object(pcs)->input_padded_pic);
+            break;
+        }
+    return __real_svt_post_full_object(object_ptr);
 }
 #endif

@@ -33,7 +33,8 @@ if [ -d "$REF/Source" ]; then
     gcc -fsanitize=address,undefined -o "$OUT/svtav1enc_ora" "$ENC"/obj/Source/App/*.o \
         "$ENC"/obj/third_party/safestringlib/*.o "$OUT/glue.o" "$ENC/libsvtenc.a" \
         -Wl,--wrap=svt_aom_motion_estimation_b64 -Wl,--wrap=svt_aom_downsample_filtering_input_picture \
-        -Wl,--wrap=svt_av1_enc_deinit \
+        -Wl,--wrap=svt_av1_enc_deinit -Wl,--wrap=svt_aom_picture_analysis_result_creator \
+        -Wl,--wrap=svt_post_full_object \
         -L"$OUT" -loraclejob -Wl,-rpath,"$OUT" -Wl,--gc-sections -lpthread -lm
 fi
 

@@ -124,10 +124,10 @@ def encode(kind: str, case: str, workdir: str, env_extra=None, timeout: int = 60
     return res
 
 
-def check(case: str, kind: str, workdir: str) -> dict:
+def check(case: str, kind: str, workdir: str, env_extra=None) -> dict:
     """Reference encode and glue encode of one case; raises on any difference."""
     ref = encode("ref", case, workdir)
-    got = encode(kind, case, workdir)
+    got = encode(kind, case, workdir, env_extra)
     g = got["glue"]
     if got["md5"] != ref["md5"]:
         raise AssertionError(f"{case}: bitstream with {kind} ME differs from the reference encoder "

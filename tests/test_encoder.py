@@ -33,6 +33,8 @@ def test_bitstream_identical_oracle_backend(case, workdir):
     r = E.check(case, "ora", workdir)
     assert r["sbs"] > 0 and r["fallback_sbs"] == 0
     assert r["verified_planes"] == 3 * r["uploads"]
+    assert r["verified_job_planes"] >= 3 * (r["pa_jobs"] + r["tf_jobs"])
+    assert r["eager_uploads"] > 0
     _no_rtcd_registered(r)
 
 
@@ -47,9 +49,20 @@ def _no_rtcd_registered(r):
 @pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
 def test_tf_jobs_and_redecimation_exercised(workdir):
     """At preset 8 temporal filtering runs: TF-ME jobs are served and the
-    filtered pictures' pyramids are re-uploaded (svtme_picture_changed)."""
+    filtered pictures' pyramids are re-uploaded (svtme_picture_changed), at
+    decimation time (eager uploads: every job finds its pictures resident)."""
     r = E.check("ra360_p12", "ora", workdir)
     assert r["tf_jobs"] > 0 and r["pa_jobs"] > 0 and r["invalidations"] > 0
+
+
+@pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
+@pytest.mark.parametrize("case", ["ra360_p12", "240p_p8_lowdelay"])
+def test_job_time_uploads_only(case, workdir):
+    """SVTME_GLUE_EAGER=0: no picture is uploaded at decimation time; every job
+    uploads what it names on first use (the path eager uploads normally skip)."""
+    r = E.check(case, "ora", workdir, {"SVTME_GLUE_EAGER": "0"})
+    assert r["eager_uploads"] == 0 and r["uploads"] > 0 and r["fallback_sbs"] == 0
+    assert r["verified_planes"] == 3 * r["uploads"]
 
 
 @pytest.mark.gpu
