@@ -455,7 +455,7 @@ def main():
 
     band = None
     if args.band_steps > 0:
-        band = band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, args.band_steps, fence)
+        band = band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, args.band_steps, fence)
 
     recs = None
     if world == 1:
@@ -551,7 +551,7 @@ def main():
         dist.destroy_process_group()
 
 
-def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, steps, fence):
+def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, steps, fence):
     """SURVEY.md 8(e) / BASELINE configs[4]: ONE 7680x4320 p8 picture per step,
     its SBs split in N equal chunks (D.BandSplit): the picture's 8-bit luma plane
     reaches every rank (rank 0 uploads it from pinned host memory and an RCCL
@@ -563,8 +563,11 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, steps, fence):
     each picture is distributed once on arrival. Timed separately: the
     distribution both ways, the search alone, the all-gather alone, and the
     pipelined step (distribution of picture i + 1 on the copy / upload streams
-    while picture i is searched and gathered); strong scaling: SBs of the
-    picture / the pipelined step time."""
+    while picture i is searched and gathered; consecutive pictures' searches on
+    the two submission lanes, each with its own chunk buffer, so that at N = 8,
+    where a rank's chunk is 1 020 workgroups against 2 048 resident slots, the
+    next picture's search fills the CUs the previous one leaves); strong
+    scaling: SBs of the picture / the pipelined step time."""
     import torch
 
     name = "8k_p8"
@@ -584,9 +587,10 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, steps, fence):
     split = D.BandSplit(n_sb, R, S.REF_RECORD_DTYPE.itemsize, world, rank)
     cur = [b + 8 for b in bases]
     jobs = [W.workload_job(name, base=b, sb_begin=split.begin, sb_count=split.count) for b in bases]
-    local = torch.zeros(split.chunk_bytes, dtype=torch.uint8, device=dev)
-    out = torch.empty(world * split.chunk_bytes, dtype=torch.uint8, device=dev) if world > 1 else None
-    searched, gathered = torch.cuda.Event(), torch.cuda.Event()
+    local = [torch.zeros(split.chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+    out = [torch.empty(world * split.chunk_bytes, dtype=torch.uint8, device=dev) if world > 1 else None
+           for _ in range(2)]
+    searched, gathered = [torch.cuda.Event() for _ in range(2)], [torch.cuda.Event() for _ in range(2)]
     host = torch.from_numpy(frames[8].reshape(-1)).pin_memory() if rank == 0 or world == 1 else None
     host_all = torch.from_numpy(frames[8].reshape(-1)).pin_memory()  # the per-rank PCIe variant
     planes = [torch.empty(Wd * Ht, dtype=torch.uint8, device=dev) for _ in range(2)]
@@ -616,14 +620,16 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, steps, fence):
         built[b].record(ustream)
 
     def search(i=0):
-        gpu.submit_batch_device([jobs[i & 1]], [local.data_ptr()], lane=0)
+        b = i & 1
+        gpu.submit_batch_device([jobs[b]], [local[b].data_ptr()], lane=b)
 
-    def gather():
-        searched.record(ext)
-        comm.wait_event(searched)
-        split.exchange(local, out, dist, stream=comm)
-        gathered.record(comm)
-        ext.wait_event(gathered)  # the next search rewrites the chunk the gather reads
+    def gather(i=0):
+        b = i & 1
+        searched[b].record(exts[b])
+        comm.wait_event(searched[b])
+        split.exchange(local[b], out[b], dist, stream=comm)
+        gathered[b].record(comm)
+        exts[b].wait_event(gathered[b])  # the lane's next search rewrites the chunk the gather reads
 
     def timed(fn):
         fence()
@@ -643,18 +649,18 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, ext, comm, steps, fence):
         distribute(i, modes[0])
         search(i)
         if world > 1:
-            gather()
+            gather(i)
     dist_ms = {m: timed(lambda i, m=m: distribute(i, m)) for m in modes}
     best = min(dist_ms, key=dist_ms.get)
     search_ms = timed(search)
-    gather_ms = timed(lambda i: split.exchange(local, out, dist, stream=comm)) if world > 1 else 0.0
+    gather_ms = timed(lambda i: split.exchange(local[i & 1], out[i & 1], dist, stream=comm)) if world > 1 else 0.0
 
     def step(i):
         distribute(i, best)
         search(i)
         if world > 1:
-            gather()
-    pair_ms = timed(lambda i: (search(i), gather())) if world > 1 else search_ms
+            gather(i)
+    pair_ms = timed(lambda i: (search(i), gather(i))) if world > 1 else search_ms
     step_ms = timed(step)
     for b in bases:
         for t in frames:
