@@ -673,7 +673,36 @@ static void glue_fallback(const char *what) {
 }
 
 /* ---- page-locked output buffers (G.mu held) */
-static int buf_take(GlueJob *j, size_t need) {
+/* The largest packed output any job of an n_sb-SB picture can have: a PA-ME
+ * layout with every PU, candidate and reference slot, or whole TF-ME records */
+static size_t buf_worst(uint32_t n_sb) {
+    const svtme_pack_layout pa = {SVTME_PU_COUNT, SVTME_MAX_PA_ME_CAND, SVTME_MAX_PA_ME_MV, 0, 1, {0, 0}};
+    const svtme_pack_layout tf = {0, 0, 0, 1, 0, {0, 0}};
+    const uint32_t a = svtme_packed_sb_bytes(&pa, 8), b = svtme_packed_sb_bytes(&tf, 8);
+    return (size_t)n_sb * (a > b ? a : b);
+}
+
+#define GLUE_POOL_BATCH 6 /* buffers page-locked together when the pool runs dry */
+
+/* Page-lock the first batch of output buffers ahead of the first job (called
+ * from the picture-analysis thread's upload, G.mu held): the jobs of the first
+ * pictures then find them in the pool */
+static void buf_prefill(uint32_t n_sb) {
+    static int done;
+    if (done)
+        return;
+    done            = 1;
+    const size_t sz = (buf_worst(n_sb) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+    for (int k = 0; k < GLUE_POOL_BATCH && G.n_pool < sizeof(G.pool) / sizeof(G.pool[0]); k++) {
+        uint8_t *p = (uint8_t *)svtme_host_alloc(sz);
+        if (!p)
+            break;
+        G.pool[G.n_pool].p = p, G.pool[G.n_pool].cap = sz;
+        G.n_pool++;
+    }
+}
+
+static int buf_take(GlueJob *j, size_t need, size_t worst) {
     int best = -1;
     for (uint32_t i = 0; i < G.n_pool; i++)
         if (G.pool[i].cap >= need && (best < 0 || G.pool[i].cap < G.pool[best].cap))
@@ -683,14 +712,26 @@ static int buf_take(GlueJob *j, size_t need) {
         G.pool[best] = G.pool[--G.n_pool];
         return 0;
     }
-    /* a new buffer holds the largest output seen so far (rounded to 1 MB): the
-     * pool then serves every later job whatever its layout */
+    /* new buffers hold the largest output a job of the largest picture seen so far
+     * can have (rounded to 1 MB), so the pool serves every later job whatever its
+     * layout; page-locking costs milliseconds, so a batch is made at once (the
+     * first jobs of an encode would otherwise pay it one job at a time) */
     static size_t largest;
-    largest       = need > largest ? need : largest;
-    need          = (largest + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
-    j->packed     = (uint8_t *)svtme_host_alloc(need);
-    j->packed_cap = need;
-    return j->packed ? 0 : -1;
+    largest    = need > largest ? need : largest;
+    largest    = worst > largest ? worst : largest;
+    const size_t sz = (largest + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+    j->packed     = (uint8_t *)svtme_host_alloc(sz);
+    j->packed_cap = sz;
+    if (!j->packed)
+        return -1;
+    for (int k = 1; k < GLUE_POOL_BATCH && G.n_pool < sizeof(G.pool) / sizeof(G.pool[0]); k++) {
+        uint8_t *p = (uint8_t *)svtme_host_alloc(sz);
+        if (!p)
+            break;
+        G.pool[G.n_pool].p = p, G.pool[G.n_pool].cap = sz;
+        G.n_pool++;
+    }
+    return 0;
 }
 
 static void buf_give(GlueJob *j) {
@@ -897,6 +938,8 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     }
     pthread_mutex_unlock(&G.gpu);
     pthread_mutex_lock(&G.mu);
+    if (eager)
+        buf_prefill(svtme_sb_total(pcs->aligned_width, pcs->aligned_height));
     for (GlueJob *j = G.jobs, *nx; j; j = nx) {
         nx = j->next;
         if (j->stale || !job_names(&j->job, pcs->picture_number))
@@ -988,7 +1031,7 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
         else
             G.n.pa_jobs++;
         const double t_start = now_s();
-        int rc = buf_take(j, (size_t)j->n_sb * j->stride);
+        int rc = buf_take(j, (size_t)j->n_sb * j->stride, buf_worst(j->n_sb));
         if (G.inflight++ == 0)
             G.busy_t0 = t_start;
         if (G.inflight > G.n.max_inflight)
