@@ -377,6 +377,12 @@ void svtme_host_free(void *p);
  * CPU; svtme_host_unregister undoes it once the copies reading it have run. */
 svtme_status svtme_host_register(void *p, uint64_t bytes);
 svtme_status svtme_host_unregister(void *p);
+/* Size the device memory of later jobs ahead of them: every submission lane's
+ * inter-stage scratch and the device buffers of the first `tickets` packed-job
+ * slots, for jobs over pictures up to width x height with up to max_refs
+ * reference slots and any pack layout. Submissions within those bounds then
+ * allocate nothing (a job beyond them still grows the buffers it needs). */
+svtme_status svtme_reserve(svtme_ctx *ctx, uint32_t width, uint32_t height, uint32_t max_refs, uint32_t tickets);
 /* Kernel timing with HIP events on the context's stream, recorded around every
  * stage launch of every submission while enabled (enable = 1). svtme_timing_read
  * waits for the recorded launch groups and returns the milliseconds of stage 0

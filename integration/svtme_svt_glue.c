@@ -687,10 +687,10 @@ static size_t buf_worst(uint32_t n_sb) {
 /* Page-lock the first batch of output buffers ahead of the first job (called
  * from the picture-analysis thread's upload, G.mu held): the jobs of the first
  * pictures then find them in the pool */
-static void buf_prefill(uint32_t n_sb) {
+static int buf_prefill(uint32_t n_sb) { /* 1 the first time */
     static int done;
     if (done)
-        return;
+        return 0;
     done            = 1;
     const size_t sz = (buf_worst(n_sb) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
     for (int k = 0; k < GLUE_POOL_BATCH && G.n_pool < sizeof(G.pool) / sizeof(G.pool[0]); k++) {
@@ -700,6 +700,7 @@ static void buf_prefill(uint32_t n_sb) {
         G.pool[G.n_pool].p = p, G.pool[G.n_pool].cap = sz;
         G.n_pool++;
     }
+    return 1;
 }
 
 static int buf_take(GlueJob *j, size_t need, size_t worst) {
@@ -938,8 +939,9 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     }
     pthread_mutex_unlock(&G.gpu);
     pthread_mutex_lock(&G.mu);
-    if (eager)
-        buf_prefill(svtme_sb_total(pcs->aligned_width, pcs->aligned_height));
+    if (eager && buf_prefill(svtme_sb_total(pcs->aligned_width, pcs->aligned_height)))
+        /* and the device side: every lane's scratch and the first tickets' buffers */
+        (void)svtme_reserve(G.ctx, pcs->aligned_width, pcs->aligned_height, 8, GLUE_POOL_BATCH);
     for (GlueJob *j = G.jobs, *nx; j; j = nx) {
         nx = j->next;
         if (j->stale || !job_names(&j->job, pcs->picture_number))

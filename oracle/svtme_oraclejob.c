@@ -215,6 +215,10 @@ void *svtme_host_alloc(uint64_t bytes) { return malloc(bytes ? (size_t)bytes : 1
 void svtme_host_free(void *p) { free(p); }
 svtme_status svtme_host_register(void *p, uint64_t bytes) { return p && bytes ? SVTME_OK : SVTME_ERR_BAD_PARAMETER; }
 svtme_status svtme_host_unregister(void *p) { return p ? SVTME_OK : SVTME_ERR_BAD_PARAMETER; }
+svtme_status svtme_reserve(svtme_ctx *c, uint32_t width, uint32_t height, uint32_t max_refs, uint32_t tickets) {
+    return c && width && height && max_refs >= 1 && max_refs <= 8 && tickets <= SVTME_MAX_TICKETS ? SVTME_OK
+                                                                                                : SVTME_ERR_BAD_PARAMETER;
+}
 
 /* the packed layout of include/svtme.h (svtme_pack_layout), as svtme_pack.hip writes it */
 static void pack_sb(const svtme_ref_record *rec, const svtme_sb_result *s, uint32_t R, const svtme_pack_layout *L,

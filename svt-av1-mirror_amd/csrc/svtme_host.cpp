@@ -935,6 +935,58 @@ extern "C" svtme_status svtme_host_unregister(void *p) {
     return SVTME_OK;
 }
 
+// Worst-case device bytes of one packed job over sbs SBs with R slots: records,
+// SB results and the packed copy (the layout of svtme_submit_picture_packed_async)
+static size_t packed_job_bytes(size_t sbs, uint32_t R, const svtme_pack_layout *L) {
+    const size_t rb = sbs * R * sizeof(svtme_ref_record);
+    const size_t sbb = L->sb_results ? sbs * sizeof(svtme_sb_result) : 0;
+    const size_t o_sb = (rb + 255) & ~(size_t)255, o_pk = (o_sb + sbb + 255) & ~(size_t)255;
+    return o_pk + sbs * svtme_packed_sb_bytes(L, R);
+}
+
+extern "C" svtme_status svtme_reserve(svtme_ctx *c, uint32_t width, uint32_t height, uint32_t max_refs,
+                                      uint32_t tickets) {
+    if (!c || width == 0 || height == 0 || max_refs == 0 || max_refs > 8 || tickets > SVTME_MAX_TICKETS)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_reserve: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t sbs = svtme_sb_total(width, height), slots = sbs * max_refs;
+    svtme_status st;
+    for (uint32_t l = 0; l < SVTME_LANES; l++) {
+        if ((st = ensure_lane(c, l)))
+            return st;
+        Lane &L = c->lanes[l];
+        const size_t kb = slots * SVTME_PU_COUNT * sizeof(unsigned long long);
+        if (L.ares_cap < sbs * SVTME_A_N * sizeof(ARes) || L.bst_cap < sbs * sizeof(BState) || L.keys_cap < kb ||
+            L.cslot_cap < slots * sizeof(CSlot))
+            HIP_TRY(hipStreamSynchronize(L.s)); // (the lane's queued work reads the old buffers)
+        if ((st = ensure_buf((void **)&L.d_ares, &L.ares_cap, sbs * SVTME_A_N * sizeof(ARes))) ||
+            (st = ensure_buf((void **)&L.d_bst, &L.bst_cap, sbs * sizeof(BState))))
+            return st;
+        if (L.keys_cap < kb) {
+            if ((st = ensure_buf((void **)&L.d_keys, &L.keys_cap, kb)))
+                return st;
+            L.keys_rest = false; // new keys are not ~0 yet
+        }
+        if ((st = ensure_buf((void **)&L.d_cslot, &L.cslot_cap, slots * sizeof(CSlot))))
+            return st;
+    }
+    const svtme_pack_layout pa = {SVTME_PU_COUNT, SVTME_MAX_PA_ME_CAND, SVTME_MAX_PA_ME_MV, 0, 1, {0, 0}};
+    const svtme_pack_layout tf = {0, 0, 0, 1, 0, {0, 0}};
+    const size_t need = std::max(packed_job_bytes(sbs, max_refs, &pa), packed_job_bytes(sbs, max_refs, &tf));
+    uint32_t k = 0;
+    for (auto &t : c->tickets) {
+        if (k == tickets)
+            break;
+        if (t.id) // outstanding: its buffer is in use
+            continue;
+        if ((st = ensure_buf(&t.d_mem, &t.d_cap, need)))
+            return st;
+        k++;
+    }
+    return SVTME_OK;
+}
+
 extern "C" svtme_status svtme_submit_picture_packed_async(svtme_ctx *c, uint32_t lane, const svtme_job *job,
                                                           const svtme_pack_layout *L, void *host_out,
                                                           uint64_t *ticket) {

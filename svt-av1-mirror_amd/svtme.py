@@ -611,6 +611,8 @@ def _job_api_protos(lib):
         _proto(lib, "svtme_host_alloc", "restype", vp)
         _proto(lib, "svtme_host_free", "argtypes", [vp])
         _proto(lib, "svtme_host_free", "restype", None)
+        _proto(lib, "svtme_reserve", "argtypes", [vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32])
+        _proto(lib, "svtme_reserve", "restype", C.c_int32)
         _proto(lib, "svtme_set_paths", "argtypes", [vp, C.c_uint32])
         _proto(lib, "svtme_set_paths", "restype", C.c_int32)
         _proto(lib, "svtme_set_timing", "argtypes", [vp, C.c_int])
@@ -760,6 +762,11 @@ class GpuME:
             return C.string_at(ptr, nbytes)
         finally:
             self.lib.svtme_host_free(ptr)
+
+    def reserve(self, width: int, height: int, max_refs: int = 8, tickets: int = 4):
+        """svtme_reserve: size the lanes' scratch and the first `tickets` packed-job
+        buffers for jobs up to width x height with max_refs reference slots."""
+        self._check(self.lib.svtme_reserve(self.ctx, width, height, max_refs, tickets), "svtme_reserve")
 
     def set_paths(self, paths: int):
         """Kernel-path selection (SVTME_PATH_* bits; 0 = every specialised kernel)."""

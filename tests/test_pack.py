@@ -5,7 +5,7 @@ svtme_svt_glue.c) equal the numpy restatement of the documented layout
 
 CPU: the oracle job API (oracle/liboraclejob.so, the encoder tests' backend).
 GPU: k_pack behind the ticket API of libsvtme.so, several jobs in flight on
-both submission lanes, and the ticket limit.
+both submission lanes, the ticket limit, and jobs after svtme_reserve.
 """
 import pytest
 
@@ -30,6 +30,15 @@ def _setup(api, base):
     ctrl = S.derive_controls(8, 35, S.input_resolution_of(W, H), 1)
     return S.make_job(W, H, ctrl, base + 8, (base + 7, base + 6), (base + 9,), temporal_layer_index=1,
                       ref_count_used=(2, 1))
+
+
+def test_reserve_arguments_oracle_backend():
+    api = S.GpuME(0, lib=S.load_oracle_job())
+    api.reserve(W, H, 8, 4)
+    for bad in ((0, H, 8, 4), (W, H, 0, 4), (W, H, 9, 4), (W, H, 8, 17)):
+        with pytest.raises(RuntimeError):
+            api.reserve(*bad)
+    api.close()
 
 
 def test_packed_layout_oracle_backend():
@@ -63,5 +72,15 @@ def test_packed_output_gpu(gpu):
     for p in pend:
         assert gpu.wait_packed(*p) == exp
     assert gpu.submit_packed(job, L) == exp
+    # reserved for a larger picture (every lane's scratch, the first tickets' buffers):
+    # the same bytes, and a picture beyond the reservation still grows what it needs
+    gpu.reserve(W, H // 2, 3, 2)
+    gpu.reserve(2 * W, 2 * H, 8, 6)
+    for t in LAYOUTS:
+        L = _layout(t)
+        assert gpu.submit_packed(job, L, lane=1 - (t[0] & 1)) == S.pack_outputs(recs, sbr if L.sb_results else None, L), t
+    for bad in ((0, H, 8, 4), (W, H, 9, 4), (W, H, 8, 17)):
+        with pytest.raises(RuntimeError):
+            gpu.reserve(*bad)
     for t in (6, 7, 8, 9):
         gpu.release(7000 + t)
