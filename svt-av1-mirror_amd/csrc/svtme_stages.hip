@@ -4540,9 +4540,27 @@ static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, ui
             hipLaunchKernelGGL(K, grid, dim3(256), 0, s, __VA_ARGS__);                                             \
     } while (0)
 
-extern "C" hipError_t svtme_prime_stages(void) { // (see svtme_prime_pyramid)
+extern "C" hipError_t svtme_prime_stages(void) { // (see svtme_prime_pyramid): every kernel a job can launch
+    const void *k[] = {
+        (const void *)svtme::k_hme<true, true, true, false>,   (const void *)svtme::k_hme<true, true, true, true>,
+        (const void *)svtme::k_hme<false, true, true, false>,  (const void *)svtme::k_hme<true, true, false, false>,
+        (const void *)svtme::k_stage_a<false>,                 (const void *)svtme::k_stage_a<true>,
+        (const void *)svtme::k_stage_d<false>,                 (const void *)svtme::k_stage_d<true>,
+        (const void *)svtme::k_stage_b<false>,                 (const void *)svtme::k_stage_b<true>,
+        (const void *)svtme::k_stage_c<false>,                 (const void *)svtme::k_stage_c<true>,
+        (const void *)svtme::k_stage_c1<true, true, true>,     (const void *)svtme::k_stage_c1<true, true>,
+        (const void *)svtme::k_stage_c1<true, false>,          (const void *)svtme::k_stage_c1<false, true, true>,
+        (const void *)svtme::k_stage_c1<false, true>,          (const void *)svtme::k_stage_c1<false, false>,
+        (const void *)svtme::k_l0_full<2>,                     (const void *)svtme::k_l0_full<4>,
+        (const void *)svtme::k_l1_full,                        (const void *)svtme::k_fp_wide,
+        (const void *)svtme::k_stage_e};
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, (const void *)svtme::k_hme<true, true, true, false>);
+    for (const void *f : k) {
+        const hipError_t e = hipFuncGetAttributes(&a, f);
+        if (e != hipSuccess)
+            return e;
+    }
+    return hipSuccess;
 }
 
 extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
