@@ -571,6 +571,7 @@ static struct {
     pthread_mutex_t mu;  /* job list, buffer pool, counters */
     pthread_cond_t cv;   /* a job finished */
     pthread_mutex_t gpu; /* one thread uploads / submits at a time (not held while waiting) */
+    pthread_mutex_t reg; /* the page-locked encoder buffers (regs) */
     svtme_ctx *ctx;
     int strict, verify, eager, max_resident;
     const char *stats_path, *trace_path;
@@ -584,7 +585,7 @@ static struct {
     uint32_t next_lane;
     GlueBuf pool[2 * SVTME_MAX_TICKETS];
     uint32_t n_pool;
-    GlueReg *regs; /* (G.gpu) */
+    GlueReg *regs; /* (G.reg) */
     uint32_t n_regs, cap_regs;
     void *rtcd0[GLUE_RTCD_N]; /* the rtcd pointers at the first SB call (after svt_aom_setup_rtcd_internal) */
     uint32_t inflight;        /* jobs between their submission and their output in host memory */
@@ -594,7 +595,8 @@ static struct {
         unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job;
         double upload_s, submit_s, wait_s, job_s, busy_s, eager_s;
     } n;
-} G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER};
+} G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER,
+     PTHREAD_MUTEX_INITIALIZER};
 
 static void glue_trace_at_exit(void) {
     FILE *f = fopen(G.trace_path, "w");
@@ -684,23 +686,30 @@ static size_t buf_worst(uint32_t n_sb) {
 
 #define GLUE_POOL_BATCH 6 /* buffers page-locked together when the pool runs dry */
 
-/* Page-lock the first batch of output buffers ahead of the first job (called
- * from the picture-analysis thread's upload, G.mu held): the jobs of the first
- * pictures then find them in the pool */
-static int buf_prefill(uint32_t n_sb) { /* 1 the first time */
+/* Ahead of the first job (called once, from the first picture-analysis upload,
+ * no glue lock held): page-lock a batch of worst-case output buffers for the
+ * pool, and size the library's device scratch and first tickets (svtme_reserve),
+ * so that the first jobs of an encode allocate nothing */
+static void buf_prefill(uint32_t w, uint32_t h) {
     static int done;
-    if (done)
-        return 0;
-    done            = 1;
-    const size_t sz = (buf_worst(n_sb) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
-    for (int k = 0; k < GLUE_POOL_BATCH && G.n_pool < sizeof(G.pool) / sizeof(G.pool[0]); k++) {
-        uint8_t *p = (uint8_t *)svtme_host_alloc(sz);
-        if (!p)
+    if (__atomic_exchange_n(&done, 1, __ATOMIC_ACQ_REL))
+        return;
+    const size_t sz = (buf_worst(svtme_sb_total(w, h)) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
+    uint8_t *b[GLUE_POOL_BATCH];
+    int n = 0;
+    for (; n < GLUE_POOL_BATCH; n++)
+        if (!(b[n] = (uint8_t *)svtme_host_alloc(sz)))
             break;
-        G.pool[G.n_pool].p = p, G.pool[G.n_pool].cap = sz;
-        G.n_pool++;
+    (void)svtme_reserve(G.ctx, w, h, 8, GLUE_POOL_BATCH);
+    pthread_mutex_lock(&G.mu);
+    for (int k = 0; k < n; k++) {
+        if (G.n_pool < sizeof(G.pool) / sizeof(G.pool[0])) {
+            G.pool[G.n_pool].p = b[k], G.pool[G.n_pool].cap = sz;
+            G.n_pool++;
+        } else
+            svtme_host_free(b[k]);
     }
-    return 1;
+    pthread_mutex_unlock(&G.mu);
 }
 
 static int buf_take(GlueJob *j, size_t need, size_t worst) {
@@ -778,17 +787,23 @@ static int verify_level(uint64_t pn, int level, const EbPictureBufferDesc *d) {
 /* Make picture pn resident with the encoder's current planes of it: an
  * asynchronous upload (the library stages the rows, the pyramid is built on its
  * upload stream, and the first job reading the picture waits for it on the GPU). */
-/* Page-lock the span an upload reads, once per encoder buffer (G.gpu held): the
- * encoder keeps its input picture buffers from svt_av1_enc_init to
- * svt_av1_enc_deinit and recycles them, so a buffer is locked on its first
- * upload and every later upload from it is one DMA with no staging pass through
- * the CPU (busy with the encoder's threads). svtme_glue_release (called by the
- * svt_av1_enc_deinit wrap) unlocks them all before the encoder frees them. */
+/* Page-lock the span an upload reads, once per encoder buffer: the encoder
+ * keeps its input picture buffers from svt_av1_enc_init to svt_av1_enc_deinit
+ * and recycles them, so a buffer is locked on its first upload and every later
+ * upload from it is one DMA with no staging pass through the CPU (busy with the
+ * encoder's threads). Locking takes a fraction of a millisecond, so it runs
+ * under its own lock, before the upload takes G.gpu (the picture-analysis
+ * thread of a new buffer does not hold up job submissions). svtme_glue_release
+ * (called by the svt_av1_enc_deinit wrap) unlocks them all before the encoder
+ * frees them. */
 static void pin_span(const void *p, uint64_t bytes) {
+    pthread_mutex_lock(&G.reg);
     for (uint32_t i = 0; i < G.n_regs; i++)
         if (G.regs[i].p == p) {
-            if (G.regs[i].bytes >= bytes)
+            if (G.regs[i].bytes >= bytes) {
+                pthread_mutex_unlock(&G.reg);
                 return;
+            }
             svtme_sync(G.ctx); /* the uploads queued from the old span have run */
             svtme_host_unregister((void *)p);
             G.regs[i] = G.regs[--G.n_regs];
@@ -805,6 +820,13 @@ static void pin_span(const void *p, uint64_t bytes) {
         G.n_regs++;
     } else
         G.n.unpinned++;
+    pthread_mutex_unlock(&G.reg);
+}
+
+/* the span of the rows an upload of the w x h visible samples of `full` reads */
+static const uint8_t *span_of(const EbPictureBufferDesc *full, uint32_t w, uint32_t h, uint64_t *bytes) {
+    *bytes = (uint64_t)(h - 1) * full->stride_y + w;
+    return full->buffer_y + (size_t)full->org_y * full->stride_y + full->org_x;
 }
 
 /* Unlock every page-locked encoder buffer (after the uploads reading them have run) */
@@ -812,10 +834,12 @@ void svtme_glue_release(void) {
     if (!G.ctx)
         return;
     pthread_mutex_lock(&G.gpu);
+    pthread_mutex_lock(&G.reg);
     if (G.n_regs)
         svtme_sync(G.ctx);
     for (uint32_t i = 0; i < G.n_regs; i++) svtme_host_unregister((void *)G.regs[i].p);
     G.n_regs = 0;
+    pthread_mutex_unlock(&G.reg);
     pthread_mutex_unlock(&G.gpu);
 }
 
@@ -853,8 +877,9 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
         }
     }
     const double t0 = now_s();
-    const uint8_t *y = full->buffer_y + (size_t)full->org_y * full->stride_y + full->org_x;
-    pin_span(y, (uint64_t)(h - 1) * full->stride_y + w);
+    uint64_t span;
+    const uint8_t *y = span_of(full, w, h, &span);
+    pin_span(y, span); /* (locked already when the caller pinned it first) */
     if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
         return -1;
     G.n.upload_s += now_s() - t0;
@@ -922,6 +947,15 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     const int eager = G.eager && full && pa && full->buffer_y == pa->buffer_y && full->stride_y == pa->stride_y &&
         full->org_x == pa->org_x && full->org_y == pa->org_y && pcs->aligned_width && pcs->aligned_height &&
         !pcs->frame_superres_enabled && !pcs->frame_resize_enabled;
+    double t_pin = 0;
+    if (eager) { /* page-lock a new buffer and fill the pools before taking G.gpu */
+        const double t0 = now_s();
+        uint64_t span;
+        const uint8_t *y = span_of(pa, pcs->aligned_width, pcs->aligned_height, &span);
+        pin_span(y, span);
+        buf_prefill(pcs->aligned_width, pcs->aligned_height);
+        t_pin = now_s() - t0;
+    }
     pthread_mutex_lock(&G.gpu);
     GluePic *p = pic_find(pcs->picture_number);
     if (p && !p->dirty) {
@@ -929,6 +963,7 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
         G.n.invalidations++;
     }
     if (eager) {
+        G.n.eager_s += t_pin;
         const double t0 = now_s();
         const EbPaReferenceObject *o = pa_object(pcs);
         uint64_t pin[9] = {pcs->picture_number};
@@ -939,9 +974,6 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     }
     pthread_mutex_unlock(&G.gpu);
     pthread_mutex_lock(&G.mu);
-    if (eager && buf_prefill(svtme_sb_total(pcs->aligned_width, pcs->aligned_height)))
-        /* and the device side: every lane's scratch and the first tickets' buffers */
-        (void)svtme_reserve(G.ctx, pcs->aligned_width, pcs->aligned_height, 8, GLUE_POOL_BATCH);
     for (GlueJob *j = G.jobs, *nx; j; j = nx) {
         nx = j->next;
         if (j->stale || !job_names(&j->job, pcs->picture_number))
