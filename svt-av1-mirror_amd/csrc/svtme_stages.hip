@@ -4540,6 +4540,10 @@ static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, ui
             hipLaunchKernelGGL(K, grid, dim3(256), 0, s, __VA_ARGS__);                                             \
     } while (0)
 
+namespace svtme {
+__global__ void k_prime_stages() {} // (an empty kernel of this code object, see svtme_prime_pyramid)
+} // namespace svtme
+
 extern "C" hipError_t svtme_prime_stages(void) { // (see svtme_prime_pyramid): every kernel a job can launch
     const void *k[] = {
         (const void *)svtme::k_hme<true, true, true, false>,   (const void *)svtme::k_hme<true, true, true, true>,
@@ -4560,7 +4564,8 @@ extern "C" hipError_t svtme_prime_stages(void) { // (see svtme_prime_pyramid): e
         if (e != hipSuccess)
             return e;
     }
-    return hipSuccess;
+    hipLaunchKernelGGL(svtme::k_prime_stages, dim3(1), dim3(64), 0, 0);
+    return hipDeviceSynchronize();
 }
 
 extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
