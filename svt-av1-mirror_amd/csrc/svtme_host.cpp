@@ -698,17 +698,20 @@ static svtme_status prepare(svtme_ctx *c) {
         HIP_TRY(hipEventCreateWithFlags(&t.launched, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
     }
-    // The first work on a stream and the first copy in each direction cost
-    // milliseconds of one-time runtime setup (≈8 ms measured in an encoder's first
-    // picture job): a fill on every stream and a small copy each way happen here,
-    // at context creation, instead of inside the first job.
+    // The first work on a stream and the first large copy in each direction cost
+    // milliseconds of one-time runtime setup (the first packed job's D2H copy call
+    // took 6.8 ms in a HIP API trace, later ones 10 us; small copies take another
+    // path and do not set it up): a fill on every stream and a 4 MB copy each way
+    // on the upload and download streams happen here, at context creation.
     void *d = nullptr, *h = nullptr;
-    HIP_TRY(hipMalloc(&d, 256));
-    HIP_TRY(hipHostMalloc(&h, 256, hipHostMallocDefault));
+    const size_t wb = (size_t)4 << 20;
+    HIP_TRY(hipMalloc(&d, wb));
+    HIP_TRY(hipHostMalloc(&h, wb, hipHostMallocDefault));
     for (uint32_t l = 0; l < SVTME_LANES; l++) HIP_TRY(hipMemsetAsync(d, 0, 256, c->lanes[l].s));
     HIP_TRY(hipMemsetAsync(d, 0, 256, c->ustream));
-    HIP_TRY(hipMemcpyAsync(d, h, 256, hipMemcpyHostToDevice, c->ustream));
-    HIP_TRY(hipMemcpyAsync(h, d, 256, hipMemcpyDeviceToHost, c->dstream));
+    HIP_TRY(hipMemcpyAsync(d, h, wb, hipMemcpyHostToDevice, c->ustream));
+    HIP_TRY(hipStreamSynchronize(c->ustream));
+    HIP_TRY(hipMemcpyAsync(h, d, wb, hipMemcpyDeviceToHost, c->dstream));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipFree(d));
     HIP_TRY(hipHostFree(h));
