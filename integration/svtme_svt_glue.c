@@ -593,7 +593,7 @@ static struct {
     struct {
         unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
         unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job;
-        double upload_s, submit_s, wait_s, job_s, busy_s, eager_s;
+        double upload_s, submit_s, wait_s, job_s, busy_s, eager_s, prefill_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER,
      PTHREAD_MUTEX_INITIALIZER};
@@ -634,12 +634,12 @@ static void glue_stats_at_exit(void) {
             "\"stale_jobs\": %llu, \"unpinned_uploads\": %llu, \"rtcd_checked\": %d, \"rtcd_changed\": %d, \"rtcd_hip\": %d, "
             "\"job_sbs\": %llu, \"max_inflight\": %llu, \"upload_ms\": %.3f, \"submit_ms\": %.3f, \"wait_ms\": %.3f, "
             "\"job_latency_ms\": %.4f, \"busy_ms\": %.3f, \"served_sb_per_s\": %.1f, \"eager_uploads\": %llu, "
-            "\"eager_upload_ms\": %.3f, \"served_sb_per_s_with_uploads\": %.1f}\n",
+            "\"eager_upload_ms\": %.3f, \"served_sb_per_s_with_uploads\": %.1f, \"prefill_ms\": %.3f}\n",
             G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
             G.n.evictions, G.n.verified, G.n.verified_job, G.n.stale, G.n.unpinned, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
             G.n.max_inflight, 1e3 * G.n.upload_s, 1e3 * G.n.submit_s, 1e3 * G.n.wait_s,
             jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate, G.n.eager_uploads, 1e3 * G.n.eager_s,
-            rate_up);
+            rate_up, 1e3 * G.n.prefill_s);
     fclose(f);
 }
 
@@ -694,6 +694,7 @@ static void buf_prefill(uint32_t w, uint32_t h) {
     static int done;
     if (__atomic_exchange_n(&done, 1, __ATOMIC_ACQ_REL))
         return;
+    const double t0 = now_s();
     const size_t sz = (buf_worst(svtme_sb_total(w, h)) + (1u << 20) - 1) & ~(size_t)((1u << 20) - 1);
     uint8_t *b[GLUE_POOL_BATCH];
     int n = 0;
@@ -709,6 +710,7 @@ static void buf_prefill(uint32_t w, uint32_t h) {
         } else
             svtme_host_free(b[k]);
     }
+    G.n.prefill_s = now_s() - t0;
     pthread_mutex_unlock(&G.mu);
 }
 
@@ -953,8 +955,8 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
         uint64_t span;
         const uint8_t *y = span_of(pa, pcs->aligned_width, pcs->aligned_height, &span);
         pin_span(y, span);
-        buf_prefill(pcs->aligned_width, pcs->aligned_height);
         t_pin = now_s() - t0;
+        buf_prefill(pcs->aligned_width, pcs->aligned_height); /* (once; timed as prefill_ms) */
     }
     pthread_mutex_lock(&G.gpu);
     GluePic *p = pic_find(pcs->picture_number);
