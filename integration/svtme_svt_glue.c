@@ -63,7 +63,9 @@
  * SVTME_GLUE_EAGER=0 leaves every upload to the first job that names the picture;
  * SVTME_GLUE_STATS=<file> appends the counters at exit (jobs, SBs, uploads,
  * timing: upload / submit / wait milliseconds, mean job latency, the busy time
- * with a job in flight and served_sb_per_s = SBs of the jobs / busy time; and
+ * with a job in flight and served_sb_per_s = SBs of the jobs / busy time; the
+ * analysis threads' upload calls (eager_upload_ms), page-locking of encoder
+ * buffers (registrations, register_ms) and the one-off pool fill (prefill_ms); and
  * the rtcd check: how many of the pointers parity mode replaces changed since
  * the first SB call, and how many point at this file's HIP wrappers);
  * SVTME_GLUE_RESIDENT caps the resident pictures (default 128).
@@ -592,8 +594,8 @@ static struct {
     double busy_t0;
     struct {
         unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
-        unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job;
-        double upload_s, submit_s, wait_s, job_s, busy_s, eager_s, prefill_s;
+        unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job, registrations;
+        double upload_s, submit_s, wait_s, job_s, busy_s, eager_s, prefill_s, register_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER,
      PTHREAD_MUTEX_INITIALIZER};
@@ -634,12 +636,13 @@ static void glue_stats_at_exit(void) {
             "\"stale_jobs\": %llu, \"unpinned_uploads\": %llu, \"rtcd_checked\": %d, \"rtcd_changed\": %d, \"rtcd_hip\": %d, "
             "\"job_sbs\": %llu, \"max_inflight\": %llu, \"upload_ms\": %.3f, \"submit_ms\": %.3f, \"wait_ms\": %.3f, "
             "\"job_latency_ms\": %.4f, \"busy_ms\": %.3f, \"served_sb_per_s\": %.1f, \"eager_uploads\": %llu, "
-            "\"eager_upload_ms\": %.3f, \"served_sb_per_s_with_uploads\": %.1f, \"prefill_ms\": %.3f}\n",
+            "\"eager_upload_ms\": %.3f, \"served_sb_per_s_with_uploads\": %.1f, \"prefill_ms\": %.3f, "
+            "\"registrations\": %llu, \"register_ms\": %.3f}\n",
             G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
             G.n.evictions, G.n.verified, G.n.verified_job, G.n.stale, G.n.unpinned, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
             G.n.max_inflight, 1e3 * G.n.upload_s, 1e3 * G.n.submit_s, 1e3 * G.n.wait_s,
             jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate, G.n.eager_uploads, 1e3 * G.n.eager_s,
-            rate_up, 1e3 * G.n.prefill_s);
+            rate_up, 1e3 * G.n.prefill_s, G.n.registrations, 1e3 * G.n.register_s);
     fclose(f);
 }
 
@@ -817,11 +820,14 @@ static void pin_span(const void *p, uint64_t bytes) {
         if (!G.regs)
             abort();
     }
+    const double t0 = now_s();
     if (svtme_host_register((void *)p, bytes) == SVTME_OK) {
         G.regs[G.n_regs].p = p, G.regs[G.n_regs].bytes = bytes;
         G.n_regs++;
     } else
         G.n.unpinned++;
+    G.n.registrations++;
+    G.n.register_s += now_s() - t0;
     pthread_mutex_unlock(&G.reg);
 }
 
@@ -878,10 +884,10 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
             G.n.evictions++;
         }
     }
-    const double t0 = now_s();
     uint64_t span;
     const uint8_t *y = span_of(full, w, h, &span);
     pin_span(y, span); /* (locked already when the caller pinned it first) */
+    const double t0 = now_s();
     if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
         return -1;
     G.n.upload_s += now_s() - t0;
@@ -949,13 +955,10 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     const int eager = G.eager && full && pa && full->buffer_y == pa->buffer_y && full->stride_y == pa->stride_y &&
         full->org_x == pa->org_x && full->org_y == pa->org_y && pcs->aligned_width && pcs->aligned_height &&
         !pcs->frame_superres_enabled && !pcs->frame_resize_enabled;
-    double t_pin = 0;
-    if (eager) { /* page-lock a new buffer and fill the pools before taking G.gpu */
-        const double t0 = now_s();
+    if (eager) { /* page-lock a new buffer (timed as register_ms) and fill the pools before taking G.gpu */
         uint64_t span;
         const uint8_t *y = span_of(pa, pcs->aligned_width, pcs->aligned_height, &span);
         pin_span(y, span);
-        t_pin = now_s() - t0;
         buf_prefill(pcs->aligned_width, pcs->aligned_height); /* (once; timed as prefill_ms) */
     }
     pthread_mutex_lock(&G.gpu);
@@ -965,7 +968,6 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
         G.n.invalidations++;
     }
     if (eager) {
-        G.n.eager_s += t_pin;
         const double t0 = now_s();
         const EbPaReferenceObject *o = pa_object(pcs);
         uint64_t pin[9] = {pcs->picture_number};
