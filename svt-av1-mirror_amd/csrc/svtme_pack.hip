@@ -77,12 +77,7 @@ extern "C" hipError_t svtme_launch_pack(const svtme_ref_record *d_recs, const sv
     return hipGetLastError();
 }
 
-__global__ void k_prime_pack() {}
 extern "C" hipError_t svtme_prime_pack(void) { // (see svtme_prime_pyramid)
     hipFuncAttributes a;
-    hipError_t e = hipFuncGetAttributes(&a, (const void *)k_pack);
-    if (e != hipSuccess)
-        return e;
-    hipLaunchKernelGGL(k_prime_pack, dim3(1), dim3(64), 0, 0);
-    return hipDeviceSynchronize();
+    return hipFuncGetAttributes(&a, (const void *)k_pack);
 }

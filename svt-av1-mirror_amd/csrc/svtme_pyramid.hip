@@ -98,14 +98,8 @@ extern "C" hipError_t svtme_launch_copy_words(const void *src, void *dst, uint32
 }
 
 // Load this translation unit's code object now (HIP loads it lazily at the first
-// launch of one of its kernels, which would otherwise land in a job's latency):
-// an empty kernel of the same code object, launched once and waited for
-__global__ void k_prime_pyramid() {}
+// launch of one of its kernels, which would otherwise land in a job's latency)
 extern "C" hipError_t svtme_prime_pyramid(void) {
     hipFuncAttributes a;
-    hipError_t e = hipFuncGetAttributes(&a, (const void *)k_build_down);
-    if (e != hipSuccess)
-        return e;
-    hipLaunchKernelGGL(k_prime_pyramid, dim3(1), dim3(64), 0, 0);
-    return hipDeviceSynchronize();
+    return hipFuncGetAttributes(&a, (const void *)k_build_down);
 }

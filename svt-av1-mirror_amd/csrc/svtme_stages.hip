@@ -448,8 +448,6 @@ __device__ __forceinline__ uint32_t zz_finish(const ZzLoads &z) {
 
 template <bool R1> // R1: the real-time tune's second round (DevJob.ta1_list)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) k_stage_a(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     __shared__ __attribute__((aligned(16))) uint8_t srcb[4][256];
     __shared__ uint32_t wbuf[4][STAGE_A_BUF_DW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -809,8 +807,6 @@ __device__ __forceinline__ void dec_l0(Dec &d, const svtme_job &job, uint32_t vm
 // HME-L0 runs (dec_l0's exits) into BState for the second round
 template <bool RT0>
 __global__ void __launch_bounds__(256) k_stage_d(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     __shared__ Dec dec[4];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
@@ -891,8 +887,6 @@ __device__ __forceinline__ void hme_refine(int level, const DevPlane &P, int16_t
 
 template <bool L2>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(L2 ? 4 : 6, 8))) k_stage_b(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     __shared__ __attribute__((aligned(16))) uint8_t srcb[4][L2 ? 64 * 64 : 32 * 32];
     __shared__ uint32_t wbuf[4][STAGE_B_BUF_DW];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1920,8 +1914,6 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
 
 template <bool SUB_ME>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_c(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     __shared__ StC st;
     uint32_t sb_local;
     const DevJob &dj        = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
@@ -2775,8 +2767,6 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
 // K32: every order fits 12 bits (the host bounds the area, svtme_fp_k32)
 template <bool SUB, bool K32, bool WIDE = false> // WIDE: 6-quad full-pel load sets (areas >= 24 wide)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 5 : 4, 8))) k_stage_c1(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
     if (u >= B.total)
@@ -2932,8 +2922,6 @@ __device__ __forceinline__ uint32_t fpw_rebase(uint32_t b, uint32_t m, uint32_t 
 
 #define FPW_WAVES 5 // waves per SIMD: 5 workgroups of 30 KB LDS per CU
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WAVES, FPW_WAVES))) k_fp_wide(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     __shared__ __attribute__((aligned(16))) uint32_t fw[FPW_ROWS * FPW_PITCH]; // rows: fw_a | fw_b
     constexpr int ROWS = 4, RSTEP = 2; // sub-sampled rows
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -3262,8 +3250,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
 // ============================================================================
 template <int PR> // position rows per lane: 2 (quadrants up to 8 rows) or 4 (up to 16)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_l0_full(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
     if (u >= B.total)
@@ -3435,8 +3421,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 // otherwise).
 // ============================================================================
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_l1_full(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
     if (u >= B.total)
@@ -3689,8 +3673,6 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_e(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     __shared__ StC st;
     __shared__ CSlot csl[8];
     uint32_t sb_local;
@@ -3847,8 +3829,6 @@ struct HmeSh {
 #define HME_WAVES_PER_EU 8 // 64 VGPRs: 8 workgroups per CU
 template <bool FP, bool SUB_ME, bool K32, bool RT = false> // RT: the real-time tune's HME-L0 reduction (a1_table)
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WAVES_PER_EU, HME_WAVES_PER_EU))) k_hme(const DevBatch B) {
-    if (B.total == 0) // (the priming launch at context creation)
-        return;
     __shared__ HmeSh sh;
     const int tid = threadIdx.x, lane = tid & 63, wid = UNI(tid >> 6);
     uint32_t sb_local;
@@ -4560,10 +4540,6 @@ static DevBatch make_batch(const DevJob *d_jobs, const DevJob *h, uint32_t n, ui
             hipLaunchKernelGGL(K, grid, dim3(256), 0, s, __VA_ARGS__);                                             \
     } while (0)
 
-namespace svtme {
-__global__ void k_prime_stages() {} // (an empty kernel of this code object, see svtme_prime_pyramid)
-} // namespace svtme
-
 extern "C" hipError_t svtme_prime_stages(void) { // (see svtme_prime_pyramid): every kernel a job can launch
     const void *k[] = {
         (const void *)svtme::k_hme<true, true, true, false>,   (const void *)svtme::k_hme<true, true, true, true>,
@@ -4584,45 +4560,7 @@ extern "C" hipError_t svtme_prime_stages(void) { // (see svtme_prime_pyramid): e
         if (e != hipSuccess)
             return e;
     }
-    // HIP also sets up each kernel lazily at its first launch (≈1-2 ms each, 8 ms for
-    // a TF-ME job's first split-path launches): every kernel runs once here on an
-    // empty batch (each returns at once when B.total == 0)
-    DevBatch z{}; // no jobs, total 0
-#define SVTME_PRIME(...) hipLaunchKernelGGL((__VA_ARGS__), dim3(1), dim3(256), 0, 0, z)
-    SVTME_PRIME(svtme::k_stage_a<false>);
-    SVTME_PRIME(svtme::k_stage_a<true>);
-    SVTME_PRIME(svtme::k_stage_d<false>);
-    SVTME_PRIME(svtme::k_stage_d<true>);
-    SVTME_PRIME(svtme::k_stage_b<false>);
-    SVTME_PRIME(svtme::k_stage_b<true>);
-    SVTME_PRIME(svtme::k_stage_c<false>);
-    SVTME_PRIME(svtme::k_stage_c<true>);
-    SVTME_PRIME(svtme::k_stage_c1<true, true, true>);
-    SVTME_PRIME(svtme::k_stage_c1<true, true>);
-    SVTME_PRIME(svtme::k_stage_c1<true, false>);
-    SVTME_PRIME(svtme::k_stage_c1<false, true, true>);
-    SVTME_PRIME(svtme::k_stage_c1<false, true>);
-    SVTME_PRIME(svtme::k_stage_c1<false, false>);
-    SVTME_PRIME(svtme::k_l0_full<2>);
-    SVTME_PRIME(svtme::k_l0_full<4>);
-    SVTME_PRIME(svtme::k_l1_full);
-    SVTME_PRIME(svtme::k_fp_wide);
-    SVTME_PRIME(svtme::k_stage_e);
-#define SVTME_PRIME_HME(FP, SUB, K32)                                                                             \
-    SVTME_PRIME(svtme::k_hme<FP, SUB, K32, false>);                                                             \
-    SVTME_PRIME(svtme::k_hme<FP, SUB, K32, true>)
-    SVTME_PRIME_HME(true, true, true); // the instantiations svtme_launch_stages launches
-    SVTME_PRIME_HME(true, true, false);
-    SVTME_PRIME_HME(true, false, true);
-    SVTME_PRIME_HME(true, false, false);
-    SVTME_PRIME_HME(false, true, true);
-#undef SVTME_PRIME_HME
-#undef SVTME_PRIME
-    hipLaunchKernelGGL(svtme::k_prime_stages, dim3(1), dim3(64), 0, 0);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess)
-        return e;
-    return hipDeviceSynchronize();
+    return hipSuccess;
 }
 
 extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_jobs, uint32_t n, hipStream_t s,
