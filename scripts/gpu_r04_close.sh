@@ -3,6 +3,8 @@
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r04_close; mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 120 python3 scripts/first_job_probe.py > $O/first_job.json 2> $O/first_job.err || { tail $O/first_job.err; exit 1; }
+cat $O/first_job.json
 bash scripts/gpu_tests.sh > $O/gpu_tests_summary.txt 2>&1; rc=$?
 cp gpurun_out/gpu_tests.log gpurun_out/smoke.log $O/ 2>/dev/null
 tail -8 $O/gpu_tests_summary.txt; [ $rc -eq 0 ] || exit $rc
