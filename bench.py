@@ -240,6 +240,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    fence()  # the buffers' zero fills (torch's stream) before the library's streams write them
     for i in range(args.warmup):
         step(i)
     fence()

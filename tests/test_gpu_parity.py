@@ -180,6 +180,7 @@ def test_mctf_batch_mixed_outputs(svtme, gpu):
     for with_mid_sb in (False, True):
         bufs = [torch.zeros(nb, dtype=torch.uint8, device="cuda") for _ in jobs]
         sbs = [None, torch.zeros(nsb * S.SB_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda"), None]
+        torch.cuda.synchronize()  # the zero fills (torch's stream) before the library's streams write
         gpu.submit_batch_device(jobs, [b.data_ptr() for b in bufs],
                                 [s.data_ptr() if s is not None else None for s in sbs] if with_mid_sb else None)
         gpu.sync()
@@ -280,6 +281,7 @@ def test_picture_upload_async(svtme, gpu):
     R = S.ref_slots(job)
     n = S.sb_total(W8, H8)
     bufs = [torch.zeros(n * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()  # the zero fills (torch's stream) before the library's streams write
     gpu.submit_batch_device([job], [bufs[0].data_ptr()])
     gpu.upload_async(4107, new)  # re-upload while the first job may still run
     gpu.submit_batch_device([job], [bufs[1].data_ptr()])
@@ -325,15 +327,15 @@ def test_lanes_parity(svtme, gpu):
 
     def buf(j):
         return torch.zeros(n * S.ref_slots(j) * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
-    outs = []
-    for it in range(6):
-        for k, j in enumerate(jobs):
-            b = buf(j)
-            gpu.submit_batch_device([j], [b.data_ptr()], lane=(it + k) & 1)
-            outs.append((k, b))
+    # every output buffer zero-filled (on torch's stream) before the lanes' jobs write them: the
+    # library's streams do not wait for torch's, and a late fill would overwrite a job's records
+    outs = [(k, buf(j)) for it in range(6) for k, j in enumerate(jobs)]
+    after = buf(jobs[0])
+    torch.cuda.synchronize()
+    for i, (k, b) in enumerate(outs):
+        gpu.submit_batch_device([jobs[k]], [b.data_ptr()], lane=(i // len(jobs) + k) & 1)
     # re-upload ref 6007 asynchronously while both lanes may still read it, then search again
     gpu.upload_async(6007, frames[13])
-    after = buf(jobs[0])
     gpu.submit_batch_device([jobs[0]], [after.data_ptr()], lane=1)
     gpu.sync()
     for k, b in outs:
