@@ -131,6 +131,9 @@ struct svtme_ctx {
     void *ustaging = nullptr;      // their device staging plane (reused in upload-stream order)
     size_t ustaging_cap = 0;
     std::map<uint64_t, PicBuf> pics;
+    // released pictures whose memory queued work may still read: freed (or reused by
+    // a picture of the same size) once their upload and last readers have completed
+    std::vector<PicBuf> graves;
     void *staging      = nullptr;
     size_t staging_cap = 0;
     svtme_ref_record *d_records = nullptr;
@@ -240,6 +243,11 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         (void)hipFree(kv.second.mem);
         if (kv.second.ready)
             (void)hipEventDestroy(kv.second.ready);
+    }
+    for (auto &g : c->graves) {
+        (void)hipFree(g.mem);
+        if (g.ready)
+            (void)hipEventDestroy(g.ready);
     }
     if (c->staging)
         (void)hipFree(c->staging);
@@ -352,6 +360,38 @@ static svtme_status ensure_buf(void **p, size_t *cap, size_t need) {
     return SVTME_OK;
 }
 
+// a released picture's memory is idle: its upload and its lanes' last readers have run
+// (a lane's event may since mark a later submission: later, never early)
+static bool grave_idle(const PicBuf &g) {
+    if (g.ready && hipEventQuery(g.ready) != hipSuccess)
+        return false;
+    for (int l = 0; l < SVTME_LANES; l++)
+        if (g.used[l] && hipEventQuery(g.used[l]) != hipSuccess)
+            return false;
+    return true;
+}
+// free the idle released pictures; with want > 0, keep (and return) one idle buffer
+// of exactly `want` bytes for reuse instead of freeing it
+static uint8_t *sweep_graves(svtme_ctx *c, size_t want) {
+    uint8_t *keep = nullptr;
+    for (size_t i = 0; i < c->graves.size();) {
+        PicBuf &g = c->graves[i];
+        if (!grave_idle(g)) {
+            i++;
+            continue;
+        }
+        if (g.ready)
+            (void)hipEventDestroy(g.ready);
+        if (!keep && want && g.bytes == want)
+            keep = g.mem;
+        else
+            (void)hipFree(g.mem);
+        c->graves[i] = c->graves.back();
+        c->graves.pop_back();
+    }
+    return keep;
+}
+
 // allocate the three planes of a W x H picture in one buffer
 static svtme_status alloc_pic(svtme_ctx *c, uint64_t pn, uint32_t W, uint32_t H, PicBuf **out) {
     auto it = c->pics.find(pn);
@@ -376,7 +416,9 @@ static svtme_status alloc_pic(svtme_ctx *c, uint64_t pn, uint32_t W, uint32_t H,
     total += 1024; // slack: search-window loads may read a few dwords past the last row
     if (it == c->pics.end()) {
         PicBuf pb;
-        HIP_TRY(hipMalloc((void **)&pb.mem, total));
+        pb.mem = sweep_graves(c, total); // a released picture's idle memory of the same size, if any
+        if (!pb.mem)
+            HIP_TRY(hipMalloc((void **)&pb.mem, total));
         pb.bytes = total;
         pb.W = W, pb.H = H;
         it = c->pics.emplace(pn, pb).first;
@@ -574,13 +616,12 @@ extern "C" svtme_status svtme_picture_release(svtme_ctx *c, uint64_t pn) {
     if (it == c->pics.end())
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_release: picture %llu not resident",
                     (unsigned long long)pn);
-    svtme_status qs = quiesce(c);
-    if (qs)
-        return qs;
-    HIP_TRY(hipFree(it->second.mem));
-    if (it->second.ready)
-        HIP_TRY(hipEventDestroy(it->second.ready));
+    HIP_TRY(hipSetDevice(c->device));
+    // no device-wide wait: the memory goes to the graves until the work queued
+    // before the release (its upload, the lanes' readers) has run
+    c->graves.push_back(it->second);
     c->pics.erase(it);
+    (void)sweep_graves(c, 0);
     return SVTME_OK;
 }
 

@@ -258,6 +258,48 @@ def test_banded_fullpel_variance_parity(svtme, gpu, area, th, k32):
     assert not _controls_case(S, gpu, ctrl, 640, 360, (7, 6), (9,))
 
 
+def test_picture_release_while_read(svtme, gpu):
+    """svtme_picture_release does not wait for the device: a job queued before the
+    release still reads the released reference (its memory is freed, or reused by
+    a picture of the same size, only once that job has run), and a picture that
+    reuses released memory holds its own planes."""
+    import torch
+
+    S = svtme
+    w, h = 640, 360
+    syn = S.Synth(w, h)
+    cur, ref7, ref9, other = syn.frame(8), syn.frame(7), syn.frame(9), syn.frame(20)
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    for pn, f in ((4208, cur), (4207, ref7), (4209, ref9)):
+        gpu.upload(pn, f)
+    job = S.make_job(w, h, ctrl, 4208, (4207,), (4209,), temporal_layer_index=1, ref_count_used=(1, 1))
+    want = gpu.submit(job)[0]
+    n, R = S.sb_total(w, h), S.ref_slots(job)
+    bufs = [torch.zeros(n * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    torch.cuda.synchronize()
+    for k, b in enumerate(bufs):  # queued on both lanes, nothing waited for
+        gpu.submit_batch_device([job], [b.data_ptr()], lane=k & 1)
+    gpu.release(4207)
+    gpu.upload_async(4230, other)  # same size: may take the released memory once the jobs have run
+    gpu.upload_async(4207, other)  # the released number again, other content
+    gpu.sync()
+    for b in bufs:
+        got = np.frombuffer(b.cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n, R)
+        assert not S.compare_records(want, got)
+    p_other = S.build_host_pyramid(other, "oracle")
+    for pn in (4230, 4207):
+        for lv, name in enumerate(("full", "quarter", "sixteenth")):
+            assert np.array_equal(gpu.download(pn, lv), getattr(p_other, name)), (pn, name)
+    # released and idle now: the next same-size picture reuses memory and holds its own planes
+    gpu.release(4230)
+    gpu.upload(4231, ref7)
+    p7 = S.build_host_pyramid(ref7, "oracle")
+    for lv, name in enumerate(("full", "quarter", "sixteenth")):
+        assert np.array_equal(gpu.download(4231, lv), getattr(p7, name)), name
+    for pn in (4207, 4208, 4209, 4231):
+        gpu.release(pn)
+
+
 def test_picture_upload_async(svtme, gpu):
     """svtme_picture_upload_async: DMA into the resident plane + in-place pyramid
     build on the upload stream; the planes equal the reference's pyramid, a job
