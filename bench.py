@@ -116,7 +116,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=200,
+                    help="untimed steps first (the first ~100 steps after start-up run ~5 %% slower: 50 steps "
+                         "after 10 measured 55.9 M SB/s, 200 after 20 61.3 M, 200 after 200 63.5 M, 1000 after 200 "
+                         "63.8 M, scripts/gpu_r04steps.sh)")
     ap.add_argument("--workload", default="4k_p8", choices=sorted(W.WORKLOADS))
     ap.add_argument("--pictures", type=int, default=0,
                     help=f"pictures per step (default: {PICTURES_PER_GPU} per GPU; several go in one batched launch)")
