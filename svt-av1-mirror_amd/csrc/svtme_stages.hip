@@ -2845,48 +2845,33 @@ struct FpW {
     uint32_t b8t, b8b, b16, b32, b64; // K32 keys: 8x8 / 16x16 (sad << 16 | order), 32x32 / 64x64 (sad << 12 | order)
 };
 
-typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
-
-// The minimum 8x8 SAD of one block over the set's positions (packed u16 mins:
-// v_pk_min_u16): positions 4 iq + {0, 1} in the low dword of acc[iq], 4 iq + {2,
-// 3} in the high one. VALID: positions >= left are outside the area (the last,
-// partial set; left is wave-uniform, so the tests are scalar).
-template <bool VALID>
-__device__ __forceinline__ uint32_t fpw_set_min8(const unsigned long long (&acc)[FPW_TQ], int left) {
-    u16x2 mm = {0xFFFF, 0xFFFF};
-#pragma unroll
-    for (int iq = 0; iq < FPW_TQ; iq++)
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int e = 4 * iq + 2 * h;
-            uint32_t v  = (uint32_t)(acc[iq] >> (32 * h));
-            if (!VALID) {
-                if (e >= left)
-                    continue;
-                if (e + 1 >= left)
-                    v |= 0xFFFF0000u;
-            }
-            mm = __builtin_elementwise_min(mm, as_u16x2(v));
-        }
-    return min_u32((uint32_t)mm.x, (uint32_t)mm.y);
-}
-
 // min over lanes l and l ^ 8 (the two search-row halves), in place
 __device__ __forceinline__ uint32_t fpw_min_hr(uint32_t v) {
     return min_u32(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false)); // row_ror:8
 }
 
-// One quad pair (positions e0 .. e0 + 7 of the set) of both blocks: the 16x16 /
-// 32x32 / 64x64 sums and keys into the set minima (the 8x8 minima are taken per
-// set, fpw_set_min8). T / T2 (top), Bq / B2 (bottom): the qsad accumulators of
-// quads a and b. MASK: positions >= ev are outside the area (the last, partial pair).
+// One quad pair (positions e0 .. e0 + 7 of the set) of both blocks: 8x8 keys of
+// each block, then the 16x16 / 32x32 / 64x64 sums and keys into the set minima.
+// T / T2 (top), Bq / B2 (bottom): the qsad accumulators of quads a and b.
+// MASK: positions >= ev are outside the area (the last, partial pair).
 template <bool MASK>
 __device__ __forceinline__ void fpw_pair(FpW &m, unsigned long long T, unsigned long long T2, unsigned long long Bq,
                                          unsigned long long B2, int e0, int ev, uint32_t sel16, uint32_t sel32,
                                          int p16, int p32) {
     const uint32_t tl = (uint32_t)T, th = (uint32_t)(T >> 32), tl2 = (uint32_t)T2, th2 = (uint32_t)(T2 >> 32);
     const uint32_t bl = (uint32_t)Bq, bh = (uint32_t)(Bq >> 32), bl2 = (uint32_t)B2, bh2 = (uint32_t)(B2 >> 32);
+    auto k8 = [&](uint32_t v, int e) { // (sad << 16 | e) of position e of a packed pair
+        const uint32_t k = (e & 1) ? ((v & 0xFFFF0000u) | (uint32_t)e) : ((v << 16) | (uint32_t)e);
+        return (MASK && e >= ev) ? 0xFFFFFFFFu : k;
+    };
+    m.b8t = min_u32(min_u32(m.b8t, k8(tl, e0)), k8(tl, e0 + 1));
+    m.b8t = min_u32(min_u32(m.b8t, k8(th, e0 + 2)), k8(th, e0 + 3));
+    m.b8t = min_u32(min_u32(m.b8t, k8(tl2, e0 + 4)), k8(tl2, e0 + 5));
+    m.b8t = min_u32(min_u32(m.b8t, k8(th2, e0 + 6)), k8(th2, e0 + 7));
+    m.b8b = min_u32(min_u32(m.b8b, k8(bl, e0)), k8(bl, e0 + 1));
+    m.b8b = min_u32(min_u32(m.b8b, k8(bh, e0 + 2)), k8(bh, e0 + 3));
+    m.b8b = min_u32(min_u32(m.b8b, k8(bl2, e0 + 4)), k8(bl2, e0 + 5));
+    m.b8b = min_u32(min_u32(m.b8b, k8(bh2, e0 + 6)), k8(bh2, e0 + 7));
     // 8x16 columns, then 16x16 over bx ^ 1 (packed: both halves stay below 2^15)
     const uint32_t sl = dpp_add<0xB1>(tl + bl), sh = dpp_add<0xB1>(th + bh);
     const uint32_t sl2 = dpp_add<0xB1>(tl2 + bl2), sh2 = dpp_add<0xB1>(th2 + bh2);
@@ -2920,9 +2905,49 @@ __device__ __forceinline__ uint32_t fpw_rebase(uint32_t b, uint32_t m, uint32_t 
     return min_u32(b, m == 0xFFFFFFFFu ? m : m + base);
 }
 
+// The set loop's LDS row reads as ds_read_b64 with immediate offsets from one
+// base per set (inline: the compiler pairs them into ds_read2_b64, 8 LDS cycles
+// for what two ds_read_b64 move in 4, and adds a base register per row), the
+// next row's 5 reads issued before the current row is consumed; the waits are
+// explicit, since the compiler does not count these reads. Steady-state A/B at
+// the 1080p 64x64 override: k_fp_wide pass 10.39 -> 10.50 M SB/s (3 rounds).
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+struct FpwRow {
+    u32x2v v[FPW_TQ + 1]; // v[j] = (A[j], A[j + 1]): even j from fw_a, odd j from fw_b
+};
+template <int OFF>
+__device__ __forceinline__ u32x2v fpw_ds64(uint32_t a) {
+    u32x2v r;
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r) : "v"(a), "i"(OFF));
+    return r;
+}
+// row G of the set (block G / 4, sub-sampled row G % 4): rows RSTEP = 2 apart
+template <int G>
+__device__ __forceinline__ void fpw_row_issue(FpwRow &R, uint32_t lb) {
+    constexpr int ROW = (G / 4) * 8 + (G % 4) * 2, O = 4 * ROW * FPW_PITCH;
+    R.v[0] = fpw_ds64<O>(lb);
+    R.v[2] = fpw_ds64<O + 8>(lb);
+    R.v[4] = fpw_ds64<O + 16>(lb);
+    R.v[1] = fpw_ds64<O + 4 * FPW_BOFF>(lb);
+    R.v[3] = fpw_ds64<O + 4 * FPW_BOFF + 8>(lb);
+}
+// wait until at most N LDS reads are outstanding (the next row's), tying the row's registers to it
+template <int N>
+__device__ __forceinline__ void fpw_row_wait(FpwRow &R) {
+    asm volatile("s_waitcnt lgkmcnt(%5)" : "+v"(R.v[0]), "+v"(R.v[1]), "+v"(R.v[2]), "+v"(R.v[3]), "+v"(R.v[4]) : "i"(N));
+}
+template <int B, int E, typename F>
+__device__ __forceinline__ void fpw_sfor(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>());
+        fpw_sfor<B + 1, E>(f);
+    }
+}
+
 #define FPW_WAVES 5 // waves per SIMD: 5 workgroups of 30 KB LDS per CU
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WAVES, FPW_WAVES))) k_fp_wide(const DevBatch B) {
     __shared__ __attribute__((aligned(16))) uint32_t fw[FPW_ROWS * FPW_PITCH]; // rows: fw_a | fw_b
+    const uint32_t fw_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t *)fw;
     constexpr int ROWS = 4, RSTEP = 2; // sub-sampled rows
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t u = UNI(xcd_remap(blockIdx.x, gridDim.x) * 4 + wid);
@@ -3094,11 +3119,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
     const uint32_t sel32 = (c32 & 2) ? ((c32 & 1) ? 0x0C0C0706u : 0x0C0C0504u) : ((c32 & 1) ? 0x0C0C0302u : 0x0C0C0100u);
     const int p16 = bx & 1, p32 = c32 + 4 * (by2 & 1);
     const int L   = 2 * bx;
-    // 8x8: the lane's best SAD per block so far (the centre probe's, or none) and
-    // the (row, set) that produced it; the position inside that set is found
-    // once after the band (the set's SADs recomputed), so the set loop keeps one
-    // packed minimum per block instead of a key per position
-    uint32_t best8[2] = {b.b8t >> 16, b.b8b >> 16}, bpos[2] = {~0u, ~0u};
     for (int ty = y0; ty < y1; ty += 2) {
         const int tyh = min(ty + hr, y1 - 1); // an odd band: half 1 repeats the last row (same keys)
         for (int set = 0; set < nsets; set++) {
@@ -3108,23 +3128,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
             for (int blk = 0; blk < 2; blk++)
 #pragma unroll
                 for (int iq = 0; iq < FPW_TQ; iq++) acc[blk][iq] = 0;
-#pragma unroll
-            for (int blk = 0; blk < 2; blk++)
-#pragma unroll
-                for (int rr = 0; rr < ROWS; rr++) {
-                    const int ro = (tyh - Y0 + (2 * by2 + blk) * 8 + rr * RSTEP) * FPW_PITCH + L + tq;
-                    const uint2 *pa = (const uint2 *)(fw + ro), *pb = (const uint2 *)(fw + ro + FPW_BOFF);
-                    uint2 q[FPW_TQ + 1]; // q[j] = (A[j], A[j + 1])
-#pragma unroll
-                    for (int i = 0; i <= FPW_TQ / 2; i++) q[2 * i] = pa[i];
-#pragma unroll
-                    for (int i = 0; i < FPW_TQ / 2; i++) q[2 * i + 1] = pb[i];
-#pragma unroll
-                    for (int iq = 0; iq < FPW_TQ; iq++) {
-                        acc[blk][iq] = qsad(q[iq].x, q[iq].y, src[blk][rr][0], acc[blk][iq]);
-                        acc[blk][iq] = qsad(q[iq + 1].x, q[iq + 1].y, src[blk][rr][1], acc[blk][iq]);
-                    }
+            // the 8 rows (2 blocks x 4 sub-sampled rows) of the set, one row ahead
+            const uint32_t lb = fw_lds + 4u * (uint32_t)((tyh - Y0 + 2 * by2 * 8) * FPW_PITCH + L + tq);
+            FpwRow R[2];
+            fpw_row_issue<0>(R[0], lb);
+            fpw_sfor<0, 2 * ROWS>([&](auto G) {
+                constexpr int g = decltype(G)::value, blk = g / ROWS, rr = g % ROWS;
+                if constexpr (g + 1 < 2 * ROWS) {
+                    fpw_row_issue<g + 1>(R[(g + 1) & 1], lb);
+                    fpw_row_wait<5>(R[g & 1]);
+                } else {
+                    fpw_row_wait<0>(R[g & 1]);
                 }
+                const FpwRow &q = R[g & 1];
+#pragma unroll
+                for (int iq = 0; iq < FPW_TQ; iq++) {
+                    acc[blk][iq] = qsad(q.v[iq].x, q.v[iq].y, src[blk][rr][0], acc[blk][iq]);
+                    acc[blk][iq] = qsad(q.v[iq + 1].x, q.v[iq + 1].y, src[blk][rr][1], acc[blk][iq]);
+                }
+            });
             // the SADs exist here: otherwise the compiler sinks the qsads of the
             // later pairs into their (conditional) uses and keeps every row live
 #pragma unroll
@@ -3133,15 +3155,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
                 for (int iq = 0; iq < FPW_TQ; iq++) asm volatile("" : "+v"(acc[blk][iq]));
             FpW m{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
             const int left = w - 4 * tq; // positions of the area in this set (wave-uniform)
-            const uint32_t spos = ((uint32_t)tyh << 8) | (uint32_t)set;
-#pragma unroll
-            for (int blk = 0; blk < 2; blk++) {
-                const uint32_t m8 = left >= 4 * FPW_TQ ? fpw_set_min8<true>(acc[blk], left)
-                                                       : fpw_set_min8<false>(acc[blk], left);
-                // strictly below: an equal SAD of a later set never wins (raster order)
-                bpos[blk]  = m8 < best8[blk] ? spos : bpos[blk];
-                best8[blk] = min_u32(best8[blk], m8);
-            }
 #pragma unroll
             for (int pp = 0; pp < FPW_TQ / 2; pp++) {
                 const int ev = left - 8 * pp;
@@ -3156,54 +3169,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
             }
             const uint32_t ob = obase + (uint32_t)(tyh * w + 4 * tq);
             if (left >= 8) { // a whole first pair: every class of every lane has a key
+                b.b8t = min_u32(b.b8t, m.b8t + ob);
+                b.b8b = min_u32(b.b8b, m.b8b + ob);
                 b.b16 = min_u32(b.b16, m.b16 + ob + (uint32_t)p16);
                 b.b32 = min_u32(b.b32, m.b32 + ob + (uint32_t)p32);
                 b.b64 = min_u32(b.b64, m.b64 + ob + (uint32_t)p32);
             } else {
+                b.b8t = fpw_rebase(b.b8t, m.b8t, ob);
+                b.b8b = fpw_rebase(b.b8b, m.b8b, ob);
                 b.b16 = fpw_rebase(b.b16, m.b16, ob + (uint32_t)p16);
                 b.b32 = fpw_rebase(b.b32, m.b32, ob + (uint32_t)p32);
                 b.b64 = fpw_rebase(b.b64, m.b64, ob + (uint32_t)p32);
             }
         }
-    }
-    // the 8x8 keys: each block's best set searched again (this lane's rows and
-    // positions of it only), its first position holding the minimum
-#pragma unroll
-    for (int blk = 0; blk < 2; blk++) {
-        if (bpos[blk] == ~0u)
-            continue; // the centre probe (or nothing) stays
-        const int tyb = (int)(bpos[blk] >> 8), tqb = (int)(bpos[blk] & 0xFFu) * FPW_TQ;
-        unsigned long long a[FPW_TQ];
-#pragma unroll
-        for (int iq = 0; iq < FPW_TQ; iq++) a[iq] = 0;
-#pragma unroll
-        for (int rr = 0; rr < ROWS; rr++) {
-            const int ro = (tyb - Y0 + (2 * by2 + blk) * 8 + rr * RSTEP) * FPW_PITCH + L + tqb;
-            const uint2 *pa = (const uint2 *)(fw + ro), *pb = (const uint2 *)(fw + ro + FPW_BOFF);
-            uint2 q[FPW_TQ + 1];
-#pragma unroll
-            for (int i = 0; i <= FPW_TQ / 2; i++) q[2 * i] = pa[i];
-#pragma unroll
-            for (int i = 0; i < FPW_TQ / 2; i++) q[2 * i + 1] = pb[i];
-#pragma unroll
-            for (int iq = 0; iq < FPW_TQ; iq++) {
-                a[iq] = qsad(q[iq].x, q[iq].y, src[blk][rr][0], a[iq]);
-                a[iq] = qsad(q[iq + 1].x, q[iq + 1].y, src[blk][rr][1], a[iq]);
-            }
-        }
-        // the first position of the set with the minimum (positions past the area cannot
-        // hold it: the minimum came from a valid one, and a later equal one never wins)
-        uint32_t e8 = 4 * FPW_TQ;
-#pragma unroll
-        for (int e = 4 * FPW_TQ - 1; e >= 0; e--) {
-            const uint32_t v = (uint32_t)(a[e >> 2] >> (16 * (e & 3))) & 0xFFFFu;
-            e8               = v == best8[blk] && e < w - 4 * tqb ? (uint32_t)e : e8;
-        }
-        const uint32_t k = (best8[blk] << 16) | (obase + (uint32_t)(tyb * w + 4 * tqb) + e8);
-        if (blk == 0)
-            b.b8t = min_u32(b.b8t, k);
-        else
-            b.b8b = min_u32(b.b8b, k);
     }
     // both halves, then the lanes of each class
     b.b8t = fpw_min_hr(b.b8t), b.b8b = fpw_min_hr(b.b8b), b.b16 = fpw_min_hr(b.b16);
