@@ -3119,9 +3119,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
     const uint32_t sel32 = (c32 & 2) ? ((c32 & 1) ? 0x0C0C0706u : 0x0C0C0504u) : ((c32 & 1) ? 0x0C0C0302u : 0x0C0C0100u);
     const int p16 = bx & 1, p32 = c32 + 4 * (by2 & 1);
     const int L   = 2 * bx;
+    const int nwhole = w / (4 * FPW_TQ); // sets with all 16 positions inside the area
     for (int ty = y0; ty < y1; ty += 2) {
         const int tyh = min(ty + hr, y1 - 1); // an odd band: half 1 repeats the last row (same keys)
-        for (int set = 0; set < nsets; set++) {
+        // one set of 16 positions; WHOLE: all inside the area (every set of a 64-wide
+        // area), so the whole sets run one straight loop and the partial set apart
+        auto run_set = [&](const int set, auto WHOLE) {
             const int tq = set * FPW_TQ;
             unsigned long long acc[2][FPW_TQ];
 #pragma unroll
@@ -3155,20 +3158,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
                 for (int iq = 0; iq < FPW_TQ; iq++) asm volatile("" : "+v"(acc[blk][iq]));
             FpW m{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
             const int left = w - 4 * tq; // positions of the area in this set (wave-uniform)
+            const uint32_t ob = obase + (uint32_t)(tyh * w + 4 * tq);
+            if constexpr (decltype(WHOLE)::value) {
 #pragma unroll
-            for (int pp = 0; pp < FPW_TQ / 2; pp++) {
-                const int ev = left - 8 * pp;
-                if (ev <= 0)
-                    break;
-                if (ev >= 8)
+                for (int pp = 0; pp < FPW_TQ / 2; pp++)
                     fpw_pair<false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1], 8 * pp,
                                     8, sel16, sel32, p16, p32);
-                else
-                    fpw_pair<true>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1], 8 * pp,
-                                   ev + 8 * pp, sel16, sel32, p16, p32);
+            } else {
+#pragma unroll
+                for (int pp = 0; pp < FPW_TQ / 2; pp++) {
+                    const int ev = left - 8 * pp;
+                    if (ev <= 0)
+                        break;
+                    if (ev >= 8)
+                        fpw_pair<false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
+                                        8 * pp, 8, sel16, sel32, p16, p32);
+                    else
+                        fpw_pair<true>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
+                                       8 * pp, ev + 8 * pp, sel16, sel32, p16, p32);
+                }
             }
-            const uint32_t ob = obase + (uint32_t)(tyh * w + 4 * tq);
-            if (left >= 8) { // a whole first pair: every class of every lane has a key
+            if (decltype(WHOLE)::value || left >= 8) { // a whole first pair: every class of every lane has a key
                 b.b8t = min_u32(b.b8t, m.b8t + ob);
                 b.b8b = min_u32(b.b8b, m.b8b + ob);
                 b.b16 = min_u32(b.b16, m.b16 + ob + (uint32_t)p16);
@@ -3181,7 +3191,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
                 b.b32 = fpw_rebase(b.b32, m.b32, ob + (uint32_t)p32);
                 b.b64 = fpw_rebase(b.b64, m.b64, ob + (uint32_t)p32);
             }
-        }
+        };
+        for (int set = 0; set < nwhole; set++) run_set(set, std::true_type());
+        if (nwhole < nsets)
+            run_set(nwhole, std::false_type());
     }
     // both halves, then the lanes of each class
     b.b8t = fpw_min_hr(b.b8t), b.b8b = fpw_min_hr(b.b8b), b.b16 = fpw_min_hr(b.b16);
