@@ -3122,9 +3122,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
     const int nwhole = w / (4 * FPW_TQ); // sets with all 16 positions inside the area
     for (int ty = y0; ty < y1; ty += 2) {
         const int tyh = min(ty + hr, y1 - 1); // an odd band: half 1 repeats the last row (same keys)
-        // one set of 16 positions; WHOLE: all inside the area (every set of a 64-wide
-        // area), so the whole sets run one straight loop and the partial set apart
-        auto run_set = [&](const int set, auto WHOLE) {
+        // one set of 16 positions into the set minima m (orders EOFF + position in the
+        // set); WHOLE: all inside the area (every set of a 64-wide area), so the whole
+        // sets run one straight loop, two sets per fold into the running minima, and
+        // the partial set apart
+        auto run_set = [&](const int set, FpW &m, auto EOFF, auto WHOLE) {
             const int tq = set * FPW_TQ;
             unsigned long long acc[2][FPW_TQ];
 #pragma unroll
@@ -3156,14 +3158,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
             for (int blk = 0; blk < 2; blk++)
 #pragma unroll
                 for (int iq = 0; iq < FPW_TQ; iq++) asm volatile("" : "+v"(acc[blk][iq]));
-            FpW m{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
             const int left = w - 4 * tq; // positions of the area in this set (wave-uniform)
-            const uint32_t ob = obase + (uint32_t)(tyh * w + 4 * tq);
             if constexpr (decltype(WHOLE)::value) {
 #pragma unroll
                 for (int pp = 0; pp < FPW_TQ / 2; pp++)
-                    fpw_pair<false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1], 8 * pp,
-                                    8, sel16, sel32, p16, p32);
+                    fpw_pair<false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
+                                    decltype(EOFF)::value + 8 * pp, 8, sel16, sel32, p16, p32);
             } else {
 #pragma unroll
                 for (int pp = 0; pp < FPW_TQ / 2; pp++) {
@@ -3178,7 +3178,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
                                        8 * pp, ev + 8 * pp, sel16, sel32, p16, p32);
                 }
             }
-            if (decltype(WHOLE)::value || left >= 8) { // a whole first pair: every class of every lane has a key
+        };
+        // the set minima (orders from set tq's first position) into the running minima
+        auto fold = [&](const FpW &m, const int tq, const bool keyed) {
+            const uint32_t ob = obase + (uint32_t)(tyh * w + 4 * tq);
+            if (keyed) { // a whole first pair: every class of every lane has a key
                 b.b8t = min_u32(b.b8t, m.b8t + ob);
                 b.b8b = min_u32(b.b8b, m.b8b + ob);
                 b.b16 = min_u32(b.b16, m.b16 + ob + (uint32_t)p16);
@@ -3192,9 +3196,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
                 b.b64 = fpw_rebase(b.b64, m.b64, ob + (uint32_t)p32);
             }
         };
-        for (int set = 0; set < nwhole; set++) run_set(set, std::true_type());
-        if (nwhole < nsets)
-            run_set(nwhole, std::false_type());
+        using I0  = std::integral_constant<int, 0>;
+        using I16 = std::integral_constant<int, 4 * FPW_TQ>;
+        int set = 0;
+        for (; set + 2 <= nwhole; set += 2) {
+            FpW m{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            run_set(set, m, I0(), std::true_type());
+            run_set(set + 1, m, I16(), std::true_type());
+            fold(m, set * FPW_TQ, true);
+        }
+        if (set < nwhole) {
+            FpW m{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            run_set(set, m, I0(), std::true_type());
+            fold(m, set * FPW_TQ, true);
+        }
+        if (nwhole < nsets) {
+            FpW m{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            run_set(nwhole, m, I0(), std::false_type());
+            fold(m, nwhole * FPW_TQ, w - 4 * nwhole * FPW_TQ >= 8);
+        }
     }
     // both halves, then the lanes of each class
     b.b8t = fpw_min_hr(b.b8t), b.b8b = fpw_min_hr(b.b8b), b.b16 = fpw_min_hr(b.b16);
