@@ -258,6 +258,23 @@ def test_banded_fullpel_variance_parity(svtme, gpu, area, th, k32):
     assert not _controls_case(S, gpu, ctrl, 640, 360, (7, 6), (9,))
 
 
+@pytest.mark.parametrize("width", [24, 28, 40, 44, 56, 76])
+def test_fp_wide_set_split_parity(svtme, gpu, width):
+    """k_fp_wide's set loop at area widths that end its 16-position sets in every
+    way: whole sets folded two at a time, a lone whole set, and a partial set of
+    a whole pair (8 positions), of a whole and a masked pair (12) or none."""
+    S = svtme
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(640, 360), 1)
+    ctrl.me_sa.sa_min.width = ctrl.me_sa.sa_max.width = width
+    ctrl.me_sa.sa_min.height = ctrl.me_sa.sa_max.height = 48
+    ctrl.me_8x8_var_enabled = 0
+    ctrl.enable_me_sr_adjustment = 0
+    lib = S.load_product()
+    lib.svtme_fp_wide_lds.restype = C.c_bool
+    assert lib.svtme_fp_wide_lds(C.byref(ctrl)), "the case must run k_fp_wide"
+    assert not _controls_case(S, gpu, ctrl, 640, 360, (7, 6), (9,))
+
+
 def test_picture_release_while_read(svtme, gpu):
     """svtme_picture_release does not wait for the device: a job queued before the
     release still reads the released reference (its memory is freed, or reused by
