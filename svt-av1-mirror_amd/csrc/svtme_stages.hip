@@ -1098,6 +1098,27 @@ __device__ unsigned long long g_hme_stamps[1 << 17][16];
         if ((k) == SVTME_STOP_AFTER)                                                                                   \
             return;                                                                                                    \
     } while (0)
+#elif defined(SVTME_CLOCKBINS) // diagnostic build (scripts/clock_probe.py): in-kernel clock over time
+// thread 0 of every k_hme workgroup adds its shader cycles (s_memtime) and its
+// 100 MHz real-time ticks (s_memrealtime) from start to end into the bin of its
+// start time (2^13 ticks = 81.92 us per bin, 4096 bins = 335 ms before wrapping):
+// cycles / ticks x 100 MHz is the clock the workgroups ran at in that bin
+__device__ unsigned long long g_clock_bins[4096][3];
+#define HME_STAMP(k)                                                                                                   \
+    do {                                                                                                               \
+        if (threadIdx.x == 0) {                                                                                        \
+            if ((k) == 0) {                                                                                            \
+                clk_c0 = __builtin_readcyclecounter();                                                                 \
+                clk_r0 = __builtin_amdgcn_s_memrealtime();                                                             \
+            } else if ((k) == 7) {                                                                                     \
+                const unsigned long long c1 = __builtin_readcyclecounter(), r1 = __builtin_amdgcn_s_memrealtime();     \
+                const int bin = (int)((clk_r0 >> 13) & 4095);                                                          \
+                atomicAdd(&g_clock_bins[bin][0], c1 - clk_c0);                                                         \
+                atomicAdd(&g_clock_bins[bin][1], r1 - clk_r0);                                                         \
+                atomicAdd(&g_clock_bins[bin][2], 1ull);                                                                \
+            }                                                                                                          \
+        }                                                                                                              \
+    } while (0)
 #else
 #define HME_STAMP(k)
 #endif
@@ -3864,6 +3885,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     const int kh  = (int)(G.bh >> 2) >> 1; // 1/16 block rows (sub)
     const int kh1 = (int)(G.bh >> 2);      // 1/4 block rows (sub): (bh / 2) / 2
     const bool zz_on = c.me_early_exit_th || c.me_safe_limit_zz_th;
+#ifdef SVTME_CLOCKBINS
+    unsigned long long clk_c0 = 0, clk_r0 = 0;
+#endif
     HME_STAMP(0);
 
     // ---- phase 0 (independent work of all waves):
@@ -4298,6 +4322,11 @@ extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks)
     if (nblocks > (1u << 17))
         nblocks = 1u << 17;
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 16 * sizeof(unsigned long long));
+}
+#endif
+#ifdef SVTME_CLOCKBINS
+extern "C" int svtme_debug_clock_bins(unsigned long long *out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clock_bins), sizeof(g_clock_bins));
 }
 #endif
 
