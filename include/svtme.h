@@ -287,6 +287,20 @@ svtme_status svtme_picture_upload_10bit(svtme_ctx *ctx, uint64_t picture_number,
  * picture finish before it is overwritten. */
 svtme_status svtme_picture_upload_async(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *y, uint32_t stride,
                                         uint32_t width, uint32_t height);
+/* Asynchronous upload from PAGEABLE memory the library never page-locks (an
+ * encoder's own picture buffers): the calling thread copies the w x h samples
+ * into a page-locked staging buffer the library owns (a ring of
+ * SVTME_UPLOAD_SLOTS, each reused once its DMA has run), outside the context
+ * lock, then the DMA and the pyramid build are queued as in
+ * svtme_picture_upload_async; `y` may change as soon as the call returns.
+ * Page-locking the caller's memory instead (svtme_host_register) makes it a
+ * driver user-pointer mapping, which the kernel may invalidate at any time
+ * (NUMA balancing, page migration, compaction); every invalidation evicts the
+ * process's GPU queues until the mapping is rebuilt -- a stall of the work in
+ * flight. */
+#define SVTME_UPLOAD_SLOTS 4
+svtme_status svtme_picture_upload_copy_async(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *y,
+                                             uint32_t stride, uint32_t width, uint32_t height);
 /* Same, from a DEVICE pointer already in HBM (no PCIe). */
 svtme_status svtme_picture_upload_device(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *d_y,
                                          uint32_t stride, uint32_t width, uint32_t height);
@@ -361,11 +375,23 @@ void *svtme_lane_stream(svtme_ctx *ctx, uint32_t lane);
  * (sb_count x svtme_packed_sb_bytes(layout, R) bytes) on the context's download
  * stream, overlapping later jobs. Returns at once with *ticket. host_out should
  * be page-locked (svtme_host_alloc): a pageable destination makes the copy
- * synchronous. At most SVTME_MAX_TICKETS tickets are outstanding; a submission
- * beyond that is refused. */
-#define SVTME_MAX_TICKETS 16
+ * synchronous. At most SVTME_MAX_TICKETS tickets are outstanding (the
+ * reference runs up to 25 ME threads and the TF threads beside them, one job in
+ * flight each, enc_handle.c:744-773). A submission that finds every slot taken
+ * waits for svtme_ticket_wait (another thread's) to retire one; it is refused
+ * (SVTME_ERR_INSUFFICIENT_RESOURCES) only when no ticket is retired within
+ * 100 ms while none is being waited on -- the caller holds them itself. */
+#define SVTME_MAX_TICKETS 64
 svtme_status svtme_submit_picture_packed_async(svtme_ctx *ctx, uint32_t lane, const svtme_job *job,
                                                const svtme_pack_layout *layout, void *host_out, uint64_t *ticket);
+/* The same for n jobs (1 .. SVTME_MAX_BATCH_JOBS) in ONE batched launch: the
+ * temporal filter's (central picture, reference) pairs of one window, all
+ * known at its first ME call (temporal_filtering.c:3029-3030, 3096). Job k's
+ * output goes to host_outs[k] under tickets[k]; each ticket is waited for and
+ * retired on its own. */
+svtme_status svtme_submit_pictures_packed_async(svtme_ctx *ctx, uint32_t lane, uint32_t n, const svtme_job *jobs,
+                                                const svtme_pack_layout *layouts, void *const *host_outs,
+                                                uint64_t *tickets);
 /* Block until ticket's packed output is in host memory, then retire the ticket.
  * Safe to call from any thread, without holding anything the submitter holds. */
 svtme_status svtme_ticket_wait(svtme_ctx *ctx, uint64_t ticket);
@@ -383,6 +409,12 @@ svtme_status svtme_host_unregister(void *p);
  * reference slots and any pack layout. Submissions within those bounds then
  * allocate nothing (a job beyond them still grows the buffers it needs). */
 svtme_status svtme_reserve(svtme_ctx *ctx, uint32_t width, uint32_t height, uint32_t max_refs, uint32_t tickets);
+/* Keep `count` picture buffers of a width x height picture (its three padded
+ * planes) in the context's free pool, so that the uploads of up to that many
+ * pictures beyond the resident ones allocate no device memory. Released
+ * pictures' buffers return to the pool once the work reading them has run
+ * (never hipFree on the steady path: it serialises the device). */
+svtme_status svtme_reserve_pictures(svtme_ctx *ctx, uint32_t width, uint32_t height, uint32_t count);
 /* Kernel timing with HIP events on the context's stream, recorded around every
  * stage launch of every submission while enabled (enable = 1). svtme_timing_read
  * waits for the recorded launch groups and returns the milliseconds of stage 0

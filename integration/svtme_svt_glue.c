@@ -39,12 +39,11 @@
  *                                  function (the fallback).
  *   Linking with -Wl,--wrap=svt_aom_motion_estimation_b64
  *   -Wl,--wrap=svt_aom_downsample_filtering_input_picture
- *   -Wl,--wrap=svt_aom_picture_analysis_result_creator
- *   -Wl,--wrap=svt_post_full_object -Wl,--wrap=svt_av1_enc_deinit and
- *   -DSVTME_GLUE_WRAP routes both call sites of the SB function, every
- *   re-decimation outside pic_analysis_process.c, the end of each picture's
- *   analysis and the encoder's teardown through this file without editing the
- *   encoder's sources.
+ *   -Wl,--wrap=svt_post_full_object -Wl,--wrap=svt_av1_enc_init
+ *   -Wl,--wrap=svt_av1_enc_deinit and -DSVTME_GLUE_WRAP routes both call sites
+ *   of the SB function, every re-decimation outside pic_analysis_process.c,
+ *   the end of each picture's analysis and each encoder's set-up and teardown
+ *   through this file without editing the encoder's sources.
  *
  * Parity / debug mode
  *   svt_aom_setup_rtcd_hip_parity() registers the per-kernel *_hip rtcd variants
@@ -68,7 +67,11 @@
  * buffers (registrations, register_ms) and the one-off pool fill (prefill_ms); and
  * the rtcd check: how many of the pointers parity mode replaces changed since
  * the first SB call, and how many point at this file's HIP wrappers);
- * SVTME_GLUE_RESIDENT caps the resident pictures (default 128).
+ * SVTME_GLUE_RESIDENT caps the resident pictures (default 128); SVTME_GLUE_PIN=1
+ * page-locks the encoder's picture buffers and uploads straight from them
+ * instead of through the library's page-locked staging (see
+ * svtme_picture_upload_copy_async: a page-locked user buffer is a driver
+ * user-pointer mapping whose invalidations stall the GPU queues).
  */
 #include <pthread.h>
 #include <stddef.h>
@@ -85,6 +88,9 @@
 #include "pic_analysis_results.h"
 #include "reference_object.h"
 #include "sequence_control_set.h"
+#ifdef SVTME_GLUE_WRAP
+#include "enc_handle.h"
+#endif
 
 #include "svtme.h"
 
@@ -101,6 +107,8 @@ void svtme_scatter_sb(PictureParentControlSet *pcs, MeContext *me, uint32_t b64_
                       uint32_t b64_origin_y, const svtme_job *job, const svtme_pack_layout *layout,
                       const uint8_t *packed_sb);
 
+void svtme_glue_release_encoder(const void *enc_ctx);
+
 #ifdef SVTME_GLUE_WRAP
 EbErrorType __real_svt_aom_motion_estimation_b64(PictureParentControlSet *, uint32_t, uint32_t, uint32_t,
                                                  MeContext *, EbPictureBufferDesc *);
@@ -112,6 +120,60 @@ EbErrorType svt_aom_motion_estimation_b64(PictureParentControlSet *, uint32_t, u
                                           EbPictureBufferDesc *);
 #define SVTME_ENCODER_ME_B64 svt_aom_motion_estimation_b64
 #endif
+
+/* ==========================================================================
+ * Encoder instances. Each encoder in the process (the channels of --nch, the
+ * passes of a multi-pass encode, an application's own instances) gets a range
+ * of its own in the library's picture numbers: its numbers + (slot << 48). Two
+ * encoders then never share a resident picture, and one encoder's teardown
+ * drops exactly its pictures, jobs and page-locked buffers. An encoder is
+ * known by the EncodeContext every copy of its SequenceControlSet points to
+ * (pcs->scs->enc_ctx: the copies of resource_coordination_process.c:907-938 are
+ * struct copies, sequence_control_set.c:297); svt_av1_enc_init's wrap adds its
+ * picture-analysis results resource (enc_handle.h:105), which marks the end of
+ * each picture's analysis in svt_post_full_object.
+ * ======================================================================== */
+#define GLUE_MAX_ENC 64
+#define GLUE_NS_SHIFT 48
+#define GLUE_PN_MASK ((1ull << GLUE_NS_SHIFT) - 1)
+typedef struct GlueEnc {
+    const void *enc_ctx; /* NULL: a free slot */
+    const void *pa_res;  /* its picture-analysis results resource, or NULL */
+} GlueEnc;
+static GlueEnc g_enc[GLUE_MAX_ENC];
+static pthread_mutex_t g_enc_mu = PTHREAD_MUTEX_INITIALIZER;
+static unsigned long long g_n_encoders, g_n_released; /* slots taken; pictures released at teardowns (g_enc_mu) */
+
+/* the slot of an encoder, taken on first sight; -1 when every slot is taken */
+static int enc_slot(const void *enc_ctx, const void *pa_res) {
+    if (!enc_ctx)
+        return -1;
+    for (int i = 0; i < GLUE_MAX_ENC; i++)
+        if (__atomic_load_n(&g_enc[i].enc_ctx, __ATOMIC_ACQUIRE) == enc_ctx && !pa_res)
+            return i;
+    pthread_mutex_lock(&g_enc_mu);
+    int k = -1;
+    for (int i = 0; i < GLUE_MAX_ENC && k < 0; i++)
+        if (g_enc[i].enc_ctx == enc_ctx)
+            k = i;
+    for (int i = 0; i < GLUE_MAX_ENC && k < 0; i++)
+        if (!g_enc[i].enc_ctx) {
+            k = i;
+            __atomic_store_n(&g_enc[i].enc_ctx, enc_ctx, __ATOMIC_RELEASE);
+            g_n_encoders++;
+        }
+    if (k >= 0 && pa_res)
+        __atomic_store_n(&g_enc[k].pa_res, pa_res, __ATOMIC_RELEASE);
+    pthread_mutex_unlock(&g_enc_mu);
+    return k;
+}
+
+static int pcs_slot(const PictureParentControlSet *pcs) {
+    return enc_slot(pcs->scs ? (const void *)pcs->scs->enc_ctx : NULL, NULL);
+}
+
+/* the library's number of picture pn of the encoder in `slot` */
+static uint64_t ns_pn(int slot, uint64_t pn) { return ((uint64_t)(slot < 0 ? 0 : slot) << GLUE_NS_SHIFT) | pn; }
 
 /* ==========================================================================
  * rtcd registration, parity / debug mode only
@@ -354,14 +416,16 @@ static uint32_t align8(uint32_t v) { return (v + 7u) & ~7u; }
  * me_process.c:248-262 before the call). */
 void svtme_job_from_pcs(svtme_job *job, const PictureParentControlSet *pcs, const MeContext *me) {
     memset(job, 0, sizeof(*job));
-    job->picture_number = pcs->picture_number;
+    const int slot      = pcs_slot(pcs); /* the encoder's picture-number range */
+    job->picture_number = ns_pn(slot, pcs->picture_number);
     job->width          = pcs->aligned_width;
     job->height         = pcs->aligned_height;
     job->num_lists      = me->num_of_list_to_search;
     job->num_refs[0]    = me->num_of_ref_pic_to_search[0];
     job->num_refs[1]    = job->num_lists == 2 ? me->num_of_ref_pic_to_search[1] : 0;
     for (int l = 0; l < job->num_lists; l++)
-        for (int r = 0; r < job->num_refs[l]; r++) job->ref_picture_number[l][r] = me->me_ds_ref_array[l][r].picture_number;
+        for (int r = 0; r < job->num_refs[l]; r++)
+            job->ref_picture_number[l][r] = ns_pn(slot, me->me_ds_ref_array[l][r].picture_number);
     job->temporal_layer_index            = me->temporal_layer_index;
     job->is_ref                          = me->is_ref;
     job->hierarchical_levels             = pcs->hierarchical_levels;
@@ -385,12 +449,13 @@ void svtme_job_from_pcs(svtme_job *job, const PictureParentControlSet *pcs, cons
 void svtme_job_from_tf(svtme_job *job, const PictureParentControlSet *centre, const MeContext *me,
                        const EbPictureBufferDesc *input_ptr) {
     memset(job, 0, sizeof(*job));
-    job->picture_number        = centre->picture_number;
+    const int slot             = pcs_slot(centre);
+    job->picture_number        = ns_pn(slot, centre->picture_number);
     job->width                 = align8(input_ptr->width); /* motion_estimation.c:3093-3094 */
     job->height                = align8(input_ptr->height);
     job->num_lists             = 1;
     job->num_refs[0]           = 1;
-    job->ref_picture_number[0][0] = me->me_ds_ref_array[0][0].picture_number;
+    job->ref_picture_number[0][0] = ns_pn(slot, me->me_ds_ref_array[0][0].picture_number);
     job->temporal_layer_index  = me->temporal_layer_index;
     job->is_ref                = me->is_ref;
     job->hierarchical_levels   = centre->hierarchical_levels;
@@ -553,6 +618,7 @@ typedef struct GlueBuf {
 typedef struct GlueReg { /* an encoder picture span page-locked for uploads */
     const void *p;
     uint64_t bytes;
+    int slot; /* the encoder whose buffer it is */
 } GlueReg;
 
 typedef struct GlueTrace { /* one job (SVTME_GLUE_TRACE) */
@@ -575,7 +641,7 @@ static struct {
     pthread_mutex_t gpu; /* one thread uploads / submits at a time (not held while waiting) */
     pthread_mutex_t reg; /* the page-locked encoder buffers (regs) */
     svtme_ctx *ctx;
-    int strict, verify, eager, max_resident;
+    int strict, verify, eager, pin, tf_batch, max_resident;
     const char *stats_path, *trace_path;
     GlueTrace *trace;
     uint32_t n_trace, cap_trace;
@@ -595,6 +661,7 @@ static struct {
     struct {
         unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
         unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job, registrations;
+        unsigned long long tf_batched, unused_jobs, launches;
         double upload_s, submit_s, wait_s, job_s, busy_s, eager_s, prefill_s, register_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER,
@@ -608,10 +675,21 @@ static void glue_trace_at_exit(void) {
         const GlueTrace *t = &G.trace[i];
         fprintf(f, "{\"pn\": %llu, \"tf\": %d, \"sbs\": %u, \"inflight\": %u, \"uploads\": %u, "
                    "\"upload_ms\": %.4f, \"create_ms\": %.4f, \"submitted_ms\": %.4f, \"done_ms\": %.4f}\n",
-                (unsigned long long)t->pn, t->tf, t->n_sb, t->inflight, t->uploads, 1e3 * t->upload_s,
+                (unsigned long long)(t->pn & GLUE_PN_MASK), t->tf, t->n_sb, t->inflight, t->uploads, 1e3 * t->upload_s,
                 1e3 * (t->t_create - G.t0), 1e3 * (t->t_submitted - G.t0), 1e3 * (t->t_done - G.t0));
     }
     fclose(f);
+}
+
+/* one trace line (G.mu held) */
+static void trace_add(const GlueTrace *t) {
+    if (G.n_trace == G.cap_trace) {
+        G.cap_trace = G.cap_trace ? 2 * G.cap_trace : 256;
+        G.trace     = (GlueTrace *)realloc(G.trace, G.cap_trace * sizeof(GlueTrace));
+        if (!G.trace)
+            abort();
+    }
+    G.trace[G.n_trace++] = *t;
 }
 
 static void glue_stats_at_exit(void) {
@@ -637,12 +715,14 @@ static void glue_stats_at_exit(void) {
             "\"job_sbs\": %llu, \"max_inflight\": %llu, \"upload_ms\": %.3f, \"submit_ms\": %.3f, \"wait_ms\": %.3f, "
             "\"job_latency_ms\": %.4f, \"busy_ms\": %.3f, \"served_sb_per_s\": %.1f, \"eager_uploads\": %llu, "
             "\"eager_upload_ms\": %.3f, \"served_sb_per_s_with_uploads\": %.1f, \"prefill_ms\": %.3f, "
-            "\"registrations\": %llu, \"register_ms\": %.3f}\n",
+            "\"registrations\": %llu, \"register_ms\": %.3f, \"encoders\": %llu, \"released_at_teardown\": %llu, "
+            "\"tf_batched\": %llu, \"unused_jobs\": %llu, \"launches\": %llu}\n",
             G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
             G.n.evictions, G.n.verified, G.n.verified_job, G.n.stale, G.n.unpinned, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
             G.n.max_inflight, 1e3 * G.n.upload_s, 1e3 * G.n.submit_s, 1e3 * G.n.wait_s,
             jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate, G.n.eager_uploads, 1e3 * G.n.eager_s,
-            rate_up, 1e3 * G.n.prefill_s, G.n.registrations, 1e3 * G.n.register_s);
+            rate_up, 1e3 * G.n.prefill_s, G.n.registrations, 1e3 * G.n.register_s, g_n_encoders, g_n_released,
+            G.n.tf_batched, G.n.unused_jobs, G.n.launches);
     fclose(f);
 }
 
@@ -652,6 +732,8 @@ static void glue_init(void) {
     G.strict       = (e = getenv("SVTME_GLUE_STRICT")) && atoi(e);
     G.verify       = (e = getenv("SVTME_GLUE_VERIFY")) && atoi(e);
     G.eager        = !(e = getenv("SVTME_GLUE_EAGER")) || atoi(e);
+    G.pin          = (e = getenv("SVTME_GLUE_PIN")) && atoi(e);
+    G.tf_batch     = !(e = getenv("SVTME_GLUE_TF_BATCH")) || atoi(e);
     G.max_resident = (e = getenv("SVTME_GLUE_RESIDENT")) ? atoi(e) : 128;
     if (G.max_resident < 9)
         G.max_resident = 9; /* a job names at most 1 + 8 pictures */
@@ -688,6 +770,7 @@ static size_t buf_worst(uint32_t n_sb) {
 }
 
 #define GLUE_POOL_BATCH 6 /* buffers page-locked together when the pool runs dry */
+#define GLUE_RESERVED_PICS 64 /* picture buffers reserved on the device ahead of the first job */
 
 /* Ahead of the first job (called once, from the first picture-analysis upload,
  * no glue lock held): page-lock a batch of worst-case output buffers for the
@@ -705,6 +788,8 @@ static void buf_prefill(uint32_t w, uint32_t h) {
         if (!(b[n] = (uint8_t *)svtme_host_alloc(sz)))
             break;
     (void)svtme_reserve(G.ctx, w, h, 8, GLUE_POOL_BATCH);
+    /* device memory for the first pictures: their uploads allocate nothing */
+    (void)svtme_reserve_pictures(G.ctx, w, h, G.max_resident < GLUE_RESERVED_PICS ? G.max_resident : GLUE_RESERVED_PICS);
     pthread_mutex_lock(&G.mu);
     for (int k = 0; k < n; k++) {
         if (G.n_pool < sizeof(G.pool) / sizeof(G.pool[0])) {
@@ -801,7 +886,7 @@ static int verify_level(uint64_t pn, int level, const EbPictureBufferDesc *d) {
  * thread of a new buffer does not hold up job submissions). svtme_glue_release
  * (called by the svt_av1_enc_deinit wrap) unlocks them all before the encoder
  * frees them. */
-static void pin_span(const void *p, uint64_t bytes) {
+static void pin_span(const void *p, uint64_t bytes, int slot) {
     pthread_mutex_lock(&G.reg);
     for (uint32_t i = 0; i < G.n_regs; i++)
         if (G.regs[i].p == p) {
@@ -822,7 +907,7 @@ static void pin_span(const void *p, uint64_t bytes) {
     }
     const double t0 = now_s();
     if (svtme_host_register((void *)p, bytes) == SVTME_OK) {
-        G.regs[G.n_regs].p = p, G.regs[G.n_regs].bytes = bytes;
+        G.regs[G.n_regs].p = p, G.regs[G.n_regs].bytes = bytes, G.regs[G.n_regs].slot = slot;
         G.n_regs++;
     } else
         G.n.unpinned++;
@@ -837,18 +922,73 @@ static const uint8_t *span_of(const EbPictureBufferDesc *full, uint32_t w, uint3
     return full->buffer_y + (size_t)full->org_y * full->stride_y + full->org_x;
 }
 
-/* Unlock every page-locked encoder buffer (after the uploads reading them have run) */
-void svtme_glue_release(void) {
+/* An encoder's teardown (the svt_av1_enc_deinit wrap, before the encoder frees
+ * its buffers): once the work queued for it has run, unlock its page-locked
+ * buffers, release its resident pictures, drop its finished jobs and free its
+ * slot, so that a later encoder (the next pass, another channel) starts from
+ * nothing of it. slot < 0: every encoder. */
+static void job_free(GlueJob *j);
+static void job_unlink(GlueJob *j);
+static void release_slot(int slot) {
     if (!G.ctx)
         return;
     pthread_mutex_lock(&G.gpu);
     pthread_mutex_lock(&G.reg);
-    if (G.n_regs)
-        svtme_sync(G.ctx);
-    for (uint32_t i = 0; i < G.n_regs; i++) svtme_host_unregister((void *)G.regs[i].p);
-    G.n_regs = 0;
+    svtme_sync(G.ctx);
+    for (uint32_t i = 0; i < G.n_regs;) {
+        if (slot < 0 || G.regs[i].slot == slot) {
+            svtme_host_unregister((void *)G.regs[i].p);
+            G.regs[i] = G.regs[--G.n_regs];
+        } else
+            i++;
+    }
     pthread_mutex_unlock(&G.reg);
+    unsigned long long released = 0;
+    for (uint32_t i = 0; i < G.n_pics;) {
+        if (slot < 0 || (int)(G.pics[i].pn >> GLUE_NS_SHIFT) == slot) {
+            svtme_picture_release(G.ctx, G.pics[i].pn);
+            G.pics[i] = G.pics[--G.n_pics];
+            released++;
+        } else
+            i++;
+    }
+    pthread_mutex_lock(&g_enc_mu);
+    g_n_released += released;
+    pthread_mutex_unlock(&g_enc_mu);
     pthread_mutex_unlock(&G.gpu);
+    pthread_mutex_lock(&G.mu);
+    for (GlueJob *j = G.jobs, *nx; j; j = nx) {
+        nx = j->next;
+        if ((slot < 0 || (int)(j->job.picture_number >> GLUE_NS_SHIFT) == slot) && j->users == 0 && j->state != 0) {
+            job_unlink(j);
+            job_free(j);
+        }
+    }
+    pthread_mutex_unlock(&G.mu);
+}
+
+void svtme_glue_release(void) {
+    release_slot(-1);
+    pthread_mutex_lock(&g_enc_mu);
+    for (int i = 0; i < GLUE_MAX_ENC; i++) {
+        __atomic_store_n(&g_enc[i].pa_res, NULL, __ATOMIC_RELEASE);
+        __atomic_store_n(&g_enc[i].enc_ctx, NULL, __ATOMIC_RELEASE);
+    }
+    pthread_mutex_unlock(&g_enc_mu);
+}
+
+void svtme_glue_release_encoder(const void *enc_ctx) {
+    int slot = -1;
+    for (int i = 0; i < GLUE_MAX_ENC && enc_ctx; i++)
+        if (__atomic_load_n(&g_enc[i].enc_ctx, __ATOMIC_ACQUIRE) == enc_ctx)
+            slot = i;
+    if (slot < 0)
+        return;
+    release_slot(slot);
+    pthread_mutex_lock(&g_enc_mu);
+    __atomic_store_n(&g_enc[slot].pa_res, NULL, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_enc[slot].enc_ctx, NULL, __ATOMIC_RELEASE);
+    pthread_mutex_unlock(&g_enc_mu);
 }
 
 /* SVTME_GLUE_VERIFY: the resident pyramid of pn equals the encoder's three planes (aborts if not) */
@@ -886,11 +1026,21 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
     }
     uint64_t span;
     const uint8_t *y = span_of(full, w, h, &span);
-    pin_span(y, span); /* (locked already when the caller pinned it first) */
-    const double t0 = now_s();
-    if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
-        return -1;
-    G.n.upload_s += now_s() - t0;
+    const double t0  = now_s();
+    if (G.pin) { /* SVTME_GLUE_PIN=1: page-lock the encoder's buffer, one DMA straight from it */
+        pin_span(y, span, (int)(pn >> GLUE_NS_SHIFT)); /* (locked already when the caller pinned it first) */
+        if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
+            return -1;
+    } else if (svtme_picture_upload_copy_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
+        return -1; /* (the rows go through the library's own page-locked staging) */
+    const double t1 = now_s();
+    G.n.upload_s += t1 - t0;
+    if (G.trace_path) { /* uploads in the trace too (tf = 2), to place them beside the jobs */
+        const GlueTrace t = {pn & GLUE_PN_MASK, 2, 0, 0, 1, t0, t1, t1, t1 - t0};
+        pthread_mutex_lock(&G.mu);
+        trace_add(&t);
+        pthread_mutex_unlock(&G.mu);
+    }
     if (G.verify)
         verify_pic(pn, full, quarter, sixteenth, &G.n.verified);
     if (!p) {
@@ -918,6 +1068,8 @@ static int job_names(const svtme_job *job, uint64_t pn) {
 }
 
 static void job_free(GlueJob *j) { /* G.mu held, j already unlinked */
+    if (j->served == 0 && j->state == 1)
+        G.n.unused_jobs++; /* a batched TF pair the encoder never asked for */
     buf_give(j);
     free(j);
 }
@@ -955,14 +1107,17 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     const int eager = G.eager && full && pa && full->buffer_y == pa->buffer_y && full->stride_y == pa->stride_y &&
         full->org_x == pa->org_x && full->org_y == pa->org_y && pcs->aligned_width && pcs->aligned_height &&
         !pcs->frame_superres_enabled && !pcs->frame_resize_enabled;
-    if (eager) { /* page-lock a new buffer (timed as register_ms) and fill the pools before taking G.gpu */
-        uint64_t span;
-        const uint8_t *y = span_of(pa, pcs->aligned_width, pcs->aligned_height, &span);
-        pin_span(y, span);
+    if (eager) { /* (SVTME_GLUE_PIN=1: page-lock a new buffer, timed as register_ms) fill the pools before taking G.gpu */
+        if (G.pin) {
+            uint64_t span;
+            const uint8_t *y = span_of(pa, pcs->aligned_width, pcs->aligned_height, &span);
+            pin_span(y, span, pcs_slot(pcs));
+        }
         buf_prefill(pcs->aligned_width, pcs->aligned_height); /* (once; timed as prefill_ms) */
     }
+    const uint64_t pn = ns_pn(pcs_slot(pcs), pcs->picture_number);
     pthread_mutex_lock(&G.gpu);
-    GluePic *p = pic_find(pcs->picture_number);
+    GluePic *p = pic_find(pn);
     if (p && !p->dirty) {
         p->dirty = 1;
         G.n.invalidations++;
@@ -970,8 +1125,8 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     if (eager) {
         const double t0 = now_s();
         const EbPaReferenceObject *o = pa_object(pcs);
-        uint64_t pin[9] = {pcs->picture_number};
-        if (pic_ensure(pcs->picture_number, pa, o->quarter_downsampled_picture_ptr, o->sixteenth_downsampled_picture_ptr,
+        uint64_t pin[9] = {pn};
+        if (pic_ensure(pn, pa, o->quarter_downsampled_picture_ptr, o->sixteenth_downsampled_picture_ptr,
                        pcs->aligned_width, pcs->aligned_height, pin, 1) == 0)
             G.n.eager_uploads++;
         G.n.eager_s += now_s() - t0;
@@ -980,7 +1135,7 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     pthread_mutex_lock(&G.mu);
     for (GlueJob *j = G.jobs, *nx; j; j = nx) {
         nx = j->next;
-        if (j->stale || !job_names(&j->job, pcs->picture_number))
+        if (j->stale || !job_names(&j->job, pn))
             continue;
         j->stale = 1;
         G.n.stale++;
@@ -992,40 +1147,135 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     pthread_mutex_unlock(&G.mu);
 }
 
-/* make the job's pictures resident and submit it (G.gpu held); *ticket on success */
-static int submit_job(GlueJob *j, const PictureParentControlSet *pcs, const MeContext *me, uint64_t *ticket) {
-    const svtme_job *job = &j->job;
-    uint64_t pin[9];
+/* The temporal filter's (central, reference) pairs of one window, in the
+ * order its frame loop visits them, with the same outlier skips
+ * (temporal_filtering.c:3096-3122; low delay: every frame, :3645-3648): all are
+ * known at the window's first ME call (blocks are the outer loop, frames the
+ * inner, :3029-3030), so that call submits every pair's job in ONE launch.
+ * out[] receives the jobs other than `first` (its clones with another
+ * reference), objs[] their reference objects. */
+static int tf_window(const PictureParentControlSet *centre, const MeContext *me, const svtme_job *first,
+                     svtme_job *out, const EbPaReferenceObject **objs, int max) {
+    PictureParentControlSet *const *list = centre->temp_filt_pcs_list;
+    const int past = centre->past_altref_nframes, fut = centre->future_altref_nframes, ic = past;
+    const int slot   = (int)(first->picture_number >> GLUE_NS_SHIFT);
+    const int ld     = centre->scs->static_config.pred_structure == SVT_AV1_PRED_LOW_DELAY_B;
+    const int step   = ld || !me->tf_ctrls.ref_frame_factor ? 1 : me->tf_ctrls.ref_frame_factor;
+    const int s0[3]  = {0, past, past + 1}, s1[3] = {past - 1, past, past + fut};
+    const int nseg   = ld ? 1 : 3;
+    const SequenceControlSet *scs = centre->scs;
+    int n = 0;
+    for (int seg = 0; seg < nseg; seg++)
+        for (int fi = ld ? 0 : s0[seg]; fi <= (ld ? past + fut : s1[seg]); fi += step) {
+            if (fi == ic || !list[fi] || !list[fi]->pa_ref_pic_wrapper)
+                continue;
+            const PictureParentControlSet *p = list[fi];
+            if (!ld) { /* the outlier skips of :3101-3122 */
+                const uint32_t low_ahd_err = centre->aligned_width * centre->aligned_height;
+                const uint8_t th           = centre->slice_type == I_SLICE ? 20 : 40;
+                if (p->tf_ahd_error_to_central > low_ahd_err &&
+                    (int)(((int)p->tf_ahd_error_to_central - (int)centre->tf_avg_ahd_error) * 100) >
+                        th * (int)centre->tf_avg_ahd_error)
+                    continue;
+                uint32_t cnt = 0;
+                for (uint32_t rw = 0; rw < scs->picture_analysis_number_of_regions_per_width; rw++)
+                    for (uint32_t rh = 0; rh < scs->picture_analysis_number_of_regions_per_height; rh++)
+                        if (abs((int)p->average_intensity_per_region[rw][rh] -
+                                (int)centre->average_intensity_per_region[rw][rh]) > 2 &&
+                            p->avg_luma != centre->tf_avg_luma)
+                            cnt++;
+                if (cnt >= (14 * scs->picture_analysis_number_of_regions_per_width *
+                            scs->picture_analysis_number_of_regions_per_height) / 16)
+                    continue;
+            }
+            const EbPaReferenceObject *o = (const EbPaReferenceObject *)p->pa_ref_pic_wrapper->object_ptr;
+            const uint64_t rpn           = ns_pn(slot, o->picture_number);
+            if (rpn == first->ref_picture_number[0][0] || n == max)
+                continue;
+            out[n] = *first;
+            out[n].ref_picture_number[0][0] = rpn;
+            objs[n++] = o;
+        }
+    return n;
+}
+
+/* make the jobs' pictures resident and submit them in one launch (G.gpu held);
+ * tickets[] on success. objs[k] (k > 0) is job k's reference object; job 0's
+ * references are the ME context's (me_ds_ref_array, set by the encoder for this call). */
+static int submit_jobs(GlueJob **js, const EbPaReferenceObject **objs, int n, const PictureParentControlSet *pcs,
+                       const MeContext *me, uint64_t *tickets) {
+    uint64_t pin[1 + 8 + SVTME_MAX_BATCH_JOBS];
     int npin = 0;
-    pin[npin++] = job->picture_number;
-    for (int l = 0; l < job->num_lists; l++)
-        for (int r = 0; r < job->num_refs[l]; r++) pin[npin++] = job->ref_picture_number[l][r];
+    const svtme_job *job0 = &js[0]->job;
+    pin[npin++] = job0->picture_number;
+    for (int l = 0; l < job0->num_lists; l++)
+        for (int r = 0; r < job0->num_refs[l]; r++) pin[npin++] = job0->ref_picture_number[l][r];
+    for (int k = 1; k < n; k++) pin[npin++] = js[k]->job.ref_picture_number[0][0];
     const EbPaReferenceObject *cur = pa_object(pcs);
-    if (pic_ensure(job->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
-                   cur->sixteenth_downsampled_picture_ptr, job->width, job->height, pin, npin))
+    if (pic_ensure(job0->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
+                   cur->sixteenth_downsampled_picture_ptr, job0->width, job0->height, pin, npin))
         return -1;
-    for (int l = 0; l < job->num_lists; l++)
-        for (int r = 0; r < job->num_refs[l]; r++) {
+    for (int l = 0; l < job0->num_lists; l++)
+        for (int r = 0; r < job0->num_refs[l]; r++) {
             const EbDownScaledBufDescPtrArray *d = &me->me_ds_ref_array[l][r];
-            if (pic_ensure(d->picture_number, d->picture_ptr, d->quarter_picture_ptr, d->sixteenth_picture_ptr,
-                           job->width, job->height, pin, npin))
+            if (pic_ensure(job0->ref_picture_number[l][r], d->picture_ptr, d->quarter_picture_ptr,
+                           d->sixteenth_picture_ptr, job0->width, job0->height, pin, npin))
                 return -1;
         }
-    if (G.verify) { /* what the job reads is the encoder's current content, however it became resident */
-        verify_pic(job->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
+    for (int k = 1; k < n; k++)
+        if (pic_ensure(js[k]->job.ref_picture_number[0][0], objs[k]->input_padded_pic,
+                       objs[k]->quarter_downsampled_picture_ptr, objs[k]->sixteenth_downsampled_picture_ptr,
+                       job0->width, job0->height, pin, npin))
+            return -1;
+    if (G.verify) { /* what the jobs read is the encoder's current content, however it became resident */
+        verify_pic(job0->picture_number, cur->input_padded_pic, cur->quarter_downsampled_picture_ptr,
                    cur->sixteenth_downsampled_picture_ptr, &G.n.verified_job);
-        for (int l = 0; l < job->num_lists; l++)
-            for (int r = 0; r < job->num_refs[l]; r++) {
+        for (int l = 0; l < job0->num_lists; l++)
+            for (int r = 0; r < job0->num_refs[l]; r++) {
                 const EbDownScaledBufDescPtrArray *d = &me->me_ds_ref_array[l][r];
-                verify_pic(d->picture_number, d->picture_ptr, d->quarter_picture_ptr, d->sixteenth_picture_ptr,
-                           &G.n.verified_job);
+                verify_pic(job0->ref_picture_number[l][r], d->picture_ptr, d->quarter_picture_ptr,
+                           d->sixteenth_picture_ptr, &G.n.verified_job);
             }
+        for (int k = 1; k < n; k++)
+            verify_pic(js[k]->job.ref_picture_number[0][0], objs[k]->input_padded_pic,
+                       objs[k]->quarter_downsampled_picture_ptr, objs[k]->sixteenth_downsampled_picture_ptr,
+                       &G.n.verified_job);
     }
+    svtme_job jobs[SVTME_MAX_BATCH_JOBS];
+    svtme_pack_layout layouts[SVTME_MAX_BATCH_JOBS];
+    void *outs[SVTME_MAX_BATCH_JOBS];
+    for (int k = 0; k < n; k++) jobs[k] = js[k]->job, layouts[k] = js[k]->layout, outs[k] = js[k]->packed;
     const double t0 = now_s();
-    const svtme_status st =
-        svtme_submit_picture_packed_async(G.ctx, G.next_lane++ % SVTME_LANES, job, &j->layout, j->packed, ticket);
+    const svtme_status st = svtme_submit_pictures_packed_async(G.ctx, G.next_lane++ % SVTME_LANES, (uint32_t)n, jobs,
+                                                               layouts, outs, tickets);
     G.n.submit_s += now_s() - t0;
     return st == SVTME_OK ? 0 : -1;
+}
+
+/* a new job in G.jobs (G.mu held) */
+static GlueJob *job_new(const PictureParentControlSet *pcs, const svtme_job *job, uint32_t users) {
+    GlueJob *j = (GlueJob *)calloc(1, sizeof(GlueJob));
+    if (!j)
+        abort();
+    j->job    = *job;
+    j->layout = layout_of(pcs, job);
+    j->n_sb   = svtme_sb_total(job->width, job->height);
+    j->R      = svtme_job_ref_slots(job);
+    j->stride = svtme_packed_sb_bytes(&j->layout, j->R);
+    j->users  = users;
+    j->next   = G.jobs;
+    G.jobs    = j;
+    if (job->me_type == SVTME_ME_MCTF)
+        G.n.tf_jobs++;
+    else
+        G.n.pa_jobs++;
+    return j;
+}
+
+static GlueJob *job_find(const svtme_job *job) { /* G.mu held */
+    GlueJob *j = G.jobs;
+    while (j && (j->stale || memcmp(&j->job, job, sizeof(*job)) != 0)) j = j->next;
+    return j;
 }
 
 EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
@@ -1038,80 +1288,89 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
         svtme_job_from_tf(&job, pcs, me_ctx, input_ptr);
     else /* scaled references (me_process.c:229-246), DG detector: the encoder's own search */
         return SVTME_ENCODER_ME_B64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
-    if (!G.ctx) {
+    if (!G.ctx || pcs_slot(pcs) < 0) { /* (no device, or more than GLUE_MAX_ENC live encoders) */
         pthread_mutex_lock(&G.mu);
         G.n.fallback_sbs++;
         pthread_mutex_unlock(&G.mu);
         return SVTME_ENCODER_ME_B64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
     }
 
-    /* find or start the picture's job (one per picture, or per TF reference) */
+    /* find or start the picture's job (one per picture, or per TF reference: the
+     * first call of a TF window starts every pair's job, in one launch) */
     pthread_mutex_lock(&G.mu);
-    GlueJob *j = G.jobs;
-    while (j && (j->stale || memcmp(&j->job, &job, sizeof(job)) != 0)) j = j->next;
+    GlueJob *j = job_find(&job);
     if (j) {
         j->users++;
         while (j->state == 0) pthread_cond_wait(&G.cv, &G.mu);
     } else {
-        j = (GlueJob *)calloc(1, sizeof(GlueJob));
-        if (!j)
-            abort();
-        j->job    = job;
-        j->layout = layout_of(pcs, &job);
-        j->n_sb   = svtme_sb_total(job.width, job.height);
-        j->R      = svtme_job_ref_slots(&job);
-        j->stride = svtme_packed_sb_bytes(&j->layout, j->R);
-        j->users  = 1;
-        j->next   = G.jobs;
-        G.jobs    = j;
-        if (job.me_type == SVTME_ME_MCTF)
-            G.n.tf_jobs++;
-        else
-            G.n.pa_jobs++;
+        GlueJob *js[SVTME_MAX_BATCH_JOBS];
+        const EbPaReferenceObject *objs[SVTME_MAX_BATCH_JOBS] = {NULL};
+        int n = 0;
+        j       = job_new(pcs, &job, 1);
+        js[n++] = j;
         const double t_start = now_s();
         int rc = buf_take(j, (size_t)j->n_sb * j->stride, buf_worst(j->n_sb));
+        if (!rc && job.me_type == SVTME_ME_MCTF && G.tf_batch) {
+            svtme_job sib[SVTME_MAX_BATCH_JOBS - 1];
+            const EbPaReferenceObject *so[SVTME_MAX_BATCH_JOBS - 1];
+            const int ns = tf_window(pcs, me_ctx, &job, sib, so, SVTME_MAX_BATCH_JOBS - 1);
+            for (int k = 0; k < ns; k++) {
+                if (job_find(&sib[k])) /* (already started) */
+                    continue;
+                GlueJob *x = job_new(pcs, &sib[k], 0);
+                if (buf_take(x, (size_t)x->n_sb * x->stride, buf_worst(x->n_sb))) {
+                    job_unlink(x);
+                    free(x);
+                    continue;
+                }
+                objs[n] = so[k];
+                js[n++] = x;
+                G.n.tf_batched++;
+            }
+        }
         if (G.inflight++ == 0)
             G.busy_t0 = t_start;
         if (G.inflight > G.n.max_inflight)
             G.n.max_inflight = G.inflight;
         const uint32_t inflight = G.inflight;
         pthread_mutex_unlock(&G.mu);
-        uint64_t ticket = 0;
+        uint64_t tickets[SVTME_MAX_BATCH_JOBS] = {0};
         unsigned long long up_n = 0;
         double up_s = 0;
         if (!rc) {
             pthread_mutex_lock(&G.gpu);
             up_n = G.n.uploads, up_s = G.n.upload_s;
-            rc   = submit_job(j, pcs, me_ctx, &ticket);
+            rc   = submit_jobs(js, objs, n, pcs, me_ctx, tickets);
             up_n = G.n.uploads - up_n, up_s = G.n.upload_s - up_s;
             pthread_mutex_unlock(&G.gpu);
         }
         double t_wait = now_s();
-        if (!rc) /* no glue lock held: other pictures' threads upload and submit meanwhile */
-            rc = svtme_ticket_wait(G.ctx, ticket) == SVTME_OK ? 0 : -1;
-        const double t_done = now_s();
-        pthread_mutex_lock(&G.mu);
-        G.n.wait_s += t_done - t_wait;
-        G.n.job_s += t_done - t_start;
-        if (--G.inflight == 0)
-            G.n.busy_s += t_done - G.busy_t0;
-        if (!rc)
-            G.n.job_sbs += j->n_sb;
-        if (G.trace_path) {
-            if (G.n_trace == G.cap_trace) {
-                G.cap_trace = G.cap_trace ? 2 * G.cap_trace : 256;
-                G.trace     = (GlueTrace *)realloc(G.trace, G.cap_trace * sizeof(GlueTrace));
-                if (!G.trace)
-                    abort();
+        for (int k = 0; k < n; k++) {
+            /* no glue lock held: other pictures' threads upload and submit meanwhile */
+            const int rk       = rc ? rc : (svtme_ticket_wait(G.ctx, tickets[k]) == SVTME_OK ? 0 : -1);
+            const double t_done = now_s();
+            pthread_mutex_lock(&G.mu);
+            if (k == 0) {
+                G.n.wait_s += t_done - t_wait;
+                G.n.job_s += t_done - t_start;
+                G.n.launches += !rc;
             }
-            const GlueTrace t = {job.picture_number, job.me_type == SVTME_ME_MCTF, j->n_sb, inflight, (uint32_t)up_n,
-                                 t_start, t_wait, t_done, up_s};
-            G.trace[G.n_trace++] = t;
+            if (!rk)
+                G.n.job_sbs += js[k]->n_sb;
+            if (G.trace_path) {
+                const GlueTrace t = {js[k]->job.picture_number, js[k]->job.me_type == SVTME_ME_MCTF, js[k]->n_sb,
+                                     inflight, k ? 0 : (uint32_t)up_n, t_start, t_wait, t_done, k ? 0 : up_s};
+                trace_add(&t);
+            }
+            js[k]->state = rk ? -1 : 1;
+            if (rk && k == 0)
+                glue_fallback("picture job failed");
+            if (k == n - 1 && --G.inflight == 0)
+                G.n.busy_s += t_done - G.busy_t0;
+            pthread_cond_broadcast(&G.cv);
+            if (k < n - 1)
+                pthread_mutex_unlock(&G.mu);
         }
-        j->state = rc ? -1 : 1;
-        if (rc)
-            glue_fallback("picture job failed");
-        pthread_cond_broadcast(&G.cv);
     }
     const int ok = j->state == 1 && b64_index < j->n_sb;
     if (ok)
@@ -1145,9 +1404,28 @@ EbErrorType __wrap_svt_aom_motion_estimation_b64(PictureParentControlSet *pcs, u
     return svtme_motion_estimation_b64(pcs, b64_index, b64_origin_x, b64_origin_y, me_ctx, input_ptr);
 }
 
+EbErrorType __real_svt_av1_enc_init(EbComponentType *svt_enc_component);
 EbErrorType __real_svt_av1_enc_deinit(EbComponentType *svt_enc_component);
+
+static const void *handle_enc_ctx(const EbComponentType *c) {
+    const EbEncHandle *h = c ? (const EbEncHandle *)c->p_component_private : NULL;
+    return h && h->scs_instance_array && h->scs_instance_array[0] ? (const void *)h->scs_instance_array[0]->enc_ctx
+                                                                  : NULL;
+}
+
+/* a new encoder: its slot, and the resource its picture analysis posts its results to */
+EbErrorType __wrap_svt_av1_enc_init(EbComponentType *svt_enc_component) {
+    const EbErrorType e = __real_svt_av1_enc_init(svt_enc_component);
+    if (e == EB_ErrorNone) {
+        const EbEncHandle *h = (const EbEncHandle *)svt_enc_component->p_component_private;
+        (void)enc_slot(handle_enc_ctx(svt_enc_component), h->picture_analysis_results_resource_ptr);
+    }
+    return e;
+}
+
 EbErrorType __wrap_svt_av1_enc_deinit(EbComponentType *svt_enc_component) {
-    svtme_glue_release(); /* before the encoder frees the buffers the glue page-locked */
+    /* before the encoder frees the buffers the glue page-locked */
+    svtme_glue_release_encoder(handle_enc_ctx(svt_enc_component));
     return __real_svt_av1_enc_deinit(svt_enc_component);
 }
 
@@ -1159,30 +1437,15 @@ void __wrap_svt_aom_downsample_filtering_input_picture(PictureParentControlSet *
 
 /* Picture analysis decimates inside its own translation unit
  * (pic_analysis_process.c:2151), out of reach of --wrap, and ends each picture
- * by posting a PictureAnalysisResults object (pic_analysis_process.c:2180-2191).
- * The wraps below record the objects the encoder creates for that FIFO (at
- * svt_av1_enc_init, enc_handle.c) and upload the picture when one is posted:
- * its PA reference planes are final then, until a later decimation. Objects
- * beyond the table's size only lose the early upload (jobs upload on first use). */
-static void *g_pa_results[1024];
-static uint32_t g_n_pa_results;
-
-EbErrorType __real_svt_aom_picture_analysis_result_creator(EbPtr *object_dbl_ptr, EbPtr object_init_data_ptr);
-EbErrorType __wrap_svt_aom_picture_analysis_result_creator(EbPtr *object_dbl_ptr, EbPtr object_init_data_ptr) {
-    const EbErrorType e = __real_svt_aom_picture_analysis_result_creator(object_dbl_ptr, object_init_data_ptr);
-    const uint32_t n    = __atomic_load_n(&g_n_pa_results, __ATOMIC_RELAXED);
-    if (e == EB_ErrorNone && n < sizeof(g_pa_results) / sizeof(g_pa_results[0])) {
-        g_pa_results[n] = *object_dbl_ptr;
-        __atomic_store_n(&g_n_pa_results, n + 1, __ATOMIC_RELEASE);
-    }
-    return e;
-}
-
+ * by posting a PictureAnalysisResults object (pic_analysis_process.c:2180-2191)
+ * to its encoder's picture-analysis results resource: when such an object is
+ * posted, the picture is uploaded, as its PA reference planes are final then
+ * (until a later decimation). */
 EbErrorType __real_svt_post_full_object(EbObjectWrapper *object_ptr);
 EbErrorType __wrap_svt_post_full_object(EbObjectWrapper *object_ptr) {
-    const uint32_t n = __atomic_load_n(&g_n_pa_results, __ATOMIC_ACQUIRE);
-    for (uint32_t i = 0; object_ptr && i < n; i++)
-        if (g_pa_results[i] == object_ptr->object_ptr) {
+    const void *res = object_ptr ? (const void *)object_ptr->system_resource_ptr : NULL;
+    for (int i = 0; res && i < GLUE_MAX_ENC; i++)
+        if (__atomic_load_n(&g_enc[i].pa_res, __ATOMIC_ACQUIRE) == res) {
             const PictureAnalysisResults *r = (const PictureAnalysisResults *)object_ptr->object_ptr;
             PictureParentControlSet *pcs    = (PictureParentControlSet *)r->pcs_wrapper->object_ptr;
             if (!pcs->is_overlay && pcs->pa_ref_pic_wrapper) /* overlays skip the analysis (:2122) */

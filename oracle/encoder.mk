@@ -17,10 +17,11 @@
 #                        TF-ME served from picture jobs) and
 #                        -Wl,--wrap=svt_aom_downsample_filtering_input_picture
 #                        (re-decimated pictures are re-uploaded),
-#                        -Wl,--wrap=svt_aom_picture_analysis_result_creator and
 #                        -Wl,--wrap=svt_post_full_object (each picture uploaded
-#                        when its analysis ends), -Wl,--wrap=svt_av1_enc_deinit
-#                        (page-locked buffers released), backed by
+#                        when its analysis ends), -Wl,--wrap=svt_av1_enc_init /
+#                        -Wl,--wrap=svt_av1_enc_deinit (each encoder's picture-
+#                        number range; its pictures, jobs and page-locked
+#                        buffers released at its teardown), backed by
 #                        liboraclejob.so: the svtme job API over the oracle (CPU)
 #   svtav1enc_gpu        the same glue backed by the product, libsvtme.so (HIP)
 # tests/test_encoder.py encodes with them and compares the bitstreams byte for byte.
@@ -74,7 +75,7 @@ liboraclejob.so: svtme_oraclejob.c svtme_oracle.c svtme_oracle_kernels.c svtme_o
 	    svtme_oracle.c svtme_oracle_kernels.c -lpthread
 
 WRAP = -Wl,--wrap=svt_aom_motion_estimation_b64 -Wl,--wrap=svt_aom_downsample_filtering_input_picture \
-       -Wl,--wrap=svt_av1_enc_deinit -Wl,--wrap=svt_aom_picture_analysis_result_creator \
+       -Wl,--wrap=svt_av1_enc_deinit -Wl,--wrap=svt_av1_enc_init \
        -Wl,--wrap=svt_post_full_object
 
 $(O)/svtav1enc_ora: $(APP_OBJ) $(O)/obj/glue.o $(O)/libsvtenc.a liboraclejob.so

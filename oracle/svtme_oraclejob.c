@@ -211,6 +211,15 @@ svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, const uint8_t
     return svtme_picture_upload(c, pn, y, stride, width, height);
 }
 
+svtme_status svtme_picture_upload_copy_async(svtme_ctx *c, uint64_t pn, const uint8_t *y, uint32_t stride,
+                                             uint32_t width, uint32_t height) {
+    return svtme_picture_upload(c, pn, y, stride, width, height);
+}
+
+svtme_status svtme_reserve_pictures(svtme_ctx *c, uint32_t width, uint32_t height, uint32_t count) {
+    return c && width && height && count <= 4096 ? SVTME_OK : SVTME_ERR_BAD_PARAMETER;
+}
+
 void *svtme_host_alloc(uint64_t bytes) { return malloc(bytes ? (size_t)bytes : 1); }
 void svtme_host_free(void *p) { free(p); }
 svtme_status svtme_host_register(void *p, uint64_t bytes) { return p && bytes ? SVTME_OK : SVTME_ERR_BAD_PARAMETER; }
@@ -280,6 +289,20 @@ svtme_status svtme_submit_picture_packed_async(svtme_ctx *c, uint32_t lane, cons
     free(recs);
     free(sbr);
     return st;
+}
+
+svtme_status svtme_submit_pictures_packed_async(svtme_ctx *c, uint32_t lane, uint32_t n, const svtme_job *jobs,
+                                                const svtme_pack_layout *layouts, void *const *host_outs,
+                                                uint64_t *tickets) {
+    if (!c || !jobs || !layouts || !host_outs || !tickets || n == 0 || n > SVTME_MAX_BATCH_JOBS)
+        return ora_fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_pictures_packed_async: bad arguments");
+    for (uint32_t k = 0; k < n; k++) {
+        const svtme_status st = svtme_submit_picture_packed_async(c, lane, &jobs[k], &layouts[k], host_outs[k],
+                                                                  &tickets[k]);
+        if (st)
+            return st;
+    }
+    return SVTME_OK;
 }
 
 svtme_status svtme_sync(svtme_ctx *c) { return c ? SVTME_OK : SVTME_ERR_BAD_PARAMETER; }

@@ -6,6 +6,8 @@ of the GPU jobs / the wall time with at least one job in flight (upload,
 search and the packed copy back included), mean job latency, jobs in flight.
 
 usage: python scripts/glue_rate.py OUT.json [case ...]   (default: 4k_p8_64f 4k_p8_16f 1080p_p8)
+(environment: SVTME_GLUE_* of integration/svtme_svt_glue.c pass through, e.g.
+SVTME_GLUE_PIN=1 for the page-locked-encoder-buffer uploads)
 """
 import json
 import os
@@ -29,13 +31,21 @@ def main():
         got = E.encode("gpu", case, wd, env_extra={"SVTME_GLUE_VERIFY": "0", "SVTME_GLUE_TRACE": trace})
         g = got["glue"]
         with open(trace) as fh:
-            jobs = [json.loads(line) for line in fh if line.strip()]
+            lines = [json.loads(line) for line in fh if line.strip()]
+        jobs = [t for t in lines if t["tf"] != 2]
+        ups = [t for t in lines if t["tf"] == 2]  # uploads (start create_ms, end done_ms)
         w, h, frames, preset = E.CASES[case][:4]
         r = {"case": case, "size": f"{w}x{h}", "frames": frames, "preset": preset,
              "identical": got["md5"] == ref["md5"], "md5": got["md5"], "ref_seconds": ref["seconds"],
-             "gpu_encoder_seconds": got["seconds"], **g, "jobs": jobs}
+             "gpu_encoder_seconds": got["seconds"], **g, "jobs": jobs, "uploads_trace": ups}
         lat = sorted(j["done_ms"] - j["create_ms"] for j in jobs)
-        print(json.dumps({k: v for k, v in r.items() if k != "jobs"}), flush=True)
+        # jobs above 1 ms and the uploads that overlapped them (a stall's candidates)
+        r["long_jobs"] = [{"pn": j["pn"], "tf": j["tf"], "ms": round(j["done_ms"] - j["create_ms"], 3),
+                           "uploads_overlapping": [u["pn"] for u in ups
+                                                   if u["create_ms"] < j["done_ms"] and u["done_ms"] > j["create_ms"]]}
+                          for j in jobs if j["done_ms"] - j["create_ms"] > 1.0]
+        r["max_job_ms"] = round(lat[-1], 3)
+        print(json.dumps({k: v for k, v in r.items() if k not in ("jobs", "uploads_trace")}), flush=True)
         print(f"  job latency ms: min {lat[0]:.3f} median {lat[len(lat) // 2]:.3f} max {lat[-1]:.3f}; "
               f"submit part median {sorted(j['submitted_ms'] - j['create_ms'] for j in jobs)[len(jobs) // 2]:.3f}",
               flush=True)

@@ -17,6 +17,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -134,6 +136,21 @@ struct svtme_ctx {
     // released pictures whose memory queued work may still read: freed (or reused by
     // a picture of the same size) once their upload and last readers have completed
     std::vector<PicBuf> graves;
+    // idle picture buffers (released pictures whose readers have run, and those
+    // svtme_reserve_pictures made), reused for pictures of the same size: no
+    // hipMalloc / hipFree on the steady path
+    std::vector<std::pair<size_t, uint8_t *>> freebufs;
+    static constexpr size_t kMaxFree = 256;
+    // page-locked staging of svtme_picture_upload_copy_async, reused in rotation
+    struct UpSlot {
+        void *h = nullptr;
+        size_t cap = 0;
+        hipEvent_t done = nullptr; // the slot's last DMA has run
+        bool busy = false;         // a thread is filling it
+        bool queued = false;       // `done` marks a DMA
+    };
+    UpSlot up[SVTME_UPLOAD_SLOTS];
+    uint32_t up_next = 0;
     void *staging      = nullptr;
     size_t staging_cap = 0;
     svtme_ref_record *d_records = nullptr;
@@ -167,6 +184,7 @@ struct svtme_ctx {
     uint64_t ticket_seq = 0;
     hipStream_t dstream = nullptr; // packed outputs to host memory, created on first use
     std::mutex mu;
+    std::condition_variable retired; // a ticket was retired (svtme_ticket_wait)
 };
 
 extern "C" uint32_t svtme_sb_total(uint32_t width, uint32_t height) {
@@ -248,6 +266,14 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
         (void)hipFree(g.mem);
         if (g.ready)
             (void)hipEventDestroy(g.ready);
+    }
+    for (auto &f : c->freebufs)
+        (void)hipFree(f.second);
+    for (auto &u : c->up) {
+        if (u.h)
+            (void)hipHostFree(u.h);
+        if (u.done)
+            (void)hipEventDestroy(u.done);
     }
     if (c->staging)
         (void)hipFree(c->staging);
@@ -370,8 +396,20 @@ static bool grave_idle(const PicBuf &g) {
             return false;
     return true;
 }
-// free the idle released pictures; with want > 0, keep (and return) one idle buffer
-// of exactly `want` bytes for reuse instead of freeing it
+// an idle buffer of exactly `bytes` from the free pool, or nullptr
+static uint8_t *take_free(svtme_ctx *c, size_t bytes) {
+    for (size_t i = 0; i < c->freebufs.size(); i++)
+        if (c->freebufs[i].first == bytes) {
+            uint8_t *m     = c->freebufs[i].second;
+            c->freebufs[i] = c->freebufs.back();
+            c->freebufs.pop_back();
+            return m;
+        }
+    return nullptr;
+}
+// move the idle released pictures' memory to the free pool (beyond kMaxFree
+// buffers it goes back to HIP); with want > 0, return one idle buffer of
+// exactly `want` bytes instead
 static uint8_t *sweep_graves(svtme_ctx *c, size_t want) {
     uint8_t *keep = nullptr;
     for (size_t i = 0; i < c->graves.size();) {
@@ -384,6 +422,8 @@ static uint8_t *sweep_graves(svtme_ctx *c, size_t want) {
             (void)hipEventDestroy(g.ready);
         if (!keep && want && g.bytes == want)
             keep = g.mem;
+        else if (c->freebufs.size() < svtme_ctx::kMaxFree)
+            c->freebufs.emplace_back(g.bytes, g.mem);
         else
             (void)hipFree(g.mem);
         c->graves[i] = c->graves.back();
@@ -392,33 +432,63 @@ static uint8_t *sweep_graves(svtme_ctx *c, size_t want) {
     return keep;
 }
 
+// bytes of a W x H picture's three padded planes in one buffer, and their offsets
+static size_t pic_bytes(uint32_t W, uint32_t H, size_t offs[3] = nullptr) {
+    size_t total = 0;
+    for (int lv = 0; lv < 3; lv++) {
+        uint32_t w, h, left, top, stride, rows, pad;
+        svtme_plane_geometry(lv, W, H, &w, &h, &left, &top, &stride, &rows, &pad);
+        if (offs)
+            offs[lv] = total;
+        total += (size_t)stride * rows;
+        total = (total + 255) & ~(size_t)255;
+    }
+    return total + 1024; // slack: search-window loads may read a few dwords past the last row
+}
+
+// device memory for a picture: the free pool, an idle released picture, or HIP;
+// when HIP is out of memory, wait for the released pictures' readers, give every
+// idle buffer back and try once more
+static svtme_status pic_mem(svtme_ctx *c, size_t total, uint8_t **out) {
+    if ((*out = take_free(c, total)) || (*out = sweep_graves(c, total)))
+        return SVTME_OK;
+    if (hipMalloc((void **)out, total) == hipSuccess)
+        return SVTME_OK;
+    (void)hipGetLastError();
+    for (auto &g : c->graves) {
+        if (g.ready)
+            HIP_TRY(hipEventSynchronize(g.ready));
+        for (int l = 0; l < SVTME_LANES; l++)
+            if (g.used[l])
+                HIP_TRY(hipEventSynchronize(g.used[l]));
+    }
+    (void)sweep_graves(c, 0);
+    for (auto &f : c->freebufs)
+        HIP_TRY(hipFree(f.second));
+    c->freebufs.clear();
+    HIP_TRY(hipMalloc((void **)out, total));
+    return SVTME_OK;
+}
+
 // allocate the three planes of a W x H picture in one buffer
 static svtme_status alloc_pic(svtme_ctx *c, uint64_t pn, uint32_t W, uint32_t H, PicBuf **out) {
     auto it = c->pics.find(pn);
     if (it != c->pics.end() && (it->second.W != W || it->second.H != H)) {
-        svtme_status qs = quiesce(c);
-        if (qs)
-            return qs;
-        HIP_TRY(hipFree(it->second.mem));
-        if (it->second.ready)
-            HIP_TRY(hipEventDestroy(it->second.ready));
+        // a new size: the old buffer goes to the graves (freed for reuse once its readers ran)
+        c->graves.push_back(it->second);
         c->pics.erase(it);
         it = c->pics.end();
     }
-    size_t offs[3], total = 0;
+    size_t offs[3];
+    const size_t total = pic_bytes(W, H, offs);
     uint32_t w[3], h[3], left[3], top[3], stride[3], rows[3], pad[3];
-    for (int lv = 0; lv < 3; lv++) {
+    for (int lv = 0; lv < 3; lv++)
         svtme_plane_geometry(lv, W, H, &w[lv], &h[lv], &left[lv], &top[lv], &stride[lv], &rows[lv], &pad[lv]);
-        offs[lv] = total;
-        total += (size_t)stride[lv] * rows[lv];
-        total = (total + 255) & ~(size_t)255;
-    }
-    total += 1024; // slack: search-window loads may read a few dwords past the last row
     if (it == c->pics.end()) {
         PicBuf pb;
-        pb.mem = sweep_graves(c, total); // a released picture's idle memory of the same size, if any
-        if (!pb.mem)
-            HIP_TRY(hipMalloc((void **)&pb.mem, total));
+        svtme_status ms = pic_mem(c, total, &pb.mem);
+        if (ms)
+            return ms;
         pb.bytes = total;
         pb.W = W, pb.H = H;
         it = c->pics.emplace(pn, pb).first;
@@ -559,6 +629,100 @@ extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, co
         return st;
     HIP_TRY(hipEventRecord(pb->ready, c->ustream));
     pb->pending = (1u << SVTME_LANES) - 1u;
+    return SVTME_OK;
+}
+
+// Upload from pageable memory through the context's page-locked staging ring:
+// take a slot (wait for its last DMA), copy the rows into it with no lock held,
+// then queue the DMA and the pyramid build like svtme_picture_upload_async.
+extern "C" svtme_status svtme_picture_upload_copy_async(svtme_ctx *c, uint64_t pn, const uint8_t *y, uint32_t stride,
+                                                        uint32_t w, uint32_t h) {
+    if (!c || !y || w == 0 || h == 0 || stride < w)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_upload_copy_async: bad arguments");
+    svtme_ctx::UpSlot *u = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        HIP_TRY(hipSetDevice(c->device));
+        const svtme_status us = ensure_ustream(c);
+        if (us)
+            return us;
+        for (int k = 0; k < SVTME_UPLOAD_SLOTS && !u; k++) {
+            svtme_ctx::UpSlot &x = c->up[(c->up_next + k) % SVTME_UPLOAD_SLOTS];
+            if (!x.busy)
+                u = &x;
+        }
+        if (!u)
+            return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "svtme_picture_upload_copy_async: %d uploads being staged",
+                        SVTME_UPLOAD_SLOTS);
+        c->up_next = (uint32_t)(u - c->up + 1) % SVTME_UPLOAD_SLOTS;
+        u->busy    = true;
+        if (!u->done)
+            HIP_TRY(hipEventCreateWithFlags(&u->done, hipEventDisableTiming));
+    }
+    // outside the context lock: other threads submit jobs meanwhile
+    const size_t need = (size_t)w * h;
+    hipError_t e      = hipSetDevice(c->device);
+    if (e == hipSuccess && u->queued)
+        e = hipEventSynchronize(u->done); // the slot's previous DMA has read it
+    if (e == hipSuccess && u->cap < need) {
+        if (u->h)
+            e = hipHostFree(u->h);
+        u->h   = nullptr;
+        u->cap = 0;
+        if (e == hipSuccess && (e = hipHostMalloc(&u->h, need, hipHostMallocDefault)) == hipSuccess)
+            u->cap = need;
+    }
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> lk(c->mu);
+        u->busy = false;
+        return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "svtme_picture_upload_copy_async: staging: %s",
+                    hipGetErrorString(e));
+    }
+    for (uint32_t r = 0; r < h; r++)
+        memcpy((uint8_t *)u->h + (size_t)r * w, y + (size_t)r * stride, w);
+    std::lock_guard<std::mutex> lk(c->mu);
+    struct Release { // the slot is free again however this returns
+        svtme_ctx::UpSlot *u;
+        ~Release() { u->busy = false; }
+    } rel{u};
+    const bool resident = c->pics.count(pn) != 0;
+    PicBuf *pb;
+    svtme_status st;
+    if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
+        return st;
+    if (resident && (st = after_readers(c, *pb, c->ustream))) // queued jobs may still read the old planes
+        return st;
+    if (!pb->ready)
+        HIP_TRY(hipEventCreateWithFlags(&pb->ready, hipEventDisableTiming));
+    if (c->ustaging_cap < need) { // only between uploads: nothing queued reads the old buffer
+        HIP_TRY(hipStreamSynchronize(c->ustream));
+        if ((st = ensure_buf(&c->ustaging, &c->ustaging_cap, need)))
+            return st;
+    }
+    HIP_TRY(hipMemcpyAsync(c->ustaging, u->h, need, hipMemcpyHostToDevice, c->ustream));
+    HIP_TRY(hipEventRecord(u->done, c->ustream));
+    u->queued = true;
+    if ((st = build_pyramid(c, pb, c->ustaging, w, w, h, 0, c->ustream)))
+        return st;
+    HIP_TRY(hipEventRecord(pb->ready, c->ustream));
+    pb->pending = (1u << SVTME_LANES) - 1u;
+    return SVTME_OK;
+}
+
+extern "C" svtme_status svtme_reserve_pictures(svtme_ctx *c, uint32_t width, uint32_t height, uint32_t count) {
+    if (!c || width == 0 || height == 0 || count > 4096)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_reserve_pictures: bad arguments");
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t bytes = pic_bytes(svtme_align8_u(width), svtme_align8_u(height));
+    uint32_t have      = 0;
+    for (auto &f : c->freebufs)
+        have += f.first == bytes;
+    for (; have < count && c->freebufs.size() < svtme_ctx::kMaxFree; have++) {
+        uint8_t *m = nullptr;
+        HIP_TRY(hipMalloc((void **)&m, bytes));
+        c->freebufs.emplace_back(bytes, m);
+    }
     return SVTME_OK;
 }
 
@@ -1045,56 +1209,103 @@ extern "C" svtme_status svtme_reserve(svtme_ctx *c, uint32_t width, uint32_t hei
     return SVTME_OK;
 }
 
+extern "C" svtme_status svtme_submit_pictures_packed_async(svtme_ctx *c, uint32_t lane, uint32_t n,
+                                                           const svtme_job *jobs, const svtme_pack_layout *layouts,
+                                                           void *const *host_outs, uint64_t *tickets) {
+    if (!c || !jobs || !layouts || !host_outs || !tickets)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_pictures_packed_async: null argument");
+    if (n == 0 || n > SVTME_MAX_BATCH_JOBS)
+        return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_pictures_packed_async: %u jobs (1..%d)", n,
+                    SVTME_MAX_BATCH_JOBS);
+    for (uint32_t k = 0; k < n; k++) {
+        const svtme_pack_layout *L = &layouts[k];
+        if (!host_outs[k])
+            return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_pictures_packed_async: null host_out %u", k);
+        if (L->sb_results && (L->n_pus == 0 || L->n_pus > SVTME_PU_COUNT || L->max_cand == 0 ||
+                              L->max_cand > SVTME_MAX_PA_ME_CAND || L->max_refs == 0 ||
+                              L->max_refs > SVTME_MAX_PA_ME_MV))
+            return fail(SVTME_ERR_BAD_PARAMETER, "pack layout: %u PUs, %u candidates, %u MVs", L->n_pus,
+                        L->max_cand, L->max_refs);
+    }
+    std::unique_lock<std::mutex> lk(c->mu);
+    HIP_TRY(hipSetDevice(c->device));
+    // n free ticket slots; with too few free, wait for other threads' svtme_ticket_wait
+    // to retire some (up to 100 ms while nobody waits on a ticket: then the caller
+    // holds them itself and is refused)
+    Ticket *t[SVTME_MAX_BATCH_JOBS];
+    auto free_slots = [&]() {
+        uint32_t k = 0;
+        for (auto &x : c->tickets)
+            if (!x.id && k < n)
+                t[k++] = &x;
+        return k == n;
+    };
+    auto someone_waits = [&]() {
+        for (auto &x : c->tickets)
+            if (x.waiting)
+                return true;
+        return false;
+    };
+    const auto grace = std::chrono::steady_clock::now() + std::chrono::milliseconds(100);
+    while (!free_slots()) {
+        if (!someone_waits() && std::chrono::steady_clock::now() >= grace)
+            return fail(SVTME_ERR_INSUFFICIENT_RESOURCES,
+                        "%d packed jobs outstanding and none being waited on (svtme_ticket_wait retires them)",
+                        SVTME_MAX_TICKETS);
+        c->retired.wait_for(lk, std::chrono::milliseconds(5));
+    }
+    if (!c->dstream)
+        HIP_TRY(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
+    svtme_ref_record *d_recs[SVTME_MAX_BATCH_JOBS];
+    svtme_sb_result *d_sb[SVTME_MAX_BATCH_JOBS];
+    void *d_pack[SVTME_MAX_BATCH_JOBS];
+    size_t pbytes[SVTME_MAX_BATCH_JOBS];
+    uint32_t counts[SVTME_MAX_BATCH_JOBS], Rs[SVTME_MAX_BATCH_JOBS];
+    bool any_sb = false;
+    svtme_status st;
+    for (uint32_t k = 0; k < n; k++) {
+        const svtme_job *job       = &jobs[k];
+        const svtme_pack_layout *L = &layouts[k];
+        if (!t[k]->done) {
+            HIP_TRY(hipEventCreateWithFlags(&t[k]->launched, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&t[k]->done, hipEventDisableTiming));
+        }
+        const uint32_t total = svtme_sb_total(job->width, job->height);
+        counts[k] = job->sb_count ? job->sb_count : (job->sb_begin < total ? total - job->sb_begin : 0);
+        Rs[k]     = svtme_job_ref_slots(job);
+        const size_t rb  = (size_t)counts[k] * Rs[k] * sizeof(svtme_ref_record);
+        const size_t sbb = L->sb_results ? (size_t)counts[k] * sizeof(svtme_sb_result) : 0;
+        pbytes[k]        = (size_t)counts[k] * svtme_packed_sb_bytes(L, Rs[k]);
+        const size_t o_sb = (rb + 255) & ~(size_t)255, o_pk = (o_sb + sbb + 255) & ~(size_t)255;
+        if ((st = ensure_buf(&t[k]->d_mem, &t[k]->d_cap, o_pk + pbytes[k]))) // free slot: nothing reads it
+            return st;
+        d_recs[k] = (svtme_ref_record *)t[k]->d_mem;
+        d_sb[k]   = L->sb_results ? (svtme_sb_result *)((uint8_t *)t[k]->d_mem + o_sb) : nullptr;
+        d_pack[k] = (uint8_t *)t[k]->d_mem + o_pk;
+        any_sb |= d_sb[k] != nullptr;
+    }
+    // one launch over every job (the stage kernels take up to SVTME_MAX_BATCH jobs)
+    if ((st = submit_batch_locked(c, jobs, n, d_recs, d_sb, any_sb, lane)))
+        return st;
+    hipStream_t ls = c->lanes[lane].s;
+    for (uint32_t k = 0; k < n; k++) {
+        HIP_TRY(svtme_launch_pack(d_recs[k], d_sb[k], counts[k], Rs[k], &layouts[k], d_pack[k], ls));
+        HIP_TRY(hipEventRecord(t[k]->launched, ls));
+        HIP_TRY(hipStreamWaitEvent(c->dstream, t[k]->launched, 0));
+        HIP_TRY(hipMemcpyAsync(host_outs[k], d_pack[k], pbytes[k], hipMemcpyDeviceToHost, c->dstream));
+        HIP_TRY(hipEventRecord(t[k]->done, c->dstream));
+        t[k]->id   = ++c->ticket_seq;
+        tickets[k] = t[k]->id;
+    }
+    return SVTME_OK;
+}
+
 extern "C" svtme_status svtme_submit_picture_packed_async(svtme_ctx *c, uint32_t lane, const svtme_job *job,
                                                           const svtme_pack_layout *L, void *host_out,
                                                           uint64_t *ticket) {
     if (!c || !job || !L || !host_out || !ticket)
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_submit_picture_packed_async: null argument");
-    if (L->sb_results && (L->n_pus == 0 || L->n_pus > SVTME_PU_COUNT || L->max_cand == 0 ||
-                          L->max_cand > SVTME_MAX_PA_ME_CAND || L->max_refs == 0 || L->max_refs > SVTME_MAX_PA_ME_MV))
-        return fail(SVTME_ERR_BAD_PARAMETER, "pack layout: %u PUs, %u candidates, %u MVs", L->n_pus, L->max_cand,
-                    L->max_refs);
-    std::lock_guard<std::mutex> lk(c->mu);
-    HIP_TRY(hipSetDevice(c->device));
-    Ticket *t = nullptr;
-    for (auto &x : c->tickets)
-        if (!x.id) {
-            t = &x;
-            break;
-        }
-    if (!t)
-        return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "%d packed jobs outstanding (svtme_ticket_wait retires them)",
-                    SVTME_MAX_TICKETS);
-    if (!c->dstream)
-        HIP_TRY(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
-    if (!t->done) {
-        HIP_TRY(hipEventCreateWithFlags(&t->launched, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&t->done, hipEventDisableTiming));
-    }
-    const uint32_t total = svtme_sb_total(job->width, job->height);
-    const uint32_t count = job->sb_count ? job->sb_count : (job->sb_begin < total ? total - job->sb_begin : 0);
-    const uint32_t R     = svtme_job_ref_slots(job);
-    const size_t rb      = (size_t)count * R * sizeof(svtme_ref_record);
-    const size_t sbb     = L->sb_results ? (size_t)count * sizeof(svtme_sb_result) : 0;
-    const size_t stride = svtme_packed_sb_bytes(L, R), pb = (size_t)count * stride;
-    const size_t o_sb = (rb + 255) & ~(size_t)255, o_pk = (o_sb + sbb + 255) & ~(size_t)255;
-    svtme_status st;
-    if ((st = ensure_buf(&t->d_mem, &t->d_cap, o_pk + pb))) // the slot is free: nothing reads the old buffer
-        return st;
-    svtme_ref_record *d_recs = (svtme_ref_record *)t->d_mem;
-    svtme_sb_result *d_sb    = L->sb_results ? (svtme_sb_result *)((uint8_t *)t->d_mem + o_sb) : nullptr;
-    void *d_pack             = (uint8_t *)t->d_mem + o_pk;
-    if ((st = submit_batch_locked(c, job, 1, &d_recs, &d_sb, d_sb != nullptr, lane)))
-        return st;
-    hipStream_t ls = c->lanes[lane].s;
-    HIP_TRY(svtme_launch_pack(d_recs, d_sb, count, R, L, d_pack, ls));
-    HIP_TRY(hipEventRecord(t->launched, ls));
-    HIP_TRY(hipStreamWaitEvent(c->dstream, t->launched, 0));
-    HIP_TRY(hipMemcpyAsync(host_out, d_pack, pb, hipMemcpyDeviceToHost, c->dstream));
-    HIP_TRY(hipEventRecord(t->done, c->dstream));
-    t->id   = ++c->ticket_seq;
-    *ticket = t->id;
-    return SVTME_OK;
+    return svtme_submit_pictures_packed_async(c, lane, 1, job, L, &host_out, ticket);
 }
 
 extern "C" svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
@@ -1120,6 +1331,7 @@ extern "C" svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
     std::lock_guard<std::mutex> lk(c->mu);
     t->waiting = false;
     t->id      = 0;
+    c->retired.notify_all();
     if (e != hipSuccess)
         return fail(SVTME_ERR_UNDEFINED, "svtme_ticket_wait: %s", hipGetErrorString(e));
     return SVTME_OK;

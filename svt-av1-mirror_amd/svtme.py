@@ -22,6 +22,7 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 
 PU_COUNT = 85
 MAX_SAD_VALUE = 128 * 128 * 255
+MAX_TICKETS = 64  # SVTME_MAX_TICKETS (include/svtme.h; tests/test_abi.py checks it)
 PAD_FULL, PAD_QUARTER, PAD_SIXTEENTH = 72, 32, 16
 SUB_SAD_SEARCH, FULL_SAD_SEARCH = 0, 1
 ME_MCTF, ME_OPEN_LOOP = 1, 3  # EbMeType (me_context.h:44-51)
@@ -580,6 +581,11 @@ def _job_api_protos(lib):
         _proto(lib, "svtme_picture_upload_10bit", "restype", C.c_int32)
         _proto(lib, "svtme_picture_upload_async", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
         _proto(lib, "svtme_picture_upload_async", "restype", C.c_int32)
+        _proto(lib, "svtme_picture_upload_copy_async", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32,
+                                                                    C.c_uint32])
+        _proto(lib, "svtme_picture_upload_copy_async", "restype", C.c_int32)
+        _proto(lib, "svtme_reserve_pictures", "argtypes", [vp, C.c_uint32, C.c_uint32, C.c_uint32])
+        _proto(lib, "svtme_reserve_pictures", "restype", C.c_int32)
         _proto(lib, "svtme_picture_upload_device", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32, C.c_uint32])
         _proto(lib, "svtme_picture_upload_device", "restype", C.c_int32)
         _proto(lib, "svtme_picture_upload_device_async", "argtypes", [vp, C.c_uint64, vp, C.c_uint32, C.c_uint32,
@@ -687,6 +693,21 @@ class GpuME:
             ptr = y
         self._check(self.lib.svtme_picture_upload_async(self.ctx, picture_number, ptr, stride or w, w, h),
                     "svtme_picture_upload_async")
+
+    def upload_copy_async(self, picture_number: int, y, w: int = 0, h: int = 0, stride: int = 0):
+        """svtme_picture_upload_copy_async: the rows are copied into the library's
+        page-locked staging ring before the call returns; `y` may change after it."""
+        if isinstance(y, np.ndarray):
+            h, w = y.shape
+            stride, ptr = w, y.ctypes.data
+        else:
+            ptr = y
+        self._check(self.lib.svtme_picture_upload_copy_async(self.ctx, picture_number, ptr, stride or w, w, h),
+                    "svtme_picture_upload_copy_async")
+
+    def reserve_pictures(self, width: int, height: int, count: int):
+        """svtme_reserve_pictures: `count` idle picture buffers of that size in the pool."""
+        self._check(self.lib.svtme_reserve_pictures(self.ctx, width, height, count), "svtme_reserve_pictures")
 
     def upload_device(self, picture_number: int, dev_ptr: int, stride: int, w: int, h: int):
         self._check(self.lib.svtme_picture_upload_device(self.ctx, picture_number, dev_ptr, stride, w, h),

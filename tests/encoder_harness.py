@@ -60,6 +60,13 @@ CASES = {
     "360p_p10_lowdelay": (640, 360, 16, 10, False, ["--pred-struct", "1"], True),
     "1080p_p9_lowdelay": (1920, 1080, 8, 9, False, ["--pred-struct", "1"], True),
     "240p_p8_lowdelay": (426, 240, 16, 8, False, ["--pred-struct", "1"], True),
+    # two encoders in one process, one after the other: the passes of a 2-pass VBR encode
+    # (app_main.c main loop, an encoder init / deinit per pass)
+    # (--lp 1: the reference's multi-threaded 2-pass VBR is not deterministic run to run)
+    "360p_p8_2pass": (640, 360, 12, 8, False, ["--passes", "2", "--rc", "1", "--tbr", "500", "--lp", "1"], True),
+    # two encoders at once: --nch 2 channels (app_main.c:196-243), different content at the
+    # same picture numbers and size (the second input starts 7 frames later)
+    "360p_p8_2ch": (640, 360, 12, 8, False, ["--nch", "2"], True),
 }
 
 
@@ -72,7 +79,7 @@ def available(kind: str) -> bool:
     return os.path.exists(encoder(kind))
 
 
-def write_y4m(path: str, w: int, h: int, frames: int, ten_bit: bool) -> None:
+def write_y4m(path: str, w: int, h: int, frames: int, ten_bit: bool, t0: int = 0) -> None:
     import svtme as S
 
     if os.path.exists(path):
@@ -85,7 +92,7 @@ def write_y4m(path: str, w: int, h: int, frames: int, ten_bit: bool) -> None:
         chroma = (np.full(cw * ch, 512, "<u2") if ten_bit else np.full(cw * ch, 128, np.uint8)).tobytes()
         for t in range(frames):
             f.write(b"FRAME\n")
-            y = syn.frame10(t).astype("<u2") if ten_bit else syn.frame(t)
+            y = syn.frame10(t0 + t).astype("<u2") if ten_bit else syn.frame(t0 + t)
             f.write(np.ascontiguousarray(y).tobytes())
             f.write(chroma)
             f.write(chroma)
@@ -112,12 +119,22 @@ def encode(kind: str, case: str, workdir: str, env_extra=None, timeout: int = 60
         env.update({"SVTME_GLUE_STRICT": "1", "SVTME_GLUE_VERIFY": "1", "SVTME_GLUE_STATS": stats})
     env.update(env_extra or {})
     cmd = [encoder(kind), "-i", y4m, "--preset", str(preset), "-b", out] + list(extra)
+    outs = [out]
+    if "--nch" in extra:  # channel k encodes its own input (content k x 7 frames later) into its own output
+        n = int(extra[extra.index("--nch") + 1])
+        ins = [y4m] + [os.path.join(workdir, f"{case}.ch{k}.y4m") for k in range(1, n)]
+        for k in range(1, n):
+            write_y4m(ins[k], w, h, frames, ten_bit, t0=7 * k)
+        outs = [os.path.join(workdir, f"{case}.{kind}.ch{k}.ivf") for k in range(n)]
+        cmd = [encoder(kind), "--nch", str(n), "-i", *ins, "--preset", *[str(preset)] * n, "-b", *outs]
     t0 = time.time()
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
     dt = time.time() - t0
     if r.returncode != 0:
         raise RuntimeError(f"{kind} encoder failed (rc {r.returncode}): {r.stderr[-2000:]}")
-    res = {"kind": kind, "case": case, "md5": _md5(out), "bytes": os.path.getsize(out), "seconds": round(dt, 3)}
+    md5 = _md5(out) if len(outs) == 1 else hashlib.md5("".join(_md5(o) for o in outs).encode()).hexdigest()
+    res = {"kind": kind, "case": case, "md5": md5, "bytes": sum(os.path.getsize(o) for o in outs),
+           "seconds": round(dt, 3)}
     if kind != "ref":
         with open(stats) as f:
             res["glue"] = json.loads(f.read().strip().splitlines()[-1])

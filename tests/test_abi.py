@@ -54,6 +54,7 @@ int main(void) {
     O(svtme_sb_result, me_8x8_cost_variance); O(svtme_sb_result, rc_me_allow_gm);
     O(svtme_controls, prehme_sa_cfg); O(svtme_controls, me_early_exit_th);
     O(svtme_controls, prev_me_stage_based_exit_th);
+    printf("SVTME_MAX_TICKETS %d\n", SVTME_MAX_TICKETS);
     return 0;
 }
 """
@@ -68,6 +69,7 @@ def test_struct_layouts_match_mirrors(svtme, tmp_path):
     got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                                 check=True).stdout.split("\n") if line)
     got = {k: int(v) for k, v in got.items()}
+    assert got["SVTME_MAX_TICKETS"] == S.MAX_TICKETS
     assert got["svtme_controls"] == C.sizeof(S.Controls)
     assert got["svtme_job"] == C.sizeof(S.Job)
     assert got["svtme_ref_record"] == S.REF_RECORD_DTYPE.itemsize == 704

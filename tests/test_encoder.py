@@ -18,7 +18,7 @@ import pytest
 import encoder_harness as E
 
 CPU_CASES = ["ra360_p12", "240p_p8_ragged", "360p_p4", "360p_p8_notf", "360p_superres", "1080p_p8", "4k_p8",
-             "360p_p8_lowdelay", "360p_p10_lowdelay", "240p_p8_lowdelay"]
+             "360p_p8_lowdelay", "360p_p10_lowdelay", "240p_p8_lowdelay", "360p_p8_2pass", "360p_p8_2ch"]
 GPU_CASES = [c for c in E.CASES if c != "4k_p8_64f"]  # the 64-frame encode is scripts/glue_rate.py's
 
 
@@ -36,6 +36,20 @@ def test_bitstream_identical_oracle_backend(case, workdir):
     assert r["verified_job_planes"] >= 3 * (r["pa_jobs"] + r["tf_jobs"])
     assert r["eager_uploads"] > 0
     _no_rtcd_registered(r)
+
+
+@pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
+@pytest.mark.parametrize("case", ["360p_p8_2pass", "360p_p8_2ch"])
+def test_two_encoders_in_one_process(case, workdir):
+    """Two encoders in one process -- the passes of a 2-pass encode one after the
+    other, two --nch channels at once with different content at the same picture
+    numbers -- each keep their own resident pictures (a picture-number range per
+    encoder): both bitstreams equal the reference's, every job's pictures equal
+    the encoder's planes (SVTME_GLUE_VERIFY), and each teardown releases its
+    encoder's pictures."""
+    r = E.check(case, "ora", workdir)
+    assert r["encoders"] == 2 and r["released_at_teardown"] > 0 and r["fallback_sbs"] == 0
+    assert r["verified_job_planes"] >= 3 * (r["pa_jobs"] + r["tf_jobs"])
 
 
 def _no_rtcd_registered(r):

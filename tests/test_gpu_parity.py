@@ -358,6 +358,95 @@ def test_picture_upload_async(svtme, gpu):
         gpu.release(pn)
 
 
+def test_picture_upload_copy_async_and_pool(svtme, gpu):
+    """svtme_picture_upload_copy_async: the rows go through the library's own
+    page-locked staging ring (the caller's buffer is never page-locked), so the
+    caller may overwrite it as soon as the call returns: more uploads than ring
+    slots from ONE reused buffer, each overwritten right after its call, every
+    pyramid equal to the reference's; a re-upload waits for the queued job that
+    reads the old planes. Pictures come from svtme_reserve_pictures' pool and
+    released pictures' memory returns to it (reused, never freed)."""
+    import torch
+
+    S = svtme
+    w, h = 328, 200
+    syn = S.Synth(w, h)
+    gpu.reserve_pictures(w, h, 3)
+    buf = np.empty((h, w), np.uint8)
+    ts = list(range(20, 20 + 2 * 4 + 1))  # > SVTME_UPLOAD_SLOTS uploads from one buffer
+    for t in ts:
+        buf[:] = syn.frame(t)
+        gpu.upload_copy_async(5000 + t, buf)
+        buf[:] = 0  # the caller's buffer is free as soon as the call returns
+    for t in ts:
+        p = S.build_host_pyramid(syn.frame(t), "oracle")
+        for lv, name in enumerate(("full", "quarter", "sixteenth")):
+            assert np.array_equal(gpu.download(5000 + t, lv), getattr(p, name)), (t, name)
+    # a job, then a re-upload of its reference before the job ran (ordering as upload_async)
+    ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
+    W8, H8 = (w + 7) & ~7, (h + 7) & ~7
+    job = S.make_job(W8, H8, ctrl, 5021, (5020,), (5022,), temporal_layer_index=1, ref_count_used=(1, 1))
+    R, n = S.ref_slots(job), S.sb_total(W8, H8)
+    bufs = [torch.zeros(n * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    gpu.submit_batch_device([job], [bufs[0].data_ptr()])
+    buf[:] = syn.frame(40)
+    gpu.upload_copy_async(5020, buf)
+    gpu.submit_batch_device([job], [bufs[1].data_ptr()])
+    gpu.sync()
+    got = [np.frombuffer(b.cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n, R) for b in bufs]
+    pyr = {t: S.build_host_pyramid(syn.frame(t), "oracle") for t in (20, 21, 22, 40)}
+    for ref, g in ((pyr[20], got[0]), (pyr[40], got[1])):
+        orecs, _ = S.run_checker(job, pyr[21], {(0, 0): ref, (1, 0): pyr[22]}, "oracle", nthreads=8)
+        assert not S.compare_records(orecs, g)
+    # released pictures' buffers go back to the pool and serve later uploads
+    for t in ts:
+        gpu.release(5000 + t)
+    gpu.sync()
+    for t in ts:
+        gpu.upload_copy_async(6000 + t, syn.frame(t))
+    for lv, name in enumerate(("full", "quarter", "sixteenth")):
+        assert np.array_equal(gpu.download(6000 + ts[-1], lv), getattr(S.build_host_pyramid(syn.frame(ts[-1]), "oracle"), name))
+    for t in ts:
+        gpu.release(6000 + t)
+
+
+def test_batched_packed_jobs(svtme, gpu):
+    """svtme_submit_pictures_packed_async: several jobs (a TF window's
+    (central, reference) pairs) in ONE launch, each with its own ticket and
+    host output, equal the same jobs submitted one by one."""
+    import ctypes as C
+
+    S = svtme
+    w, h = 640, 360
+    syn = S.Synth(w, h)
+    for t in range(4, 13):
+        gpu.upload(7100 + t, syn.frame(t))
+    ctrl = S.derive_controls_tf(2, 1, 35, S.input_resolution_of(w, h))
+    jobs = [S.case_job(ctrl, w, h, 7108, (7100 + r,), (), 0, me_type=S.ME_MCTF, tf_me_exit_th=0)
+            for r in (4, 5, 6, 7, 9, 10, 11, 12)]
+    L = S.PackLayout()
+    L.n_pus, L.max_cand, L.max_refs, L.full_records, L.sb_results = 0, 0, 0, 1, 0
+    exp = [gpu.submit_packed(j, L) for j in jobs]
+    n = len(jobs)
+    nbytes = len(exp[0])
+    ptrs = [gpu.lib.svtme_host_alloc(nbytes) for _ in range(n)]
+    arr_jobs = (S.Job * n)(*jobs)
+    arr_l = (S.PackLayout * n)(*([L] * n))
+    arr_p = (C.c_void_p * n)(*ptrs)
+    tickets = (C.c_uint64 * n)()
+    gpu.lib.svtme_submit_pictures_packed_async.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(S.Job),
+                                                           C.POINTER(S.PackLayout), C.POINTER(C.c_void_p),
+                                                           C.POINTER(C.c_uint64)]
+    gpu.lib.svtme_submit_pictures_packed_async.restype = C.c_int32
+    gpu._check(gpu.lib.svtme_submit_pictures_packed_async(gpu.ctx, 1, n, arr_jobs, arr_l, arr_p, tickets),
+               "svtme_submit_pictures_packed_async")
+    for k in reversed(range(n)):  # retired in any order
+        assert gpu.wait_packed(tickets[k], ptrs[k], nbytes) == exp[k], k
+    for t in range(4, 13):
+        gpu.release(7100 + t)
+
+
 def test_lanes_parity(svtme, gpu):
     """svtme_submit_batch_device_lane: batches alternating over the two lanes
     (own streams and scratch, overlapping on the GPU), banded full-pel jobs

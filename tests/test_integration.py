@@ -32,7 +32,8 @@ def test_glue_compiles_against_reference_headers(tmp_path):
     for s in ("T svt_aom_setup_rtcd_hip_parity", "T svtme_controls_from_me_context", "T svtme_job_from_pcs",
               "T svtme_job_from_tf", "T svtme_scatter_sb", "T svtme_motion_estimation_b64", "T svtme_picture_changed",
               "U svt_sad_loop_kernel_hip", "U svt_pme_sad_loop_kernel_hip", "U svtme_rtcd_failed",
-              "U svtme_submit_picture_packed_async", "U svtme_ticket_wait", "U svtme_picture_upload_async",
+              "U svtme_submit_pictures_packed_async", "U svtme_ticket_wait", "U svtme_picture_upload_async",
+              "U svtme_picture_upload_copy_async", "U svtme_reserve_pictures",
               "U svtme_picture_release", "U svt_aom_motion_estimation_b64"):
         assert s in syms, s
     for ptr in ("svt_sad_loop_kernel", "svt_nxm_sad_kernel", "downsample_2d", "sad_16b_kernel",
@@ -44,8 +45,10 @@ def test_glue_compiles_against_reference_headers(tmp_path):
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference headers only in the build container")
 def test_glue_wrap_build_exports_wrappers(tmp_path):
-    """-DSVTME_GLUE_WRAP (the --wrap link of oracle/encoder.mk) defines the two
-    wrappers and calls through to the encoder's own functions."""
+    """-DSVTME_GLUE_WRAP (the --wrap link of oracle/encoder.mk) defines the
+    wrappers (the SB function, re-decimation, each encoder's init and deinit, the
+    end of each picture's analysis) and calls through to the encoder's own
+    functions."""
     obj = str(tmp_path / "glue_wrap.o")
     r = subprocess.run(["gcc", "-std=gnu11", "-Wall", "-Werror", "-DSVTME_GLUE_WRAP", "-DARCH_X86_64=1",
                         "-DEN_AVX512_SUPPORT=0", "-c", "-o", obj, GLUE] + _incs(), capture_output=True, text=True)
@@ -53,7 +56,9 @@ def test_glue_wrap_build_exports_wrappers(tmp_path):
     syms = subprocess.run(["nm", obj], capture_output=True, text=True).stdout
     for s in ("T __wrap_svt_aom_motion_estimation_b64", "T __wrap_svt_aom_downsample_filtering_input_picture",
               "U __real_svt_aom_motion_estimation_b64", "U __real_svt_aom_downsample_filtering_input_picture",
-              "T __wrap_svt_av1_enc_deinit", "U __real_svt_av1_enc_deinit"):
+              "T __wrap_svt_av1_enc_deinit", "U __real_svt_av1_enc_deinit",
+              "T __wrap_svt_av1_enc_init", "U __real_svt_av1_enc_init",
+              "T __wrap_svt_post_full_object", "U __real_svt_post_full_object"):
         assert s in syms, s
 
 

@@ -35,7 +35,7 @@ def _setup(api, base):
 def test_reserve_arguments_oracle_backend():
     api = S.GpuME(0, lib=S.load_oracle_job())
     api.reserve(W, H, 8, 4)
-    for bad in ((0, H, 8, 4), (W, H, 0, 4), (W, H, 9, 4), (W, H, 8, 17)):
+    for bad in ((0, H, 8, 4), (W, H, 0, 4), (W, H, 9, 4), (W, H, 8, S.MAX_TICKETS + 1)):
         with pytest.raises(RuntimeError):
             api.reserve(*bad)
     api.close()
@@ -65,13 +65,35 @@ def test_packed_output_gpu(gpu):
     pend = [gpu.submit_packed(job, L, lane=k & 1, wait=False) for k in range(6)]
     for p in reversed(pend):
         assert gpu.wait_packed(*p) == exp
-    # at most SVTME_MAX_TICKETS outstanding: the next one is refused, the context keeps serving
-    pend = [gpu.submit_packed(job, L, lane=k & 1, wait=False) for k in range(16)]
+    # at most SVTME_MAX_TICKETS outstanding: one thread holding them all is refused the
+    # next one (nobody retires a ticket within the grace period), the context keeps serving
+    pend = [gpu.submit_packed(job, L, lane=k & 1, wait=False) for k in range(S.MAX_TICKETS)]
     with pytest.raises(RuntimeError, match="outstanding"):
         gpu.submit_packed(job, L, wait=False)
     for p in pend:
         assert gpu.wait_packed(*p) == exp
     assert gpu.submit_packed(job, L) == exp
+    # more submitting threads than ticket slots (the reference's up to 25 ME threads plus
+    # TF threads, each with a job in flight): a submission finding every slot taken waits
+    # for another thread's svtme_ticket_wait instead of failing
+    import threading
+
+    errs, done = [], []
+
+    def worker(k):
+        try:
+            for _ in range(3):
+                if gpu.submit_packed(job, L, lane=k & 1) != exp:
+                    errs.append(f"thread {k}: packed bytes differ")
+            done.append(k)
+        except Exception as e:  # noqa: BLE001
+            errs.append(f"thread {k}: {e}")
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(S.MAX_TICKETS + 16)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    assert not errs and len(done) == S.MAX_TICKETS + 16, errs[:3]
     # reserved for a larger picture (every lane's scratch, the first tickets' buffers):
     # the same bytes, and a picture beyond the reservation still grows what it needs
     gpu.reserve(W, H // 2, 3, 2)
@@ -79,7 +101,7 @@ def test_packed_output_gpu(gpu):
     for t in LAYOUTS:
         L = _layout(t)
         assert gpu.submit_packed(job, L, lane=1 - (t[0] & 1)) == S.pack_outputs(recs, sbr if L.sb_results else None, L), t
-    for bad in ((0, H, 8, 4), (W, H, 9, 4), (W, H, 8, 17)):
+    for bad in ((0, H, 8, 4), (W, H, 9, 4), (W, H, 8, S.MAX_TICKETS + 1)):
         with pytest.raises(RuntimeError):
             gpu.reserve(*bad)
     for t in (6, 7, 8, 9):
