@@ -395,6 +395,11 @@ svtme_status svtme_submit_pictures_packed_async(svtme_ctx *ctx, uint32_t lane, u
 /* Block until ticket's packed output is in host memory, then retire the ticket.
  * Safe to call from any thread, without holding anything the submitter holds. */
 svtme_status svtme_ticket_wait(svtme_ctx *ctx, uint64_t ticket);
+/* The same, and the job's GPU-side times (HIP events): from its turn on its
+ * lane to its packed output on the device (waits for its pictures' uploads,
+ * the search, the pack), and from there to the output in host memory (the
+ * download stream's copy). Either pointer may be NULL. */
+svtme_status svtme_ticket_wait_timed(svtme_ctx *ctx, uint64_t ticket, float *gpu_ms, float *copy_ms);
 /* Page-locked host memory for packed outputs (NULL on failure), and its release. */
 void *svtme_host_alloc(uint64_t bytes);
 void svtme_host_free(void *p);

@@ -626,6 +626,7 @@ typedef struct GlueTrace { /* one job (SVTME_GLUE_TRACE) */
     int tf;
     uint32_t n_sb, inflight, uploads;
     double t_create, t_submitted, t_done, upload_s;
+    float gpu_ms, copy_ms; /* GPU-side: lane turn -> packed output; -> host memory (svtme_ticket_wait_timed) */
 } GlueTrace;
 
 static double now_s(void) {
@@ -674,9 +675,11 @@ static void glue_trace_at_exit(void) {
     for (uint32_t i = 0; i < G.n_trace; i++) {
         const GlueTrace *t = &G.trace[i];
         fprintf(f, "{\"pn\": %llu, \"tf\": %d, \"sbs\": %u, \"inflight\": %u, \"uploads\": %u, "
-                   "\"upload_ms\": %.4f, \"create_ms\": %.4f, \"submitted_ms\": %.4f, \"done_ms\": %.4f}\n",
+                   "\"upload_ms\": %.4f, \"create_ms\": %.4f, \"submitted_ms\": %.4f, \"done_ms\": %.4f, "
+                   "\"gpu_ms\": %.4f, \"copy_ms\": %.4f}\n",
                 (unsigned long long)(t->pn & GLUE_PN_MASK), t->tf, t->n_sb, t->inflight, t->uploads, 1e3 * t->upload_s,
-                1e3 * (t->t_create - G.t0), 1e3 * (t->t_submitted - G.t0), 1e3 * (t->t_done - G.t0));
+                1e3 * (t->t_create - G.t0), 1e3 * (t->t_submitted - G.t0), 1e3 * (t->t_done - G.t0), t->gpu_ms,
+                t->copy_ms);
     }
     fclose(f);
 }
@@ -1036,7 +1039,7 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
     const double t1 = now_s();
     G.n.upload_s += t1 - t0;
     if (G.trace_path) { /* uploads in the trace too (tf = 2), to place them beside the jobs */
-        const GlueTrace t = {pn & GLUE_PN_MASK, 2, 0, 0, 1, t0, t1, t1, t1 - t0};
+        const GlueTrace t = {pn & GLUE_PN_MASK, 2, 0, 0, 1, t0, t1, t1, t1 - t0, 0, 0};
         pthread_mutex_lock(&G.mu);
         trace_add(&t);
         pthread_mutex_unlock(&G.mu);
@@ -1347,7 +1350,9 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
         double t_wait = now_s();
         for (int k = 0; k < n; k++) {
             /* no glue lock held: other pictures' threads upload and submit meanwhile */
-            const int rk       = rc ? rc : (svtme_ticket_wait(G.ctx, tickets[k]) == SVTME_OK ? 0 : -1);
+            float gms = 0, cms = 0;
+            const int rk =
+                rc ? rc : (svtme_ticket_wait_timed(G.ctx, tickets[k], &gms, &cms) == SVTME_OK ? 0 : -1);
             const double t_done = now_s();
             pthread_mutex_lock(&G.mu);
             if (k == 0) {
@@ -1359,7 +1364,7 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
                 G.n.job_sbs += js[k]->n_sb;
             if (G.trace_path) {
                 const GlueTrace t = {js[k]->job.picture_number, js[k]->job.me_type == SVTME_ME_MCTF, js[k]->n_sb,
-                                     inflight, k ? 0 : (uint32_t)up_n, t_start, t_wait, t_done, k ? 0 : up_s};
+                                     inflight, k ? 0 : (uint32_t)up_n, t_start, t_wait, t_done, k ? 0 : up_s, gms, cms};
                 trace_add(&t);
             }
             js[k]->state = rk ? -1 : 1;

@@ -307,6 +307,14 @@ svtme_status svtme_submit_pictures_packed_async(svtme_ctx *c, uint32_t lane, uin
 
 svtme_status svtme_sync(svtme_ctx *c) { return c ? SVTME_OK : SVTME_ERR_BAD_PARAMETER; }
 
+svtme_status svtme_ticket_wait_timed(svtme_ctx *c, uint64_t ticket, float *gpu_ms, float *copy_ms) {
+    if (gpu_ms)
+        *gpu_ms = 0;
+    if (copy_ms)
+        *copy_ms = 0;
+    return svtme_ticket_wait(c, ticket);
+}
+
 svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
     return c && ticket ? SVTME_OK : ora_fail(SVTME_ERR_BAD_PARAMETER, "svtme_ticket_wait: bad arguments");
 }

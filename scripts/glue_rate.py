@@ -25,8 +25,11 @@ def main():
     cases = sys.argv[2:] or ["4k_p8_64f", "4k_p8_16f", "1080p_p8"]
     wd = os.path.join("/tmp", "svtme_glue_rate")
     res = []
-    for case in cases:
-        ref = E.encode("ref", case, wd)
+    reps = int(os.environ.get("GLUE_RATE_REPEAT", "1"))  # the same encode several times (a rare stall's odds)
+    refs = {}
+    for case in [c for c in cases for _ in range(reps)]:
+        ref = refs.get(case) or E.encode("ref", case, wd)
+        refs[case] = ref
         trace = os.path.join(wd, f"{case}.trace.jsonl")
         got = E.encode("gpu", case, wd, env_extra={"SVTME_GLUE_VERIFY": "0", "SVTME_GLUE_TRACE": trace})
         g = got["glue"]
@@ -41,6 +44,7 @@ def main():
         lat = sorted(j["done_ms"] - j["create_ms"] for j in jobs)
         # jobs above 1 ms and the uploads that overlapped them (a stall's candidates)
         r["long_jobs"] = [{"pn": j["pn"], "tf": j["tf"], "ms": round(j["done_ms"] - j["create_ms"], 3),
+                           "gpu_ms": j.get("gpu_ms"), "copy_ms": j.get("copy_ms"),
                            "uploads_overlapping": [u["pn"] for u in ups
                                                    if u["create_ms"] < j["done_ms"] and u["done_ms"] > j["create_ms"]]}
                           for j in jobs if j["done_ms"] - j["create_ms"] > 1.0]

@@ -120,6 +120,7 @@ struct Lane {
 struct Ticket {
     uint64_t id = 0;               // 0: the slot is free
     bool waiting = false;          // a thread is blocked on `done`
+    hipEvent_t queued = nullptr;   // the job's turn on its lane (timing: svtme_ticket_wait_timed)
     hipEvent_t launched = nullptr; // end of the job's launches on its lane
     hipEvent_t done = nullptr;     // end of the copy into host memory (download stream)
     void *d_mem = nullptr;         // records | SB results | packed bytes
@@ -297,6 +298,8 @@ extern "C" void svtme_ctx_destroy(svtme_ctx *c) {
             (void)hipFree(t.d_mem);
         if (t.launched)
             (void)hipEventDestroy(t.launched);
+        if (t.queued)
+            (void)hipEventDestroy(t.queued);
         if (t.done)
             (void)hipEventDestroy(t.done);
     }
@@ -1267,8 +1270,9 @@ extern "C" svtme_status svtme_submit_pictures_packed_async(svtme_ctx *c, uint32_
         const svtme_job *job       = &jobs[k];
         const svtme_pack_layout *L = &layouts[k];
         if (!t[k]->done) {
-            HIP_TRY(hipEventCreateWithFlags(&t[k]->launched, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&t[k]->done, hipEventDisableTiming));
+            HIP_TRY(hipEventCreate(&t[k]->queued)); // timing events: svtme_ticket_wait_timed
+            HIP_TRY(hipEventCreate(&t[k]->launched));
+            HIP_TRY(hipEventCreate(&t[k]->done));
         }
         const uint32_t total = svtme_sb_total(job->width, job->height);
         counts[k] = job->sb_count ? job->sb_count : (job->sb_begin < total ? total - job->sb_begin : 0);
@@ -1284,6 +1288,10 @@ extern "C" svtme_status svtme_submit_pictures_packed_async(svtme_ctx *c, uint32_
         d_pack[k] = (uint8_t *)t[k]->d_mem + o_pk;
         any_sb |= d_sb[k] != nullptr;
     }
+    if ((st = ensure_lane(c, lane)))
+        return st;
+    for (uint32_t k = 0; k < n; k++)
+        HIP_TRY(hipEventRecord(t[k]->queued, c->lanes[lane].s));
     // one launch over every job (the stage kernels take up to SVTME_MAX_BATCH jobs)
     if ((st = submit_batch_locked(c, jobs, n, d_recs, d_sb, any_sb, lane)))
         return st;
@@ -1308,7 +1316,7 @@ extern "C" svtme_status svtme_submit_picture_packed_async(svtme_ctx *c, uint32_t
     return svtme_submit_pictures_packed_async(c, lane, 1, job, L, &host_out, ticket);
 }
 
-extern "C" svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
+extern "C" svtme_status svtme_ticket_wait_timed(svtme_ctx *c, uint64_t ticket, float *gpu_ms, float *copy_ms) {
     if (!c || !ticket)
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_ticket_wait: null ctx or ticket");
     hipEvent_t done = nullptr;
@@ -1327,7 +1335,12 @@ extern "C" svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
         done       = t->done;
     }
     HIP_TRY(hipSetDevice(c->device));
-    const hipError_t e = hipEventSynchronize(done); // without the context lock: other threads submit meanwhile
+    hipError_t e = hipEventSynchronize(done); // without the context lock: other threads submit meanwhile
+    // GPU-side times: the job's turn on its lane -> its packed output ready; -> in host memory
+    if (e == hipSuccess && gpu_ms)
+        e = hipEventElapsedTime(gpu_ms, t->queued, t->launched);
+    if (e == hipSuccess && copy_ms)
+        e = hipEventElapsedTime(copy_ms, t->launched, t->done);
     std::lock_guard<std::mutex> lk(c->mu);
     t->waiting = false;
     t->id      = 0;
@@ -1335,6 +1348,10 @@ extern "C" svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
     if (e != hipSuccess)
         return fail(SVTME_ERR_UNDEFINED, "svtme_ticket_wait: %s", hipGetErrorString(e));
     return SVTME_OK;
+}
+
+extern "C" svtme_status svtme_ticket_wait(svtme_ctx *c, uint64_t ticket) {
+    return svtme_ticket_wait_timed(c, ticket, nullptr, nullptr);
 }
 
 extern "C" svtme_status svtme_set_timing(svtme_ctx *c, int enable) {

@@ -32,7 +32,7 @@ def test_glue_compiles_against_reference_headers(tmp_path):
     for s in ("T svt_aom_setup_rtcd_hip_parity", "T svtme_controls_from_me_context", "T svtme_job_from_pcs",
               "T svtme_job_from_tf", "T svtme_scatter_sb", "T svtme_motion_estimation_b64", "T svtme_picture_changed",
               "U svt_sad_loop_kernel_hip", "U svt_pme_sad_loop_kernel_hip", "U svtme_rtcd_failed",
-              "U svtme_submit_pictures_packed_async", "U svtme_ticket_wait", "U svtme_picture_upload_async",
+              "U svtme_submit_pictures_packed_async", "U svtme_ticket_wait_timed", "U svtme_picture_upload_async",
               "U svtme_picture_upload_copy_async", "U svtme_reserve_pictures",
               "U svtme_picture_release", "U svt_aom_motion_estimation_b64"):
         assert s in syms, s
