@@ -902,9 +902,10 @@ static svtme_status prepare(svtme_ctx *c) {
     if ((st = ensure_ustream(c)) || (st = ensure_ring(c)))
         return st;
     HIP_TRY(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
-    for (auto &t : c->tickets) {
-        HIP_TRY(hipEventCreateWithFlags(&t.launched, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+    for (auto &t : c->tickets) { // timing events: svtme_ticket_wait_timed
+        HIP_TRY(hipEventCreate(&t.queued));
+        HIP_TRY(hipEventCreate(&t.launched));
+        HIP_TRY(hipEventCreate(&t.done));
     }
     // The first work on a stream and the first large copy in each direction cost
     // milliseconds of one-time runtime setup (the first packed job's D2H copy call
@@ -1269,11 +1270,6 @@ extern "C" svtme_status svtme_submit_pictures_packed_async(svtme_ctx *c, uint32_
     for (uint32_t k = 0; k < n; k++) {
         const svtme_job *job       = &jobs[k];
         const svtme_pack_layout *L = &layouts[k];
-        if (!t[k]->done) {
-            HIP_TRY(hipEventCreate(&t[k]->queued)); // timing events: svtme_ticket_wait_timed
-            HIP_TRY(hipEventCreate(&t[k]->launched));
-            HIP_TRY(hipEventCreate(&t[k]->done));
-        }
         const uint32_t total = svtme_sb_total(job->width, job->height);
         counts[k] = job->sb_count ? job->sb_count : (job->sb_begin < total ? total - job->sb_begin : 0);
         Rs[k]     = svtme_job_ref_slots(job);

@@ -1214,6 +1214,24 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
 #pragma unroll
         for (int qq = 0; qq < HQ16; qq++) acc[t][qq] = 0;
     Row8 buf[3];
+#if defined(SVTME_DIAG_A1) && SVTME_DIAG_A1 == 1 // diagnostic: every lane reads the first lane's rows (broadcast loads)
+#define row8 row8_diag
+    auto row8_diag = [&](const uint8_t *, int st, int ro, int q) {
+        typedef __attribute__((address_space(1))) const u32x2a4 gu2;
+        const uint32_t *rp = (const uint32_t *)(uni_ptr(a0) + (ptrdiff_t)__builtin_amdgcn_readfirstlane(ro) * st) +
+                             __builtin_amdgcn_readfirstlane(q);
+        return Row8{ldg4(rp), *(gu2 *)(uintptr_t)(rp + 4)};
+    };
+#elif defined(SVTME_DIAG_A1) && SVTME_DIAG_A1 == 2 // diagnostic: no loads, rows synthesised in registers
+#define row8 row8_diag
+    auto row8_diag = [&](const uint8_t *, int, int ro, int q) {
+        const uint32_t x = (uint32_t)ro * 2654435761u + (uint32_t)q;
+        Row8 r;
+        r.lo = u32x4a4{x, x ^ 0x5A5A5A5Au, x + 0x01010101u, x >> 3};
+        r.hi = u32x2a4{x * 3u, x ^ 0x33333333u};
+        return r;
+    };
+#endif
     buf[0] = row8(a0, stride, min(yf, ylast), q0);
     buf[1] = row8(a0, stride, min(yf + 2, ylast), q0);
 #pragma unroll
@@ -1270,6 +1288,9 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
     }
     return best;
 }
+#ifdef row8
+#undef row8
+#endif
 
 // One quarter of the SADs of the 32 x kh1 (sub) quarter-resolution source
 // block (LDS, rows 32 bytes apart) at HQ1 quads of position row y of a 1/4
