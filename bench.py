@@ -165,6 +165,12 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group("gloo")
+        # self-check of the launch: the process group spans exactly the ranks the launcher started
+        if dist.get_world_size() != world or dist.get_rank() != rank:
+            raise SystemExit(f"torch.distributed has rank {dist.get_rank()} of {dist.get_world_size()}, the launcher "
+                             f"set RANK={rank} WORLD_SIZE={world}")
+        if args.gpus != world:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
     import svtme as S
     import svtme_dist as D
@@ -488,12 +494,16 @@ def main():
                                            "time; the GPU also runs the pre-HME / HME-L0 searches the reference "
                                            "may skip, in the same pass (DESIGN.md 4)"})
 
+    devices = sorted(set(gather_devices(dist, local_rank, dev)))  # (a collective: every rank)
     if rank == 0:
         out = {
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "SB/s",
             "n_gpus": world,
+            "ranks": {"world_size_env": world, "process_group": dist.get_world_size() if dist else 1,
+                      "backend": (dist.get_backend() if dist else None),
+                      "devices": devices},
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -555,6 +565,18 @@ def main():
         dist.destroy_process_group()
 
 
+def gather_devices(dist, local_rank, dev):
+    """The HIP device of every rank (one process per GPU: N distinct devices)."""
+    if dist is None:
+        return [local_rank]
+    import torch
+
+    t = torch.tensor([local_rank], dtype=torch.int64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [int(o.item()) for o in out]
+
+
 def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, steps, fence):
     """SURVEY.md 8(e) / BASELINE configs[4]: ONE 7680x4320 p8 picture per step,
     its SBs split in N equal chunks (D.BandSplit): the picture's 8-bit luma plane
@@ -597,7 +619,10 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, steps, fence):
     searched, gathered = [torch.cuda.Event() for _ in range(2)], [torch.cuda.Event() for _ in range(2)]
     host = torch.from_numpy(frames[8].reshape(-1)).pin_memory() if rank == 0 or world == 1 else None
     host_all = torch.from_numpy(frames[8].reshape(-1)).pin_memory()  # the per-rank PCIe variant
-    planes = [torch.empty(Wd * Ht, dtype=torch.uint8, device=dev) for _ in range(2)]
+    ps = D.PlaneSlices(Wd, Ht, world, rank)  # the sliced variant: this rank's rows only
+    host_mine = torch.from_numpy(ps.host_rows(frames[8]).copy()).pin_memory()
+    slices = [torch.zeros(ps.slice_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+    planes = [torch.empty(max(Wd * Ht, ps.plane_bytes), dtype=torch.uint8, device=dev) for _ in range(2)]
     ustream = torch.cuda.ExternalStream(gpu.upload_stream(), device=dev)
     copy = torch.cuda.Stream(device=dev)
     arrived, built = [torch.cuda.Event() for _ in range(2)], [torch.cuda.Event() for _ in range(2)]
@@ -609,15 +634,22 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, steps, fence):
         copy.wait_event(built[b])  # the pyramid build two pictures back has read planes[b]
         if mode == "pcie" or world == 1:
             with torch.cuda.stream(copy):
-                planes[b].copy_(host_all, non_blocking=True)
+                planes[b][: Wd * Ht].copy_(host_all, non_blocking=True)
             arrived[b].record(copy)
+        elif mode == "sliced":  # every rank uploads its H/N rows, one RCCL all-gather over xGMI assembles the plane
+            with torch.cuda.stream(copy):
+                slices[b][: host_mine.numel()].copy_(host_mine, non_blocking=True)
+            arrived[b].record(copy)
+            comm.wait_event(arrived[b])
+            ps.gather(slices[b], planes[b][: ps.plane_bytes], dist, stream=comm)
+            arrived[b].record(comm)
         else:  # rank 0 uploads, one RCCL broadcast over xGMI fans the plane out
             if rank == 0:
                 with torch.cuda.stream(copy):
                     planes[b].copy_(host, non_blocking=True)
             arrived[b].record(copy)
             comm.wait_event(arrived[b])
-            D.broadcast_plane(planes[b], dist, src=0, stream=comm)
+            D.broadcast_plane(planes[b][: Wd * Ht], dist, src=0, stream=comm)
             arrived[b].record(comm)
         ustream.wait_event(arrived[b])
         gpu.upload_device_async(cur[b], planes[b].data_ptr(), Wd, Wd, Ht)
@@ -648,7 +680,7 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, steps, fence):
             ms = float(t.item())
         return ms
 
-    modes = ("pcie",) if world == 1 else ("broadcast", "pcie")
+    modes = ("pcie",) if world == 1 else ("sliced", "broadcast", "pcie")
     for i in range(4):
         distribute(i, modes[0])
         search(i)
@@ -677,8 +709,11 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, steps, fence):
             "value": round(n_sb / (step_ms * 1e-3), 1), "value_resident_input": round(n_sb / (pair_ms * 1e-3), 1),
             "unit": "SB/s", "scaling": "strong",
             "allgather_bytes_per_rank": split.gather_bytes_in,
+            "pcie_bytes_per_rank": {"pcie": Wd * Ht, "broadcast": Wd * Ht if rank == 0 else 0,
+                                    "sliced": (ps.r1 - ps.r0) * Wd},
             "note": "value = SBs of the picture / the pipelined step (the current picture's 8-bit plane distributed "
-                    "to every rank -- pcie: each rank's own upload; broadcast: rank 0 uploads, RCCL broadcast -- "
+                    "to every rank -- pcie: each rank's own upload; broadcast: rank 0 uploads, RCCL broadcast; "
+                    "sliced: each rank uploads its H/N rows, one RCCL all-gather assembles the plane -- "
                     "its pyramid built on device, the chunk searched, the records all-gathered), max over ranks; "
                     "value_resident_input: search + all-gather with the picture already resident; the parts "
                     "timed alone"}

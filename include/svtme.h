@@ -442,6 +442,7 @@ uint32_t svtme_timing_read(svtme_ctx *ctx, float stage_ms[5]);
 #define SVTME_PATH_NO_L0_FULL 4u   /* SVTME_NO_L0_FULL: full-SAD stage A on k_stage_a, not k_l0_full */
 #define SVTME_PATH_NO_FP_WIDE 8u   /* SVTME_NO_FP_WIDE: wide full-pel areas on k_stage_c1, not k_fp_wide */
 #define SVTME_PATH_SPLIT_PASS 16u  /* SVTME_SPLIT_PASS: k_hme -> k_stage_c1 -> k_stage_e, not one k_hme */
+#define SVTME_PATH_NO_A1_GATE 32u  /* SVTME_NO_A1_GATE: list-1 pre-HME searched with list 0 (no second A1 round) */
 svtme_status svtme_set_paths(svtme_ctx *ctx, uint32_t paths);
 /* Device pointer of the last job's record buffer (for RCCL all-gather). */
 void *svtme_device_records(svtme_ctx *ctx, uint64_t *bytes);

@@ -227,7 +227,7 @@ extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
         uint32_t bit;
     } env_paths[] = {{"SVTME_NO_FUSED_HME", SVTME_PATH_NO_FUSED_HME}, {"SVTME_NO_L1_FULL", SVTME_PATH_NO_L1_FULL},
                      {"SVTME_NO_L0_FULL", SVTME_PATH_NO_L0_FULL},       {"SVTME_NO_FP_WIDE", SVTME_PATH_NO_FP_WIDE},
-                     {"SVTME_SPLIT_PASS", SVTME_PATH_SPLIT_PASS}};
+                     {"SVTME_SPLIT_PASS", SVTME_PATH_SPLIT_PASS},     {"SVTME_NO_A1_GATE", SVTME_PATH_NO_A1_GATE}};
     for (const auto &e : env_paths)
         if (const char *v = getenv(e.var))
             if (*v && strcmp(v, "0") != 0)
@@ -242,7 +242,7 @@ extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
 }
 
 extern "C" svtme_status svtme_set_paths(svtme_ctx *c, uint32_t paths) {
-    if (!c || (paths & ~31u))
+    if (!c || (paths & ~63u))
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_set_paths: null ctx or unknown path bits 0x%x", paths);
     std::lock_guard<std::mutex> lk(c->mu);
     c->paths = paths;

@@ -3745,6 +3745,7 @@ struct HmeA { // state of phases A0 .. B
     HSrch srch[48];
     int32_t nsrch, nitems;
     int32_t nitems3, base2; // end of the HT16-row tiles; first item of the 2-row group (64-aligned)
+    int32_t end1, base3;    // end of the first A1 round; first item of the gated list-1 pre-HME group
     unsigned long long key1[32];
     int16_t x1o[32], y1o[32];
     HSrch1 s1[32];
@@ -3763,9 +3764,13 @@ struct HmeA { // state of phases A0 .. B
 // 1800-1867, called in slot order by hme_level0_b64 :1974-2036); then RND 1
 // has every search but those, and RND 2 those alone: the slots of bit set
 // l0need, areas from the centre (l00x, l00y)
+// GATE (RND 0): the list-1 pre-HME regions form a group of their own after the
+// others, searched in a second round only where check_prehme_early_exit
+// (motion_estimation.c:1693-1719) does not mirror list 0's result (a1_gated)
 template <int RND>
 __device__ __forceinline__ void a1_table(HmeA &A, const DevJob &dj, uint32_t vmask, int16_t sox, int16_t soy, int kh,
-                                         uint32_t l0need = 0, int16_t l00x = 0, int16_t l00y = 0) {
+                                         uint32_t l0need = 0, int16_t l00x = 0, int16_t l00y = 0,
+                                         bool gate = false) {
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
     const int lane          = threadIdx.x & 63;
@@ -3833,28 +3838,55 @@ __device__ __forceinline__ void a1_table(HmeA &A, const DevJob &dj, uint32_t vma
     // fewer wavefront-rows: the 3-row group first, the 2-row group from the next
     // multiple of 64 items
     const bool l0    = k >= 2;
-    const int n3_pre = (int)wave_sum_u32(mk && !l0 ? (uint32_t)items3 : 0u);
+    const bool g     = RND == 0 && gate && mk && !l0 && l == 1; // the gated group (second round)
+    const int n3_pre = (int)wave_sum_u32(mk && !l0 && !g ? (uint32_t)items3 : 0u);
     const int n3_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items3 : 0u);
     const int n2_l0  = (int)wave_sum_u32(mk && l0 ? (uint32_t)items2 : 0u);
     const bool split = ((n3_pre + 63) / 64) * HT16 + ((n2_l0 + 63) / 64) * 2 < ((n3_pre + n3_l0 + 63) / 64) * HT16;
     const bool t2    = mk && split && l0;
     const int items  = t2 ? items2 : items3;
     e.tt             = (uint8_t)(t2 ? 2 : HT16);
-    int n3s, n2s;
-    const int k3 = wave_compact(mk && !t2, &n3s), k2 = wave_compact(t2, &n2s);
-    const int i3 = wave_incl_scan(mk && !t2 ? items : 0), i2 = wave_incl_scan(t2 ? items : 0);
-    const int N3 = (int)lane63((uint32_t)i3), N2 = (int)lane63((uint32_t)i2);
+    int n3s, n2s, ngs;
+    const int k3 = wave_compact(mk && !t2 && !g, &n3s), k2 = wave_compact(t2, &n2s), kg = wave_compact(g, &ngs);
+    const int i3 = wave_incl_scan(mk && !t2 && !g ? items : 0), i2 = wave_incl_scan(t2 ? items : 0);
+    const int ig = wave_incl_scan(g ? items : 0);
+    const int N3 = (int)lane63((uint32_t)i3), N2 = (int)lane63((uint32_t)i2), NG = (int)lane63((uint32_t)ig);
     const int base2 = (N3 + 63) & ~63;
+    const int end1  = N2 ? base2 + N2 : N3;
+    const int base3 = (end1 + 63) & ~63;
     if (mk) {
-        e.item0                          = t2 ? base2 + i2 - items : i3 - items;
-        A.srch[t2 ? n3s + k2 : k3] = e;
+        e.item0 = g ? base3 + ig - items : t2 ? base2 + i2 - items : i3 - items;
+        A.srch[g ? n3s + n2s + kg : t2 ? n3s + k2 : k3] = e;
     }
     if (lane == 0) {
-        A.nsrch   = n3s + n2s;
+        A.nsrch   = n3s + n2s + ngs;
         A.nitems3 = N3;
         A.base2   = base2;
-        A.nitems  = N2 ? base2 + N2 : N3;
+        A.end1    = end1;
+        A.base3   = NG ? base3 : end1;
+        A.nitems  = NG ? base3 + NG : end1;
     }
+}
+
+// A1's second round: does check_prehme_early_exit (motion_estimation.c:1693-1719)
+// search list-1 pre-HME region e? Its mirror of list 0's region (l1_early_exit:
+// sad < 32 x 32 or |mv| < 16 in both components) needs list 0's result, final
+// after the first round: zz early exit of the list-0 slot (valid, sad 0), or its
+// search's key decoded as phase D decodes it. Only a certain mirror skips the
+// search (dec_prehme then takes the mirror without reading the key).
+__device__ __forceinline__ bool a1_mirrored(const HmeA &A, const svtme_controls &c, uint32_t need, int id) {
+    const int r = ((id - SVTME_A_PH) >> 1) & 3, k = (id - SVTME_A_PH) & 1;
+    if (c.me_early_exit_th && A.d.zz[r] < c.me_early_exit_th)
+        return true;
+    if (!((need >> (2 * r)) & 1u))
+        return false;
+    const int id0 = SVTME_A_PH + 2 * r + k;
+    uint32_t best;
+    int x, y;
+    key_result(A.key[id0], &best, &x, &y);
+    const uint32_t sad = best * 2; // sub-sampled rows (the gated layout is SUB_SAD HME only)
+    const int16_t col = i16((x + A.kxo[id0]) * 4), row = i16((y + A.kyo[id0]) * 4); // as phase D stores them
+    return sad < 32 * 32 || (absi(col) < 16 && absi(row) < 16);
 }
 
 // k_hme shared memory: the job copy, the SB's HME state, the per-record
@@ -3919,7 +3951,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         dec_init(d);
         if (lane < SVTME_A_N)
             sh.u.a.key[lane] = ~0ull;
-        a1_table<RT ? 1 : 0>(sh.u.a, dj, vmask, sox, soy, kh);
+        // list-1 pre-HME regions in a second, gated A1 round (a1_mirrored)
+        const bool gate = !RT && c.prehme_enable && c.prehme_l1_early_exit && job.num_lists == 2 &&
+                          c.hme_search_method != SVTME_FULL_SAD_SEARCH && !(dj.paths & SVTME_PATH_NO_A1_GATE);
+        a1_table<RT ? 1 : 0>(sh.u.a, dj, vmask, sox, soy, kh, 0, 0, 0, gate);
     } else {
         if (zz_on) {
             // the wave's slots are wid - 1, wid + 2, wid + 5: the current rows are
@@ -3997,7 +4032,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                                             : !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th));
         const unsigned long long m = __ballot(nd);
         if (lane == 0)
+#ifdef SVTME_DIAG_NO_L1_PREHME // diagnostic (wrong results): no list-1 pre-HME search, the cost of those tiles
+            sh.u.a.need = (uint32_t)m & ~0x5500u;
+#else
             sh.u.a.need = (uint32_t)m;
+#endif
     }
     __syncthreads();
     HME_PRIO_LO();
@@ -4018,14 +4057,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         const int nitems = sh.u.a.nitems, nsrch = sh.u.a.nsrch;
         const uint32_t need = sh.u.a.need;
         const int pstride = dj.cur.lv[2].stride; // every plane of one level shares the geometry
-        const int nitems3 = sh.u.a.nitems3, base2 = sh.u.a.base2;
-        auto tiles = [&](auto fullk) {
-            for (int it = tid; it < nitems; it += 256) {
+        const int nitems3 = sh.u.a.nitems3, base2 = sh.u.a.base2, end1 = sh.u.a.end1, base3 = sh.u.a.base3;
+        // round 1: items [0, end1); round 2 (gated list-1 pre-HME): [base3, nitems), after a barrier
+        auto tiles = [&](auto fullk, int lo, int hi, bool gated) {
+            for (int it = lo + tid; it < hi; it += 256) {
                 if (it >= nitems3 && it < base2)
                     continue; // the padding before the 2-row group
                 const HSrch &e = sh.u.a.srch[find_search(sh.u.a.srch, nsrch, it)];
                 if (!((need >> e.need) & 1u))
                     continue;
+                if (gated && a1_mirrored(sh.u.a, c, need, e.id))
+                    continue; // phase D mirrors list 0's result (check_prehme_early_exit)
                 const int local = it - e.item0;
                 const int rt = mdiv(local, e.ncm), col = local - rt * e.ncols;
                 // the wavefront's tiles all have e.tt rows (the groups are 64-aligned)
@@ -4047,13 +4089,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                     if (kk != ~0ull)
                         atomicMin(&sh.u.a.key[e.id], kk);
                 };
-                if (UNI(it >= base2))
+                if (UNI(it >= base2 && it < base3))
                     run(std::integral_constant<int, 2>());
                 else
                     run(std::integral_constant<int, HT16>());
             }
         };
-        tiles(std::false_type()); // (a kh == 8 specialisation spills: the scheduler hoists every row)
+        tiles(std::false_type(), 0, end1, false); // (a kh == 8 specialisation spills: the scheduler hoists every row)
+        if (base3 < nitems) { // (workgroup-uniform)
+            __syncthreads();
+            tiles(std::false_type(), base3, nitems, true);
+        }
     };
     a1_tiles();
     if constexpr (RT) {

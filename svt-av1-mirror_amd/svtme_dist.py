@@ -80,6 +80,38 @@ def broadcast_plane(plane, dist, src: int = 0, group=None, stream=None):
     return plane
 
 
+class PlaneSlices:
+    """SURVEY.md 8(e) input distribution that scales with the ranks: rank r
+    copies rows [r * rows, (r + 1) * rows) of the current H x W luma plane
+    (rows = ceil(H / world)) from host memory over ITS OWN PCIe link into a
+    device slice, and one all_gather_into_tensor over xGMI assembles the whole
+    plane on every rank (the gathered buffer holds world x rows rows; those past
+    H are padding nobody reads). Each rank then builds the pyramid from it
+    (svtme_picture_upload_device_async). PCIe bytes per rank: H W / world,
+    against H W for every rank uploading the whole plane or for rank 0 before a
+    broadcast."""
+
+    def __init__(self, width: int, height: int, world: int, rank: int):
+        self.w, self.h, self.world, self.rank = width, height, world, rank
+        self.rows = -(-height // world)
+        self.r0 = min(rank * self.rows, height)
+        self.r1 = min(height, self.r0 + self.rows)
+        self.slice_bytes = self.rows * width
+        self.plane_bytes = world * self.slice_bytes
+
+    def host_rows(self, frame):
+        """This rank's rows of the plane (a view of the H x W frame, flattened)."""
+        return frame[self.r0: self.r1].reshape(-1)
+
+    def gather(self, d_slice, d_plane, dist, group=None, stream=None):
+        """d_slice: uint8 tensor of slice_bytes (this rank's rows first);
+        d_plane: uint8 tensor of plane_bytes; its first H x W bytes are the plane."""
+        if self.world == 1:
+            d_plane[: self.slice_bytes].copy_(d_slice)
+            return d_plane
+        return gather_chunks_device(d_slice, d_plane, dist, group=group, stream=stream)
+
+
 def gather_chunks_device(d_local, d_out, dist, group=None, stream=None):
     """All-gather the ranks' record chunks between device buffers.
 

@@ -197,7 +197,7 @@ def test_owner_exchange_equals_single_rank(svtme, tmp_path, world, k):
         assert not S.compare_records(ref, full)
 
 
-def _bcast_worker(rank, world, port, out_path, n_pics):
+def _bcast_worker(rank, world, port, out_path, n_pics, mode="broadcast"):
     """bench.py's band_8k step on CPU: rank 0 holds the current picture's luma
     plane, one broadcast (svtme_dist.broadcast_plane) gives it to every rank,
     every rank builds the pyramid from what it received, searches its equal SB
@@ -227,8 +227,17 @@ def _bcast_worker(rank, world, port, out_path, n_pics):
         frames = S.test_frames("pan", w, h, [cur - 1, cur - 2, cur, cur + 1])
         refs = {(0, 0): S.build_host_pyramid(frames[cur - 1]), (0, 1): S.build_host_pyramid(frames[cur - 2]),
                 (1, 0): S.build_host_pyramid(frames[cur + 1])}  # resident: distributed with earlier pictures
-        plane = torch.from_numpy(frames[cur].copy()) if rank == 0 else torch.zeros((h, w), dtype=torch.uint8)
-        D.broadcast_plane(plane, dist, src=0)
+        if mode == "broadcast":
+            plane = torch.from_numpy(frames[cur].copy()) if rank == 0 else torch.zeros((h, w), dtype=torch.uint8)
+            D.broadcast_plane(plane, dist, src=0)
+        else:  # sliced: each rank holds (uploads) only its rows; one all-gather assembles the plane
+            ps = D.PlaneSlices(w, h, world, rank)
+            sl = torch.zeros(ps.slice_bytes, dtype=torch.uint8)
+            mine = torch.from_numpy(ps.host_rows(frames[cur]).copy())
+            sl[: mine.numel()] = mine
+            full = torch.zeros(ps.plane_bytes, dtype=torch.uint8)
+            ps.gather(sl, full, dist)
+            plane = full[: h * w].reshape(h, w)
         local = torch.zeros(split.chunk_bytes, dtype=torch.uint8)
         if split.count:
             job = S.case_job(ctrl, w, h, cur, (cur - 1, cur - 2), (cur + 1,), 1, sb_begin=split.begin,
@@ -244,11 +253,15 @@ def _bcast_worker(rank, world, port, out_path, n_pics):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["broadcast", "sliced"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_broadcast_chunked_search_allgather_equals_single_rank(svtme, tmp_path, world):
+def test_broadcast_chunked_search_allgather_equals_single_rank(svtme, tmp_path, world, mode):
+    """The input either broadcast from rank 0 or uploaded in row slices (each
+    rank its own rows, svtme_dist.PlaneSlices) and all-gathered; then the
+    chunked search and the record all-gather: bit-identical to one rank."""
     S = svtme
     out = str(tmp_path / "bcast")
-    mp.spawn(_bcast_worker, args=(world, _free_port(), out, 2), nprocs=world, join=True)
+    mp.spawn(_bcast_worker, args=(world, _free_port(), out, 2, mode), nprocs=world, join=True)
     w, h = 264, 200
     ctrl = S.derive_controls(8, 35, S.input_resolution_of(w, h), 1)
     for rank in range(world):  # every rank holds every picture's records
