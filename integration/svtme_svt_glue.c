@@ -67,11 +67,12 @@
  * buffers (registrations, register_ms) and the one-off pool fill (prefill_ms); and
  * the rtcd check: how many of the pointers parity mode replaces changed since
  * the first SB call, and how many point at this file's HIP wrappers);
- * SVTME_GLUE_RESIDENT caps the resident pictures (default 128); SVTME_GLUE_PIN=1
- * page-locks the encoder's picture buffers and uploads straight from them
- * instead of through the library's page-locked staging (see
- * svtme_picture_upload_copy_async: a page-locked user buffer is a driver
- * user-pointer mapping whose invalidations stall the GPU queues).
+ * SVTME_GLUE_RESIDENT caps the resident pictures (default 128); SVTME_GLUE_PIN=0
+ * uploads through the library's own page-locked staging
+ * (svtme_picture_upload_copy_async) instead of page-locking the encoder's
+ * picture buffers and copying straight from them (measured: the staging copies
+ * run on the analysis threads under the submission lock and delay jobs by
+ * milliseconds in bursts of uploads).
  */
 #include <pthread.h>
 #include <stddef.h>
@@ -735,7 +736,7 @@ static void glue_init(void) {
     G.strict       = (e = getenv("SVTME_GLUE_STRICT")) && atoi(e);
     G.verify       = (e = getenv("SVTME_GLUE_VERIFY")) && atoi(e);
     G.eager        = !(e = getenv("SVTME_GLUE_EAGER")) || atoi(e);
-    G.pin          = (e = getenv("SVTME_GLUE_PIN")) && atoi(e);
+    G.pin          = !(e = getenv("SVTME_GLUE_PIN")) || atoi(e);
     G.tf_batch     = !(e = getenv("SVTME_GLUE_TF_BATCH")) || atoi(e);
     G.max_resident = (e = getenv("SVTME_GLUE_RESIDENT")) ? atoi(e) : 128;
     if (G.max_resident < 9)

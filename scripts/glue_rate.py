@@ -7,7 +7,7 @@ search and the packed copy back included), mean job latency, jobs in flight.
 
 usage: python scripts/glue_rate.py OUT.json [case ...]   (default: 4k_p8_64f 4k_p8_16f 1080p_p8)
 (environment: SVTME_GLUE_* of integration/svtme_svt_glue.c pass through, e.g.
-SVTME_GLUE_PIN=1 for the page-locked-encoder-buffer uploads)
+SVTME_GLUE_PIN=0 for uploads through the library's staging ring)
 """
 import json
 import os
