@@ -1,7 +1,7 @@
 """Why the first launches of a fresh process run slower: the in-kernel clock of
 k_hme over time, from a diagnostic build (-DSVTME_CLOCKBINS).
 
-Build (container):  scripts/build_diag_lib.sh clk   (-> svt-av1-mirror_amd/libsvtme_clk.so)
+Build (container):  bash scripts/build_diag_lib.sh clk -DSVTME_CLOCKBINS
 Run (GPU box):      python3 scripts/clock_probe.py [steps] [idle_ms]
 
 Replays bench.py's timed loop in a fresh process (the workload's pictures

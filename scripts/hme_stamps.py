@@ -1,7 +1,6 @@
 """Per-phase timing of k_hme from a diagnostic build (-DSVTME_STAMPS).
 
-Build (container):  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DSVTME_STAMPS \
-    -o svt-av1-mirror_amd/libsvtme_stamp.so svt-av1-mirror_amd/csrc/*.hip svt-av1-mirror_amd/csrc/svtme_host.cpp
+Build (container):  bash scripts/build_diag_lib.sh stamp -DSVTME_STAMPS
 Run (GPU box):      python3 scripts/hme_stamps.py [workload] [pictures]
 
 Thread 0 of every k_hme workgroup stamps the shader clock at 7 points: start,
