@@ -1464,8 +1464,9 @@ struct StC {
     int32_t nreq, nfp, k32, fp_items;
     FpRef fp[8];
     unsigned long long keys[8][SVTME_PU_COUNT];
-    uint32_t best_sad[8][SVTME_PU_COUNT];
-    uint32_t best_mv[8][SVTME_PU_COUNT];
+    // per slot, the image of its svtme_ref_record: best_sad [0, 85), best_mv [85, 170),
+    // the tail [170, 176) (filled as the record is written): one 16-byte copy per lane
+    __attribute__((aligned(16))) uint32_t rec[8][176];
     uint32_t me_distortion[SVTME_PU_COUNT];
     uint8_t cand0[SVTME_PU_COUNT + 3];
     uint32_t gm_cnt[2][4][2][2];
@@ -1632,12 +1633,12 @@ __device__ void fullpel_run(StC &st, const DevPlane &C, uint32_t ox, uint32_t oy
         const FpRef &F             = st.fp[f];
         const unsigned long long k = st.keys[F.slot][pu];
         const uint32_t sad         = (uint32_t)(k >> 32);
-        if (k != ~0ull && sad < st.best_sad[F.slot][pu]) {
+        if (k != ~0ull && sad < st.rec[F.slot][pu]) {
             const int p      = (int)(uint32_t)k - F.order_base;
             const int16_t my = (int16_t)(F.yo + p / F.w);
             const int16_t mx = (int16_t)(F.xo + p % F.w);
-            st.best_sad[F.slot][pu] = sad;
-            st.best_mv[F.slot][pu]  = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
+            st.rec[F.slot][pu] = sad;
+            st.rec[F.slot][SVTME_PU_COUNT + pu]  = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
         }
     }
     __syncthreads();
@@ -1673,11 +1674,11 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
         const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
         if (mode == 0) { // construct_me_candidate_array_single_ref
             const int pu         = c_z_to_raster[n];
-            st.me_distortion[pu] = st.best_sad[0][n];
+            st.me_distortion[pu] = st.rec[0][n];
             st.cand0[pu]         = 0;
             if (st.do_ref[0] && use) {
                 o->me_candidate_array[pu][0] = mk_cand(0, 0, 0, 0, 0);
-                o->me_mv_array[pu][0]        = st.best_mv[0][n];
+                o->me_mv_array[pu][0]        = st.rec[0][SVTME_PU_COUNT + n];
             }
         } else if (mode == 1) { // construct_me_candidate_array_mrp_off
             const int pu        = c_z_to_raster[n];
@@ -1688,7 +1689,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
             uint8_t off  = 0;
             uint32_t blk = (org0 ? 1u : 0u) | (org1 ? 2u : 0u); // bit li
-            const uint32_t s0 = st.best_sad[0][n], s1 = st.best_sad[4][n];
+            const uint32_t s0 = st.rec[0][n], s1 = st.rec[4][n];
             const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
             st.me_distortion[pu] = best;
             int min_list         = -1;
@@ -1699,7 +1700,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                 if (!((blk >> li) & 1u))
                     continue;
                 if (prune_th > 0) {
-                    const uint32_t dd = (st.best_sad[li * 4][n] - best) * 100;
+                    const uint32_t dd = (st.rec[li * 4][n] - best) * 100;
                     if (dd > best * prune_th) {
                         blk &= ~(1u << li);
                         continue;
@@ -1707,7 +1708,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                 }
                 if (min_list != -1 && min_list != li) {
                     if (use)
-                        o->me_mv_array[pu][li ? job.max_l0 : 0] = st.best_mv[li * 4][n];
+                        o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
                     continue;
                 }
                 if (use) {
@@ -1715,7 +1716,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                     o->me_candidate_array[pu][off] = cb;
                     if (off == 0)
                         c0 = cb;
-                    o->me_mv_array[pu][li ? job.max_l0 : 0] = st.best_mv[li * 4][n];
+                    o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
                 }
                 off++;
             }
@@ -1738,7 +1739,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                     if (!st.do_ref[li * 4 + r])
                         continue;
                     blk |= 1u << (li * 4 + r);
-                    best = min_u32(best, st.best_sad[li * 4 + r][n]);
+                    best = min_u32(best, st.rec[li * 4 + r][n]);
                 }
             st.me_distortion[pu] = best;
             uint8_t c0 = 0;
@@ -1747,7 +1748,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                     if (!((blk >> (li * 4 + r)) & 1u))
                         continue;
                     if (prune_th > 0) {
-                        const uint32_t dd = (st.best_sad[li * 4 + r][n] - best) * 100;
+                        const uint32_t dd = (st.rec[li * 4 + r][n] - best) * 100;
                         if (dd > best * prune_th) {
                             blk &= ~(1u << (li * 4 + r));
                             continue;
@@ -1758,7 +1759,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                         o->me_candidate_array[pu][off] = cb;
                         if (off == 0)
                             c0 = cb;
-                        o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.best_mv[li * 4 + r][n];
+                        o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.rec[li * 4 + r][SVTME_PU_COUNT + n];
                     }
                     off++;
                 }
@@ -1854,7 +1855,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                 const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - st.refpic[li * 4 + ri]));
                 active_th = job.gm_use_distance_based_active_th ? max(dist * 16, 32) : 32;
             }
-            const uint32_t mv = st.best_mv[li * 4 + ri][n];
+            const uint32_t mv = st.rec[li * 4 + ri][SVTME_PU_COUNT + n];
             const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4;
             uint32_t(*cnt)[4][2][2] = st.gm_cnt;
             if (mx < -active_th)
@@ -1898,7 +1899,7 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
         for (int k = 0; k < 8; k++) {
             if (!(slot_valid(vmask, k) && st.do_ref[k]))
                 continue; // wave-uniform
-            const uint32_t t = wave_sum_u32(st.best_sad[k][21 + lane]);
+            const uint32_t t = wave_sum_u32(st.rec[k][21 + lane]);
             if (lane == k)
                 sum8 = t;
         }
@@ -1919,33 +1920,33 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
     }
     __syncthreads();
 
-    // ---- records (sb_count x R, slots in list-0-then-list-1 order)
+    // ---- records (sb_count x R, slots in list-0-then-list-1 order): the LDS record
+    // images, 44 16-byte pieces each (704 bytes), the tail words and the SADs of an
+    // unsearched slot patched on the way
     {
+        static_assert(sizeof(svtme_ref_record) == 176 * 4, "svtme_ref_record: 176 dwords");
         svtme_ref_record *out = dj.out_records + (size_t)sb_local * dj.R;
         const int R = (int)dj.R;
-        for (int k = 0; k < R; k++) { // 704 bytes = 176 dwords per record
+        for (int i = tid; i < R * 44; i += 256) {
+            const int k = i / 44, q = i - 44 * k;
             const int s = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
-            const int w = tid;
-            if (w >= 176)
-                continue;
-            uint32_t v;
-            if (w < 85)
-                v = st.searched[s] ? st.best_sad[s][w] : U32MAX;
-            else if (w < 170)
-                v = st.best_mv[s][w - 85];
-            else if (w == 170)
-                v = (uint32_t)st.hme_sad[s];
-            else if (w == 171)
-                v = (uint32_t)(st.hme_sad[s] >> 32);
-            else if (w == 172)
-                v = (uint32_t)(uint16_t)st.sc_x[s] | ((uint32_t)(uint16_t)st.sc_y[s] << 16);
-            else if (w == 173)
-                v = st.zz[s];
-            else if (w == 174)
-                v = (uint32_t)st.searched[s] | ((uint32_t)st.do_ref[s] << 8) | ((uint32_t)st.tf_exit << 16);
-            else
-                v = 0;
-            ((uint32_t *)(out + k))[w] = v;
+            uint4 v     = ((const uint4 *)st.rec[s])[q];
+            if (q < 22 && !st.searched[s]) { // words 0 .. 87: the SADs (< 85) of an unsearched slot
+                if (4 * q + 0 < 85) v.x = U32MAX;
+                if (4 * q + 1 < 85) v.y = U32MAX;
+                if (4 * q + 2 < 85) v.z = U32MAX;
+                if (4 * q + 3 < 85) v.w = U32MAX;
+            }
+            if (q == 42) { // words 168, 169 (MVs), 170, 171: hme_sad
+                v.z = (uint32_t)st.hme_sad[s];
+                v.w = (uint32_t)(st.hme_sad[s] >> 32);
+            } else if (q == 43) { // 172: search centre, 173: zz SAD, 174: flags, 175: 0
+                v.x = (uint32_t)(uint16_t)st.sc_x[s] | ((uint32_t)(uint16_t)st.sc_y[s] << 16);
+                v.y = st.zz[s];
+                v.z = (uint32_t)st.searched[s] | ((uint32_t)st.do_ref[s] << 8) | ((uint32_t)st.tf_exit << 16);
+                v.w = 0;
+            }
+            ((uint4 *)(out + k))[q] = v;
         }
     }
     if (dj.out_sb) {
@@ -1992,7 +1993,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         if (lane == 0)
             st.tf_exit = tf_exit;
     }
-    for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) (&st.best_mv[0][0])[e] = 0;
+    for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) st.rec[e / SVTME_PU_COUNT][SVTME_PU_COUNT + e % SVTME_PU_COUNT] = 0;
     __syncthreads();
 
     // ---- integer_search_b64 (motion_estimation.c:1249-1516); lane s of wave 0 owns slot s.
@@ -2089,7 +2090,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                         if ((accurate && (st.is_best_hme[s] < (24 * 24))) ||
                             (job.is_ref && st.hme_sad[s] < (24 * 24)))
                             h = i16(h / 2);
-                        if ((l || r) && st.best_sad[0][0] < 5000 && h == st.is_hb[s] && w == st.is_wb[s]) {
+                        if ((l || r) && st.rec[0][0] < 5000 && h == st.is_hb[s] && w == st.is_wb[s]) {
                             h = i16(h >> 1);
                             w = i16(w >> 1);
                         }
@@ -2111,7 +2112,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         for (int e = tid; e < 8 * SVTME_PU_COUNT; e += 256) {
             const int s = e / SVTME_PU_COUNT;
             if (st.in_round[s])
-                (&st.best_sad[0][0])[e] = SVTME_MAX_SAD_VALUE;
+                st.rec[e / SVTME_PU_COUNT][e % SVTME_PU_COUNT] = SVTME_MAX_SAD_VALUE;
         }
         if (st.nfp) {
             fullpel<SUB_ME>(st, C, ox, oy); // centre probe (motion_estimation.c:1414-1417)
@@ -2119,10 +2120,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             if (w0 && lane < 8 && st.in_round[lane] && c.me_8x8_var_enabled && (st.is_w[lane] * st.is_h[lane] > 24)) {
                 const int s = lane;
                 int16_t w = st.is_w[s], h = st.is_h[s];
-                const uint32_t mean = st.best_sad[s][0] / 64;
+                const uint32_t mean = st.rec[s][0] / 64;
                 uint32_t sum_sq     = 0;
                 for (int i = 0; i < 64; i++) {
-                    const int32_t diff = (int32_t)st.best_sad[s][21 + i] - (int32_t)mean;
+                    const int32_t diff = (int32_t)st.rec[s][21 + i] - (int32_t)mean;
                     sum_sq += (uint32_t)(diff * diff);
                 }
                 const uint32_t var = sum_sq / 64;
@@ -3663,15 +3664,13 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
     const svtme_job &job = dj.job;
     const int tid        = threadIdx.x;
     const int R          = (int)dj.R;
-    if (tid == 0) {
-#pragma unroll
-        for (int s = 0; s < 8; s++) {
-            st.pl[s][0]  = dj.ref[s >> 2][s & 3].lv[0];
-            st.dist[s]   = ref_dist_const(job, s >> 2, s & 3);
-            st.refpic[s] = job.ref_picture_number[s >> 2][s & 3];
-        }
-        st.tf_exit = 0;
+    if (tid < 8) { // slot tid
+        st.pl[tid][0]  = dj.ref[tid >> 2][tid & 3].lv[0];
+        st.dist[tid]   = ref_dist_const(job, tid >> 2, tid & 3);
+        st.refpic[tid] = job.ref_picture_number[tid >> 2][tid & 3];
     }
+    if (tid == 0)
+        st.tf_exit = 0;
     if (tid < 8) {
         st.searched[tid] = 0;
         st.do_ref[tid]   = 0;
@@ -3718,8 +3717,8 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
             }
             mv = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
         }
-        st.best_sad[s][pu] = sad;
-        st.best_mv[s][pu]  = mv;
+        st.rec[s][pu] = sad;
+        st.rec[s][SVTME_PU_COUNT + pu]  = mv;
     }
     __syncthreads();
     stage_c_tail(st, dj, sb_local, G.bw, G.bh, vmask);
@@ -3921,9 +3920,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     // full-pel and decode phases) and its LDS copy (per-lane reads of the HME phases)
     const DevJob &gj = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
     {
-        const uint32_t *js = (const uint32_t *)&gj;
-        uint32_t *jd       = (uint32_t *)&sh.dj;
-        for (int i = tid; i < (int)(sizeof(DevJob) / 4); i += 256) jd[i] = js[i];
+        // one 16-byte load per thread (a loop of dword loads waited for each round trip)
+        static_assert(sizeof(DevJob) % 16 == 0 && sizeof(DevJob) / 16 <= 256, "DevJob: one uint4 per thread");
+        if (tid < (int)(sizeof(DevJob) / 16))
+            ((uint4 *)&sh.dj)[tid] = ((const uint4 *)&gj)[tid];
         if (tid < 8)
             sh.u.a.zzacc[tid] = 0;
     }
