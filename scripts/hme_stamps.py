@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
 import svtme as S  # noqa: E402
 import workloads as W  # noqa: E402
 
-PHASES = ["A0 zz", "A1 table", "A1 tiles", "D + L1 table", "L1 tiles", "full-pel", "decode+tail"]
+PHASES = ["A0 (job, zz, A1 table)", "zz decisions", "A1 tiles", "D + L1 table", "L1 (+L2) tiles", "centre + full-pel", "E (prune, records)"]
 
 
 def main():
