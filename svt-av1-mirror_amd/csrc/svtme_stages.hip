@@ -4342,26 +4342,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     __syncthreads(); // phase A..B state is dead from here (StC overlays it)
     // ---- C: set_final_seach_centre_sb / hme_prune_ref_and_adjust_sr once (wave 0), then
     // integer_search_b64 of every record, one wavefront each (k_stage_c1, one band)
-    StC &st = sh.u.st;
     if (wid == 0) {
         HME_PRIO_HI();
         const SlotCentre scv = final_centre(job, &sh.bs, vmask); // lane = slot
-        if (lane < 8) {
+        if (lane < 8)
             sh.cen[lane] = scv;
-            // phase E's per-slot state, for slots no record covers (a record's wave
-            // overwrites its slot after its search)
-            st.pl[lane][0]  = dj.ref[lane >> 2][lane & 3].lv[0];
-            st.dist[lane]   = ref_dist_const(job, lane >> 2, lane & 3);
-            st.refpic[lane] = job.ref_picture_number[lane >> 2][lane & 3];
-            st.searched[lane] = 0;
-            st.do_ref[lane]   = 0;
-            st.hme_sad[lane]  = U32MAX;
-            st.zz[lane]       = U32MAX;
-            st.sc_x[lane] = st.sc_y[lane] = 0;
-        }
-        const bool tfx = job.me_type == SVTME_ME_MCTF && rl64(scv.hme_sad, 0) < job.tf_me_exit_th; // :3109-3113
         if (lane == 0)
-            sh.tf_exit = st.tf_exit = tfx;
+            sh.tf_exit = job.me_type == SVTME_ME_MCTF && scv.hme_sad < job.tf_me_exit_th; // :3109-3113
     }
     __syncthreads();
     HME_PRIO_LO();
@@ -4388,52 +4375,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         const SlotCentre &v = sh.cen[s];
         fp_slot<SUB_ME, K32, 2, false, HME_WHOLE>(gj, G, s, src, by, bx, rl64(v.hme_sad, 0), (uint32_t)UNI(v.zz), (uint32_t)UNI(v.reduce_div),
                                 (int16_t)UNI(v.sc_x), (int16_t)UNI(v.sc_y), (uint8_t)UNI(v.do_ref),
-                                (uint8_t)UNI(sh.tf_exit), 0, 1u, &st.keys[k][0], &sh.cin[k]);
-    }
-    // ---- E, each record's part, by the wave that searched it (no barrier: its own LDS
-    // writes): the slot state and the 85 keys decoded into the slot's record image
-    // (stage_e_body's decode); a loop of its own, so the search's registers are free
-    wave_lds_fence();
-    for (int k = wid; k < (int)dj.R; k += 4) {
-        const int s       = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
-        const CSlot cv    = sh.cin[k];
-        const uint32_t wm = cv.searched ? magic_u32((uint32_t)max(1, (int)cv.w)) : 0u;
-        if (lane == 0) {
-            sh.csl[s]      = cv;
-            st.wm[s]       = wm;
-            st.hme_sad[s]  = cv.hme_sad;
-            st.zz[s]       = cv.zz;
-            st.sc_x[s]     = cv.sc_x;
-            st.sc_y[s]     = cv.sc_y;
-            st.searched[s] = cv.searched;
-            st.do_ref[s]   = cv.do_ref;
-        }
-        for (int pu = lane; pu < SVTME_PU_COUNT; pu += 64) {
-            uint32_t sad = U32MAX, mv = 0;
-            if (cv.searched) { // wave-uniform
-                const unsigned long long key = st.keys[k][pu];
-                const uint32_t o             = (uint32_t)key;
-                sad                          = (uint32_t)(key >> 32);
-                int16_t mx, my;
-                if (cv.probe && o == 0) {
-                    mx = cv.xc;
-                    my = cv.yc;
-                } else { // p / w by multiply-high (p * w < 2^32)
-                    const int p = (int)o - (int)cv.probe;
-                    const int q = mdiv(p, wm);
-                    my          = i16(cv.yo + q);
-                    mx          = i16(cv.xo + (p - q * cv.w));
-                }
-                mv = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
-            }
-            st.rec[s][pu]                  = sad;
-            st.rec[s][SVTME_PU_COUNT + pu] = mv;
-        }
+                                (uint8_t)UNI(sh.tf_exit), 0, 1u, &sh.u.st.keys[k][0], &sh.cin[k]);
     }
     __syncthreads();
     HME_STAMP(6);
-    // ---- E: me_prune_ref, records, candidates / distortions / GM detection
-    stage_c_tail(st, dj, sb_local, G.bw, G.bh, vmask); // (the LDS copy of the job)
+    // ---- E: decode, me_prune_ref, records, candidates / distortions / GM detection
+    stage_e_body(sh.u.st, sh.csl, gj, sb_local, G, vmask, sh.cin, &sh.u.st.keys[0][0], false);
     HME_STAMP(7);
 }
 
