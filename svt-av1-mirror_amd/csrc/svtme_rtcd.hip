@@ -137,47 +137,58 @@ __device__ uint32_t sad8(const uint8_t *src, uint32_t ss, const uint8_t *ref, ui
     return s;
 }
 
+// sum over the 2^k lanes of an aligned group (butterfly: every lane of the group holds it)
+template <int K>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v) {
+#pragma unroll
+    for (int m = 1; m < (1 << K); m <<= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
 // svt_ext_sad_calculation_8x8_16x16 (motion_estimation.c:98-164): io[0..3] best 8x8 sad,
-// io[4] best 16x16 sad, io[5..8] mv8x8, io[9] mv16x16, io[10] sad16x16, io[11..14] sad8x8
+// io[4] best 16x16 sad, io[5..8] mv8x8, io[9] mv16x16, io[10] sad16x16, io[11..14] sad8x8.
+// One wave: lane = block b (lane >> 4, raster in the 16x16) x row (lane >> 1 & 7) x
+// 4-pixel half (lane & 1); the 16 lanes of a block sum its SAD.
 __global__ void k_ext_8x8_16x16(const uint8_t *src, uint32_t ss, const uint8_t *ref, uint32_t rs, uint32_t mv,
                                 int sub, uint32_t *io) {
-    if (threadIdx.x != 0)
-        return;
-    uint32_t s8[4];
-    for (int b = 0; b < 4; b++)
-        s8[b] = sad8(src + (b >> 1) * 8 * ss + (b & 1) * 8, ss, ref + (size_t)(b >> 1) * 8 * rs + (b & 1) * 8, rs,
-                     sub != 0);
-    for (int b = 0; b < 4; b++) {
-        io[11 + b] = s8[b];
-        if (s8[b] < io[b]) {
-            io[b]     = s8[b];
+    const int lane = threadIdx.x, b = lane >> 4, r = (lane >> 1) & 7, h = lane & 1;
+    const int y = (b >> 1) * 8 + r, x = (b & 1) * 8 + h * 4;
+    uint32_t a = 0;
+    if (!sub || (r & 1) == 0)
+        for (int j = 0; j < 4; j++) a += absd(src[y * ss + x + j], ref[(size_t)y * rs + x + j]);
+    const uint32_t s8  = group_sum<4>(a) << (sub ? 1 : 0);
+    const uint32_t s16 = s8 + __shfl_xor(s8, 16, 64) + __shfl_xor(s8, 32, 64) + __shfl_xor(s8, 48, 64);
+    if ((lane & 15) == 0) {
+        io[11 + b] = s8;
+        if (s8 < io[b]) {
+            io[b]     = s8;
             io[5 + b] = mv;
         }
     }
-    const uint32_t s16 = s8[0] + s8[1] + s8[2] + s8[3];
-    if (s16 < io[4]) {
-        io[4] = s16;
-        io[9] = mv;
+    if (lane == 0) {
+        if (s16 < io[4]) {
+            io[4] = s16;
+            io[9] = mv;
+        }
+        io[10] = s16;
     }
-    io[10] = s16;
 }
 
 // svt_ext_sad_calculation_32x32_64x64 (motion_estimation.c:171-205):
-// io[0..15] sad16x16, [16..19] best32, [20] best64, [21..24] mv32, [25] mv64, [26..29] sad32
+// io[0..15] sad16x16, [16..19] best32, [20] best64, [21..24] mv32, [25] mv64, [26..29] sad32.
+// Lane q < 4: quadrant q's sum of its four 16x16 SADs; the 64x64 sum over the 4 lanes.
 __global__ void k_ext_32x32_64x64(uint32_t mv, uint32_t *io) {
-    if (threadIdx.x != 0)
-        return;
-    uint32_t s64 = 0;
-    for (int q = 0; q < 4; q++) {
-        const uint32_t s = io[4 * q] + io[4 * q + 1] + io[4 * q + 2] + io[4 * q + 3];
-        io[26 + q]       = s;
+    const int q = threadIdx.x & 3;
+    const uint32_t s   = io[4 * q] + io[4 * q + 1] + io[4 * q + 2] + io[4 * q + 3];
+    const uint32_t s64 = group_sum<2>(s);
+    if (threadIdx.x < 4) {
+        io[26 + q] = s;
         if (s < io[16 + q]) {
             io[16 + q] = s;
             io[21 + q] = mv;
         }
-        s64 += s;
     }
-    if (s64 < io[20]) {
+    if (threadIdx.x == 0 && s64 < io[20]) {
         io[20] = s64;
         io[25] = mv;
     }
@@ -215,29 +226,39 @@ __global__ void k_ext_all_8x8_16x16(const uint8_t *src, uint32_t ss, const uint8
 }
 
 // svt_ext_eight_sad_calculation_32x32_64x64 (motion_estimation.c:369-425):
-// io [0..127] sad16x16[16][8], [128..131] best32, [132] best64, [133..136] mv32, [137] mv64, [138..169] sad32[4][8]
+// io [0..127] sad16x16[16][8], [128..131] best32, [132] best64, [133..136] mv32, [137] mv64, [138..169] sad32[4][8].
+// Lane = quadrant q (lane >> 3) x position si (lane & 7), 32 lanes. The reference
+// updates each best in position order with a strict <, so its result is the
+// lowest position of the minimum, taken only if below the incoming best: a
+// (sad << 3 | si) minimum over the 8 lanes of a quadrant.
 __global__ void k_ext_eight_32x32_64x64(uint32_t mv, uint32_t *io) {
-    if (threadIdx.x != 0)
-        return;
-    for (int si = 0; si < 8; si++) {
-        const int16_t xm   = (int16_t)((int16_t)(mv & 0xFFFF) + si);
-        const int16_t ym   = (int16_t)(mv >> 16);
-        const uint32_t nmv = ((uint32_t)(uint16_t)ym << 16) | (uint16_t)xm;
-        uint32_t s64       = 0;
-        for (int q = 0; q < 4; q++) {
-            const uint32_t s = io[(4 * q) * 8 + si] + io[(4 * q + 1) * 8 + si] + io[(4 * q + 2) * 8 + si] +
-                io[(4 * q + 3) * 8 + si];
-            io[138 + q * 8 + si] = s;
-            if (s < io[128 + q]) {
-                io[128 + q] = s;
-                io[133 + q] = nmv;
-            }
-            s64 += s;
+    const int lane = threadIdx.x & 31, q = lane >> 3, si = lane & 7;
+    const uint32_t s = io[(4 * q) * 8 + si] + io[(4 * q + 1) * 8 + si] + io[(4 * q + 2) * 8 + si] +
+        io[(4 * q + 3) * 8 + si];
+    const uint32_t s64 = s + __shfl_xor(s, 8, 64) + __shfl_xor(s, 16, 64) + __shfl_xor(s, 24, 64);
+    auto min8 = [](unsigned long long k) { // over the 8 lanes of a group
+        for (int m = 1; m < 8; m <<= 1) {
+            const unsigned long long o = __shfl_xor(k, m, 64);
+            k = o < k ? o : k;
         }
-        if (s64 < io[132]) {
-            io[132] = s64;
-            io[137] = nmv;
+        return k;
+    };
+    const unsigned long long k32 = min8(((unsigned long long)s << 3) | (uint32_t)si);
+    const unsigned long long k64 = min8(((unsigned long long)s64 << 3) | (uint32_t)si);
+    auto mv_at = [&](uint32_t p) {
+        const int16_t xm = (int16_t)((int16_t)(mv & 0xFFFF) + (int)p), ym = (int16_t)(mv >> 16);
+        return ((uint32_t)(uint16_t)ym << 16) | (uint16_t)xm;
+    };
+    if (threadIdx.x < 32) {
+        io[138 + q * 8 + si] = s;
+        if (si == 0 && (uint32_t)(k32 >> 3) < io[128 + q]) {
+            io[128 + q] = (uint32_t)(k32 >> 3);
+            io[133 + q] = mv_at((uint32_t)k32 & 7);
         }
+    }
+    if (threadIdx.x == 0 && (uint32_t)(k64 >> 3) < io[132]) {
+        io[132] = (uint32_t)(k64 >> 3);
+        io[137] = mv_at((uint32_t)k64 & 7);
     }
 }
 

@@ -56,3 +56,38 @@ def test_hip_sad_loop_random_sweep(svtme):
         b = R.run_sad_loop(ora, "svtora_", case, 1000 + i)
         for k in a:
             assert np.array_equal(a[k], b[k]), (case, k, a, b)
+
+
+@pytest.mark.gpu
+def test_hip_ext_kernels_random_sweep(svtme):
+    """The lane-parallel ext kernels against the oracle on extra random cases,
+    with tie-heavy 16x16 SADs (0..3) so that the lowest-position rule of the
+    reference's strict-< updates decides many of them (no golden needed)."""
+    lib, ora = svtme.load_product(), svtme.load_oracle()
+    lib.svtme_rtcd_failed()
+    rng = np.random.default_rng(91)
+    for i in range(16):
+        case = (bool(i & 1), int(rng.integers(16, 200)), int(rng.integers(16, 200)), int(rng.integers(0, 4)),
+                900 + i)
+        a, b = R.run_ext8(lib, "svt_", case), R.run_ext8(ora, "svtora_", case)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), ("ext8", case, k)
+        a, b = R.run_ext32(lib, "svt_", 950 + i), R.run_ext32(ora, "svtora_", 950 + i)
+        for k in a:
+            assert np.array_equal(a[k], b[k]), ("ext32", i, k)
+    for i in range(24):
+        out = []
+        for lb, p in ((lib, "svt_"), (ora, "svtora_")):
+            r = np.random.default_rng(1000 + i)
+            s16 = r.integers(0, 4, (16, 8)).astype(np.uint32)
+            b32 = r.integers(0, 18, 4).astype(np.uint32)
+            b64 = r.integers(0, 70, 1).astype(np.uint32)
+            m32, m64 = np.full(4, 7, np.uint32), np.full(1, 7, np.uint32)
+            s32 = np.zeros((4, 8), np.uint32)
+            f = R._fn(lb, p, "ext_eight_sad_calculation_32x32_64x64")
+            f.restype = None
+            f(R._u32(s16), R._u32(b32), R._u32(b64), R._u32(m32), R._u32(m64), C.c_uint32(R._mv(r)), R._u32(s32))
+            out.append((b32, b64, m32, m64, s32))
+        for x, y in zip(*out):
+            assert np.array_equal(x, y), ("ext_eight32", i)
+    assert lib.svtme_rtcd_failed() == 0, lib.svtme_last_error()
