@@ -91,6 +91,8 @@
 #include "sequence_control_set.h"
 #ifdef SVTME_GLUE_WRAP
 #include "enc_handle.h"
+#include "enc_mode_config.h"
+#include "pd_results.h"
 #endif
 
 #include "svtme.h"
@@ -140,17 +142,18 @@ EbErrorType svt_aom_motion_estimation_b64(PictureParentControlSet *, uint32_t, u
 typedef struct GlueEnc {
     const void *enc_ctx; /* NULL: a free slot */
     const void *pa_res;  /* its picture-analysis results resource, or NULL */
+    const void *pd_res;  /* its picture-decision results resource (the ME tasks), or NULL */
 } GlueEnc;
 static GlueEnc g_enc[GLUE_MAX_ENC];
 static pthread_mutex_t g_enc_mu = PTHREAD_MUTEX_INITIALIZER;
 static unsigned long long g_n_encoders, g_n_released; /* slots taken; pictures released at teardowns (g_enc_mu) */
 
 /* the slot of an encoder, taken on first sight; -1 when every slot is taken */
-static int enc_slot(const void *enc_ctx, const void *pa_res) {
+static int enc_slot(const void *enc_ctx, const void *pa_res, const void *pd_res) {
     if (!enc_ctx)
         return -1;
     for (int i = 0; i < GLUE_MAX_ENC; i++)
-        if (__atomic_load_n(&g_enc[i].enc_ctx, __ATOMIC_ACQUIRE) == enc_ctx && !pa_res)
+        if (__atomic_load_n(&g_enc[i].enc_ctx, __ATOMIC_ACQUIRE) == enc_ctx && !pa_res && !pd_res)
             return i;
     pthread_mutex_lock(&g_enc_mu);
     int k = -1;
@@ -165,12 +168,14 @@ static int enc_slot(const void *enc_ctx, const void *pa_res) {
         }
     if (k >= 0 && pa_res)
         __atomic_store_n(&g_enc[k].pa_res, pa_res, __ATOMIC_RELEASE);
+    if (k >= 0 && pd_res)
+        __atomic_store_n(&g_enc[k].pd_res, pd_res, __ATOMIC_RELEASE);
     pthread_mutex_unlock(&g_enc_mu);
     return k;
 }
 
 static int pcs_slot(const PictureParentControlSet *pcs) {
-    return enc_slot(pcs->scs ? (const void *)pcs->scs->enc_ctx : NULL, NULL);
+    return enc_slot(pcs->scs ? (const void *)pcs->scs->enc_ctx : NULL, NULL, NULL);
 }
 
 /* the library's number of picture pn of the encoder in `slot` */
@@ -600,6 +605,8 @@ typedef struct GlueJob {
     uint32_t served;
     uint32_t users;    /* threads between finding the job and the end of their scatter */
     int state;         /* 0 running, 1 done, -1 failed (its SBs run on the encoder's function) */
+    uint64_t ticket;   /* a prefetched job's ticket until a thread takes it to wait (0: none) */
+    int prefetched;    /* submitted when picture decision posted the picture's ME tasks */
     int stale;         /* a picture it reads was re-decimated after it ran: later calls start a new job */
     struct GlueJob *next;
 } GlueJob;
@@ -643,7 +650,7 @@ static struct {
     pthread_mutex_t gpu; /* one thread uploads / submits at a time (not held while waiting) */
     pthread_mutex_t reg; /* the page-locked encoder buffers (regs) */
     svtme_ctx *ctx;
-    int strict, verify, eager, pin, tf_batch, max_resident;
+    int strict, verify, eager, pin, tf_batch, prefetch, max_resident;
     const char *stats_path, *trace_path;
     GlueTrace *trace;
     uint32_t n_trace, cap_trace;
@@ -663,7 +670,7 @@ static struct {
     struct {
         unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
         unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job, registrations;
-        unsigned long long tf_batched, unused_jobs, launches;
+        unsigned long long tf_batched, unused_jobs, launches, prefetched, prefetch_hits, prefetch_ready;
         double upload_s, submit_s, wait_s, job_s, busy_s, eager_s, prefill_s, register_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER,
@@ -720,13 +727,14 @@ static void glue_stats_at_exit(void) {
             "\"job_latency_ms\": %.4f, \"busy_ms\": %.3f, \"served_sb_per_s\": %.1f, \"eager_uploads\": %llu, "
             "\"eager_upload_ms\": %.3f, \"served_sb_per_s_with_uploads\": %.1f, \"prefill_ms\": %.3f, "
             "\"registrations\": %llu, \"register_ms\": %.3f, \"encoders\": %llu, \"released_at_teardown\": %llu, "
-            "\"tf_batched\": %llu, \"unused_jobs\": %llu, \"launches\": %llu}\n",
+            "\"tf_batched\": %llu, \"unused_jobs\": %llu, \"launches\": %llu, \"prefetched\": %llu, "
+            "\"prefetch_hits\": %llu, \"prefetch_ready\": %llu}\n",
             G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
             G.n.evictions, G.n.verified, G.n.verified_job, G.n.stale, G.n.unpinned, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
             G.n.max_inflight, 1e3 * G.n.upload_s, 1e3 * G.n.submit_s, 1e3 * G.n.wait_s,
             jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate, G.n.eager_uploads, 1e3 * G.n.eager_s,
             rate_up, 1e3 * G.n.prefill_s, G.n.registrations, 1e3 * G.n.register_s, g_n_encoders, g_n_released,
-            G.n.tf_batched, G.n.unused_jobs, G.n.launches);
+            G.n.tf_batched, G.n.unused_jobs, G.n.launches, G.n.prefetched, G.n.prefetch_hits, G.n.prefetch_ready);
     fclose(f);
 }
 
@@ -738,6 +746,7 @@ static void glue_init(void) {
     G.eager        = !(e = getenv("SVTME_GLUE_EAGER")) || atoi(e);
     G.pin          = !(e = getenv("SVTME_GLUE_PIN")) || atoi(e);
     G.tf_batch     = !(e = getenv("SVTME_GLUE_TF_BATCH")) || atoi(e);
+    G.prefetch     = !(e = getenv("SVTME_GLUE_PREFETCH")) || atoi(e);
     G.max_resident = (e = getenv("SVTME_GLUE_RESIDENT")) ? atoi(e) : 128;
     if (G.max_resident < 9)
         G.max_resident = 9; /* a job names at most 1 + 8 pictures */
@@ -933,6 +942,10 @@ static const uint8_t *span_of(const EbPictureBufferDesc *full, uint32_t w, uint3
  * nothing of it. slot < 0: every encoder. */
 static void job_free(GlueJob *j);
 static void job_unlink(GlueJob *j);
+static void settle_prefetched(int (*pick)(const GlueJob *, int), int arg);
+static int pick_slot(const GlueJob *j, int slot) {
+    return j->users == 0 && (slot < 0 || (int)(j->job.picture_number >> GLUE_NS_SHIFT) == slot);
+}
 static void release_slot(int slot) {
     if (!G.ctx)
         return;
@@ -961,6 +974,7 @@ static void release_slot(int slot) {
     pthread_mutex_unlock(&g_enc_mu);
     pthread_mutex_unlock(&G.gpu);
     pthread_mutex_lock(&G.mu);
+    settle_prefetched(pick_slot, slot); /* (their work has run: svtme_sync above) */
     for (GlueJob *j = G.jobs, *nx; j; j = nx) {
         nx = j->next;
         if ((slot < 0 || (int)(j->job.picture_number >> GLUE_NS_SHIFT) == slot) && j->users == 0 && j->state != 0) {
@@ -976,6 +990,7 @@ void svtme_glue_release(void) {
     pthread_mutex_lock(&g_enc_mu);
     for (int i = 0; i < GLUE_MAX_ENC; i++) {
         __atomic_store_n(&g_enc[i].pa_res, NULL, __ATOMIC_RELEASE);
+        __atomic_store_n(&g_enc[i].pd_res, NULL, __ATOMIC_RELEASE);
         __atomic_store_n(&g_enc[i].enc_ctx, NULL, __ATOMIC_RELEASE);
     }
     pthread_mutex_unlock(&g_enc_mu);
@@ -991,6 +1006,7 @@ void svtme_glue_release_encoder(const void *enc_ctx) {
     release_slot(slot);
     pthread_mutex_lock(&g_enc_mu);
     __atomic_store_n(&g_enc[slot].pa_res, NULL, __ATOMIC_RELEASE);
+    __atomic_store_n(&g_enc[slot].pd_res, NULL, __ATOMIC_RELEASE);
     __atomic_store_n(&g_enc[slot].enc_ctx, NULL, __ATOMIC_RELEASE);
     pthread_mutex_unlock(&g_enc_mu);
 }
@@ -1084,6 +1100,42 @@ static void job_unlink(GlueJob *j) { /* G.mu held */
     *pp = j->next;
 }
 
+/* Prefetched jobs whose ticket no thread has taken, chosen by `pick` (stale
+ * ones, an encoder's at its teardown, or the oldest when too many are out):
+ * take their tickets, wait for them outside G.mu, and mark them done; the stale
+ * ones nobody uses are freed. G.mu held on entry and on return. */
+static void settle_prefetched(int (*pick)(const GlueJob *, int), int arg) {
+    GlueJob *list[SVTME_MAX_TICKETS];
+    uint64_t tk[SVTME_MAX_TICKETS];
+    int n = 0;
+    for (GlueJob *j = G.jobs; j && n < SVTME_MAX_TICKETS; j = j->next)
+        if (j->ticket && pick(j, arg)) {
+            tk[n]     = j->ticket;
+            j->ticket = 0;
+            j->users++; /* held while this thread waits */
+            list[n++] = j;
+        }
+    if (!n)
+        return;
+    pthread_mutex_unlock(&G.mu);
+    int ok[SVTME_MAX_TICKETS];
+    for (int k = 0; k < n; k++) ok[k] = svtme_ticket_wait(G.ctx, tk[k]) == SVTME_OK;
+    pthread_mutex_lock(&G.mu);
+    for (int k = 0; k < n; k++) {
+        GlueJob *j = list[k];
+        j->state   = ok[k] ? 1 : -1;
+        if (--j->users == 0 && (j->stale || j->served >= j->n_sb)) {
+            job_unlink(j);
+            job_free(j);
+        }
+    }
+    pthread_cond_broadcast(&G.cv);
+}
+static int pick_stale(const GlueJob *j, int arg) {
+    (void)arg;
+    return j->stale && j->users == 0;
+}
+
 static EbPaReferenceObject *pa_object(const PictureParentControlSet *pcs) {
     return (EbPaReferenceObject *)pcs->pa_ref_pic_wrapper->object_ptr;
 }
@@ -1148,6 +1200,7 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
             job_free(j);
         }
     }
+    settle_prefetched(pick_stale, 0); /* (prefetched jobs of the old content nobody took) */
     pthread_mutex_unlock(&G.mu);
 }
 
@@ -1282,6 +1335,86 @@ static GlueJob *job_find(const svtme_job *job) { /* G.mu held */
     return j;
 }
 
+/* Picture decision has posted the PA-ME tasks of pcs: build the picture's job
+ * as the ME thread will (me_process.c:118-121 svt_aom_sig_deriv_me, :218-257 the
+ * lists and references, into a scratch MeContext) and submit it now, so that
+ * its results are on their way to host memory before the first segment's first
+ * SB call. That call finds it (the same job, field for field) and waits for its
+ * ticket; a job the encoder ends up not asking for (a field differs, or a
+ * picture it reads is rebuilt first) is settled and dropped (`unused_jobs`),
+ * and the SB calls run their own job as without prefetch. SVTME_GLUE_PREFETCH=0
+ * turns it off. */
+static int pick_oldest(const GlueJob *j, int arg) {
+    (void)arg;
+    return j->users == 0 && j->prefetched;
+}
+void svtme_glue_prefetch_pa(PictureParentControlSet *pcs) {
+    pthread_once(&G.once, glue_init);
+    if (!G.ctx || !G.prefetch || !pcs || pcs_slot(pcs) < 0)
+        return;
+    if (pcs->slice_type == I_SLICE || svt_aom_is_pic_skipped(pcs) || pcs->frame_superres_enabled ||
+        pcs->frame_resize_enabled || !pcs->pa_ref_pic_wrapper)
+        return; /* (no PA-ME job; scaled references run the encoder's own search) */
+    static __thread MeContext *me;
+    if (!me && !(me = (MeContext *)calloc(1, sizeof(MeContext))))
+        return;
+    svt_aom_sig_deriv_me(pcs->scs, pcs, me);
+    me->me_type                     = ME_OPEN_LOOP;
+    me->num_of_list_to_search       = pcs->slice_type == P_SLICE ? 1 : 2;
+    me->num_of_ref_pic_to_search[0] = pcs->ref_list0_count_try;
+    me->num_of_ref_pic_to_search[1] = pcs->slice_type == B_SLICE ? pcs->ref_list1_count_try : 0;
+    me->temporal_layer_index        = pcs->temporal_layer_index;
+    me->is_ref                      = pcs->is_ref;
+    for (int l = 0; l < me->num_of_list_to_search; l++)
+        for (int r = 0; r < me->num_of_ref_pic_to_search[l]; r++) {
+            if (!pcs->ref_pa_pic_ptr_array[l][r])
+                return;
+            const EbPaReferenceObject *o = (const EbPaReferenceObject *)pcs->ref_pa_pic_ptr_array[l][r]->object_ptr;
+            me->me_ds_ref_array[l][r].picture_ptr           = o->input_padded_pic;
+            me->me_ds_ref_array[l][r].quarter_picture_ptr   = o->quarter_downsampled_picture_ptr;
+            me->me_ds_ref_array[l][r].sixteenth_picture_ptr = o->sixteenth_downsampled_picture_ptr;
+            me->me_ds_ref_array[l][r].picture_number        = o->picture_number;
+        }
+    svtme_job job;
+    svtme_job_from_pcs(&job, pcs, me);
+    pthread_mutex_lock(&G.mu);
+    int out = 0;
+    for (GlueJob *x = G.jobs; x; x = x->next) out += x->ticket != 0;
+    if (out >= 8) /* (ME threads that never came: settle the oldest instead of holding tickets) */
+        settle_prefetched(pick_oldest, 0);
+    if (job_find(&job)) {
+        pthread_mutex_unlock(&G.mu);
+        return;
+    }
+    GlueJob *j = job_new(pcs, &job, 0);
+    job_unlink(j); /* listed once it is submitted */
+    const int rc0 = buf_take(j, (size_t)j->n_sb * j->stride, buf_worst(j->n_sb));
+    pthread_mutex_unlock(&G.mu);
+    uint64_t ticket = 0;
+    int rc = rc0;
+    if (!rc) {
+        const EbPaReferenceObject *objs[1] = {NULL};
+        pthread_mutex_lock(&G.gpu);
+        rc = submit_jobs(&j, objs, 1, pcs, me, &ticket);
+        pthread_mutex_unlock(&G.gpu);
+    }
+    pthread_mutex_lock(&G.mu);
+    if (rc) { /* the SB calls start their own job */
+        j->state = -1;
+        job_free(j);
+    } else {
+        j->ticket     = ticket;
+        j->prefetched = 1;
+        G.n.prefetched++;
+        G.n.launches++;
+        j->next = G.jobs;
+        G.jobs  = j;
+        if (job_find(&job) != j) /* (an SB call started the same job meanwhile: this one goes) */
+            j->stale = 1, settle_prefetched(pick_stale, 0);
+    }
+    pthread_mutex_unlock(&G.mu);
+}
+
 EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
                                         uint32_t b64_origin_y, MeContext *me_ctx, EbPictureBufferDesc *input_ptr) {
     pthread_once(&G.once, glue_init);
@@ -1303,7 +1436,36 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
      * first call of a TF window starts every pair's job, in one launch) */
     pthread_mutex_lock(&G.mu);
     GlueJob *j = job_find(&job);
-    if (j) {
+    if (j && j->ticket) { /* prefetched at picture decision, not yet waited for: this thread waits */
+        const uint64_t tk = j->ticket;
+        j->ticket         = 0;
+        j->users++;
+        const double t_start = now_s();
+        if (G.inflight++ == 0)
+            G.busy_t0 = t_start;
+        if (G.inflight > G.n.max_inflight)
+            G.n.max_inflight = G.inflight;
+        const uint32_t inflight = G.inflight;
+        pthread_mutex_unlock(&G.mu);
+        float gms = 0, cms = 0;
+        const int rk       = svtme_ticket_wait_timed(G.ctx, tk, &gms, &cms) == SVTME_OK ? 0 : -1;
+        const double t_done = now_s();
+        pthread_mutex_lock(&G.mu);
+        G.n.wait_s += t_done - t_start;
+        G.n.job_s += t_done - t_start;
+        G.n.prefetch_hits++;
+        G.n.prefetch_ready += t_done - t_start < 10e-6; /* (its results were in host memory already) */
+        if (!rk)
+            G.n.job_sbs += j->n_sb;
+        if (G.trace_path) {
+            const GlueTrace t = {j->job.picture_number, 0, j->n_sb, inflight, 0, t_start, t_start, t_done, 0, gms, cms};
+            trace_add(&t);
+        }
+        j->state = rk ? -1 : 1;
+        if (--G.inflight == 0)
+            G.n.busy_s += t_done - G.busy_t0;
+        pthread_cond_broadcast(&G.cv);
+    } else if (j) {
         j->users++;
         while (j->state == 0) pthread_cond_wait(&G.cv, &G.mu);
     } else {
@@ -1424,7 +1586,8 @@ EbErrorType __wrap_svt_av1_enc_init(EbComponentType *svt_enc_component) {
     const EbErrorType e = __real_svt_av1_enc_init(svt_enc_component);
     if (e == EB_ErrorNone) {
         const EbEncHandle *h = (const EbEncHandle *)svt_enc_component->p_component_private;
-        (void)enc_slot(handle_enc_ctx(svt_enc_component), h->picture_analysis_results_resource_ptr);
+        (void)enc_slot(handle_enc_ctx(svt_enc_component), h->picture_analysis_results_resource_ptr,
+                       h->picture_decision_results_resource_ptr);
     }
     return e;
 }
@@ -1451,7 +1614,14 @@ EbErrorType __real_svt_post_full_object(EbObjectWrapper *object_ptr);
 EbErrorType __wrap_svt_post_full_object(EbObjectWrapper *object_ptr) {
     const void *res = object_ptr ? (const void *)object_ptr->system_resource_ptr : NULL;
     for (int i = 0; res && i < GLUE_MAX_ENC; i++)
-        if (__atomic_load_n(&g_enc[i].pa_res, __ATOMIC_ACQUIRE) == res) {
+        if (__atomic_load_n(&g_enc[i].pd_res, __ATOMIC_ACQUIRE) == res) {
+            /* picture decision posts a picture's PA-ME tasks (pd_process.c:3544-3556):
+             * its job goes to the GPU before the first segment reaches an ME thread */
+            const PictureDecisionResults *r = (const PictureDecisionResults *)object_ptr->object_ptr;
+            if (r->task_type == TASK_PAME && r->segment_index == 0)
+                svtme_glue_prefetch_pa((PictureParentControlSet *)r->pcs_wrapper->object_ptr);
+            break;
+        } else if (__atomic_load_n(&g_enc[i].pa_res, __ATOMIC_ACQUIRE) == res) {
             const PictureAnalysisResults *r = (const PictureAnalysisResults *)object_ptr->object_ptr;
             PictureParentControlSet *pcs    = (PictureParentControlSet *)r->pcs_wrapper->object_ptr;
             if (!pcs->is_overlay && pcs->pa_ref_pic_wrapper) /* overlays skip the analysis (:2122) */
