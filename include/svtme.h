@@ -411,8 +411,10 @@ svtme_status svtme_host_unregister(void *p);
 /* Size the device memory of later jobs ahead of them: every submission lane's
  * inter-stage scratch and the device buffers of the first `tickets` packed-job
  * slots, for jobs over pictures up to width x height with up to max_refs
- * reference slots and any pack layout. Submissions within those bounds then
- * allocate nothing (a job beyond them still grows the buffers it needs). */
+ * reference slots and any pack layout, and for batches of up to
+ * SVTME_MAX_BATCH_JOBS such pictures of one reference slot each (a TF window).
+ * Submissions within those bounds then allocate nothing (a job beyond them
+ * still grows the buffers it needs, after its lane's queued work has run). */
 svtme_status svtme_reserve(svtme_ctx *ctx, uint32_t width, uint32_t height, uint32_t max_refs, uint32_t tickets);
 /* Keep `count` picture buffers of a width x height picture (its three padded
  * planes) in the context's free pool, so that the uploads of up to that many

@@ -635,6 +635,7 @@ typedef struct GlueTrace { /* one job (SVTME_GLUE_TRACE) */
     uint32_t n_sb, inflight, uploads;
     double t_create, t_submitted, t_done, upload_s;
     float gpu_ms, copy_ms; /* GPU-side: lane turn -> packed output; -> host memory (svtme_ticket_wait_timed) */
+    double t_prep, t_locked; /* job(s) built and buffers taken; the GPU lock held (submission starts) */
 } GlueTrace;
 
 static double now_s(void) {
@@ -684,10 +685,11 @@ static void glue_trace_at_exit(void) {
         const GlueTrace *t = &G.trace[i];
         fprintf(f, "{\"pn\": %llu, \"tf\": %d, \"sbs\": %u, \"inflight\": %u, \"uploads\": %u, "
                    "\"upload_ms\": %.4f, \"create_ms\": %.4f, \"submitted_ms\": %.4f, \"done_ms\": %.4f, "
-                   "\"gpu_ms\": %.4f, \"copy_ms\": %.4f}\n",
+                   "\"gpu_ms\": %.4f, \"copy_ms\": %.4f, \"prep_ms\": %.4f, \"lock_ms\": %.4f}\n",
                 (unsigned long long)(t->pn & GLUE_PN_MASK), t->tf, t->n_sb, t->inflight, t->uploads, 1e3 * t->upload_s,
                 1e3 * (t->t_create - G.t0), 1e3 * (t->t_submitted - G.t0), 1e3 * (t->t_done - G.t0), t->gpu_ms,
-                t->copy_ms);
+                t->copy_ms, t->t_prep ? 1e3 * (t->t_prep - t->t_create) : 0.0,
+                t->t_prep ? 1e3 * (t->t_locked - t->t_prep) : 0.0);
     }
     fclose(f);
 }
@@ -1503,8 +1505,10 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
         uint64_t tickets[SVTME_MAX_BATCH_JOBS] = {0};
         unsigned long long up_n = 0;
         double up_s = 0;
+        double t_prep = now_s(), t_locked = t_prep;
         if (!rc) {
             pthread_mutex_lock(&G.gpu);
+            t_locked = now_s();
             up_n = G.n.uploads, up_s = G.n.upload_s;
             rc   = submit_jobs(js, objs, n, pcs, me_ctx, tickets);
             up_n = G.n.uploads - up_n, up_s = G.n.upload_s - up_s;
@@ -1527,7 +1531,8 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
                 G.n.job_sbs += js[k]->n_sb;
             if (G.trace_path) {
                 const GlueTrace t = {js[k]->job.picture_number, js[k]->job.me_type == SVTME_ME_MCTF, js[k]->n_sb,
-                                     inflight, k ? 0 : (uint32_t)up_n, t_start, t_wait, t_done, k ? 0 : up_s, gms, cms};
+                                     inflight, k ? 0 : (uint32_t)up_n, t_start, t_wait, t_done, k ? 0 : up_s, gms, cms,
+                                     t_prep, t_locked};
                 trace_add(&t);
             }
             js[k]->state = rk ? -1 : 1;

@@ -1176,7 +1176,11 @@ extern "C" svtme_status svtme_reserve(svtme_ctx *c, uint32_t width, uint32_t hei
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_reserve: bad arguments");
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
-    const size_t sbs = svtme_sb_total(width, height), slots = sbs * max_refs;
+    // one picture with max_refs slots, or a batch of SVTME_MAX_BATCH_JOBS pictures of one
+    // slot each (a TF window): the per-SB scratch covers the batch's SBs
+    const size_t pic_sbs = svtme_sb_total(width, height);
+    const size_t sbs     = pic_sbs * SVTME_MAX_BATCH_JOBS;
+    const size_t slots   = pic_sbs * std::max<size_t>(max_refs, SVTME_MAX_BATCH_JOBS);
     svtme_status st;
     for (uint32_t l = 0; l < SVTME_LANES; l++) {
         if ((st = ensure_lane(c, l)))
@@ -1199,7 +1203,7 @@ extern "C" svtme_status svtme_reserve(svtme_ctx *c, uint32_t width, uint32_t hei
     }
     const svtme_pack_layout pa = {SVTME_PU_COUNT, SVTME_MAX_PA_ME_CAND, SVTME_MAX_PA_ME_MV, 0, 1, {0, 0}};
     const svtme_pack_layout tf = {0, 0, 0, 1, 0, {0, 0}};
-    const size_t need = std::max(packed_job_bytes(sbs, max_refs, &pa), packed_job_bytes(sbs, max_refs, &tf));
+    const size_t need = std::max(packed_job_bytes(pic_sbs, max_refs, &pa), packed_job_bytes(pic_sbs, max_refs, &tf));
     uint32_t k = 0;
     for (auto &t : c->tickets) {
         if (k == tickets)
