@@ -88,17 +88,18 @@
 #include "pcs.h"
 #include "pic_analysis_results.h"
 #include "reference_object.h"
+#include "enc_mode_config.h"
+#include "pd_results.h"
 #include "sequence_control_set.h"
 #ifdef SVTME_GLUE_WRAP
 #include "enc_handle.h"
-#include "enc_mode_config.h"
-#include "pd_results.h"
 #endif
 
 #include "svtme.h"
 
 EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
                                         uint32_t b64_origin_y, MeContext *me_ctx, EbPictureBufferDesc *input_ptr);
+void svtme_glue_prefetch_pa(PictureParentControlSet *pcs);
 void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDesc *full);
 void svtme_glue_release(void);
 void svt_aom_setup_rtcd_hip_parity(void);

@@ -35,7 +35,10 @@ def code_objects(lib_path, workdir):
     import os
 
     fb = os.path.join(workdir, "fatbin.bin")
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", lib_path], check=True)
+    # (an explicit output file: objcopy with none rewrites its input in place, and the
+    # library may be mapped by the running process)
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", lib_path, os.path.join(workdir, "scratch.so")],
+                   check=True)
     data = open(fb, "rb").read()
     magic = b"__CLANG_OFFLOAD_BUNDLE__"
     offs, i = [], data.find(magic)
