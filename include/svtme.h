@@ -277,14 +277,17 @@ svtme_status svtme_picture_upload(svtme_ctx *ctx, uint64_t picture_number, const
  * searched plane is the 8-bit MSB plane p >> 2 (enc_handle.c:4964-4972). */
 svtme_status svtme_picture_upload_10bit(svtme_ctx *ctx, uint64_t picture_number, const uint16_t *y,
                                         uint32_t stride, uint32_t width, uint32_t height);
-/* Asynchronous form of svtme_picture_upload: the rows are copied by DMA into
- * the resident plane and the pyramid is built on the context's upload stream,
- * overlapping with jobs already running; the call returns once the copy is
- * queued (pageable memory: once the driver has staged it). The first job that
- * reads the picture waits for the upload on the GPU. With pinned host memory
- * the caller keeps `y` unchanged until svtme_sync() or a job reading the
- * picture has completed. Jobs queued earlier that read an older version of the
- * picture finish before it is overwritten. */
+/* Asynchronous form of svtme_picture_upload: the pyramid is built on the
+ * context's upload stream, overlapping with jobs already running. From
+ * page-locked host memory (svtme_host_alloc, svtme_host_register, hipHostMalloc)
+ * the build reads the plane itself over PCIe; from pageable memory the rows are
+ * first copied by DMA into a device staging plane (SVTME_UPLOAD_ZERO_COPY=0:
+ * always the DMA). The call returns once the work is queued (pageable memory:
+ * once the driver has staged it). The first job that reads the picture waits
+ * for the upload on the GPU. With pinned host memory the caller keeps `y`
+ * unchanged until svtme_sync() or a job reading the picture has completed.
+ * Jobs queued earlier that read an older version of the picture finish before
+ * it is overwritten. */
 svtme_status svtme_picture_upload_async(svtme_ctx *ctx, uint64_t picture_number, const uint8_t *y, uint32_t stride,
                                         uint32_t width, uint32_t height);
 /* Asynchronous upload from PAGEABLE memory the library never page-locks (an
@@ -404,8 +407,8 @@ svtme_status svtme_ticket_wait_timed(svtme_ctx *ctx, uint64_t ticket, float *gpu
 void *svtme_host_alloc(uint64_t bytes);
 void svtme_host_free(void *p);
 /* Page-lock an existing host range (e.g. an encoder's picture buffer) so that
- * svtme_picture_upload_async copies it by DMA without staging it through the
- * CPU; svtme_host_unregister undoes it once the copies reading it have run. */
+ * svtme_picture_upload_async reads it from the GPU without staging it through
+ * the CPU; svtme_host_unregister undoes it once the uploads reading it have run. */
 svtme_status svtme_host_register(void *p, uint64_t bytes);
 svtme_status svtme_host_unregister(void *p);
 /* Size the device memory of later jobs ahead of them: every submission lane's

@@ -38,6 +38,8 @@ extern "C" hipError_t svtme_launch_stages(const DevJob *d_jobs, const DevJob *h_
                                           hipEvent_t *ev, uint32_t *mask);
 extern "C" uint32_t svtme_launch_key(const DevJob *dj);
 extern "C" hipError_t svtme_prime_pyramid(void);
+extern "C" hipError_t svtme_launch_host_rows(const uint8_t *src, uint32_t src_stride, int w, int h, uint8_t *dst,
+                                             uint32_t dst_stride, hipStream_t s);
 extern "C" hipError_t svtme_prime_pack(void);
 extern "C" hipError_t svtme_prime_stages(void);
 extern "C" void svtme_stage_a_list(const svtme_job *job, uint8_t *list, uint32_t *count);
@@ -175,6 +177,9 @@ struct svtme_ctx {
     // while enabled (attached to the dispatch packets: hipExtLaunchKernelGGL)
     static constexpr int kTimeSets = 256;
     bool timing = false;
+    // uploads from page-locked host memory build the pyramid from the host plane itself
+    // over PCIe (no DMA into a staging plane); SVTME_UPLOAD_ZERO_COPY=0: DMA + build
+    bool zero_copy = true;
     hipEvent_t tev[kTimeSets][10] = {};
     uint32_t tmask[kTimeSets] = {};
     int t_pending = 0;
@@ -232,6 +237,8 @@ extern "C" svtme_status svtme_ctx_create(int device, svtme_ctx **out) {
         if (const char *v = getenv(e.var))
             if (*v && strcmp(v, "0") != 0)
                 c->paths |= e.bit;
+    if (const char *v = getenv("SVTME_UPLOAD_ZERO_COPY"))
+        c->zero_copy = !(*v && strcmp(v, "0") == 0);
     const svtme_status ps = prepare(c);
     if (ps) {
         svtme_ctx_destroy(c);
@@ -524,6 +531,35 @@ static svtme_status build_pyramid(svtme_ctx *c, PicBuf *pb, const void *dsrc, ui
     return SVTME_OK;
 }
 
+// The device address of a page-locked host range (hipHostMalloc / hipHostRegister),
+// or null for pageable memory (then a DMA through a staging plane is needed)
+static const uint8_t *device_view(const svtme_ctx *c, const void *y) {
+    if (!c->zero_copy)
+        return nullptr;
+    hipPointerAttribute_t pa;
+    if (hipPointerGetAttributes(&pa, y) != hipSuccess) {
+        (void)hipGetLastError(); // (pageable memory reads as an error)
+        return nullptr;
+    }
+    if (pa.type != hipMemoryTypeHost || !pa.devicePointer)
+        return nullptr;
+    return (const uint8_t *)pa.devicePointer + (pa.hostPointer ? ((const uint8_t *)y - (const uint8_t *)pa.hostPointer) : 0);
+}
+
+// the pyramid of an 8-bit plane the device reads in page-locked host memory: the
+// interior of level 0 streamed over PCIe by a few workgroups (svtme_launch_host_rows),
+// then the padding and the lower levels from it, on device
+static svtme_status build_pyramid_host(svtme_ctx *c, PicBuf *pb, const uint8_t *dv, uint32_t stride, uint32_t w,
+                                       uint32_t h, hipStream_t st) {
+    const DevPlane &p0 = pb->pyr.lv[0];
+    HIP_TRY(svtme_launch_host_rows(dv, stride, (int)w, (int)h, p0.base, (uint32_t)p0.stride, st));
+    return build_pyramid(c, pb, p0.base, (uint32_t)p0.stride, w, h, 0, st);
+}
+// zero-copy needs dword-aligned rows (the stream kernel's loads and stores)
+static bool zero_copy_ok(const void *y, uint32_t stride, const PicBuf *pb) {
+    return (((uintptr_t)y | stride | (uintptr_t)pb->pyr.lv[0].base | (uint32_t)pb->pyr.lv[0].stride) & 3) == 0;
+}
+
 static svtme_status upload_host(svtme_ctx *c, uint64_t pn, const void *y, uint32_t stride, uint32_t w, uint32_t h,
                                 int ten_bit) {
     if (!c || !y || w == 0 || h == 0 || stride < w)
@@ -531,17 +567,23 @@ static svtme_status upload_host(svtme_ctx *c, uint64_t pn, const void *y, uint32
     std::lock_guard<std::mutex> lk(c->mu);
     HIP_TRY(hipSetDevice(c->device));
     const uint32_t bpp = ten_bit ? 2 : 1;
-    svtme_status st    = ensure_buf(&c->staging, &c->staging_cap, (size_t)w * h * bpp);
-    if (st)
-        return st;
-    HIP_TRY(hipMemcpy2DAsync(c->staging, (size_t)w * bpp, y, (size_t)stride * bpp, (size_t)w * bpp, h,
-                             hipMemcpyHostToDevice, c->stream));
+    const uint8_t *dv  = ten_bit ? nullptr : device_view(c, y); // page-locked: read in place
+    svtme_status st;
     PicBuf *pb;
     if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
         return st;
+    if (dv && !zero_copy_ok(y, stride, pb))
+        dv = nullptr;
+    if (!dv) {
+        if ((st = ensure_buf(&c->staging, &c->staging_cap, (size_t)w * h * bpp)))
+            return st;
+        HIP_TRY(hipMemcpy2DAsync(c->staging, (size_t)w * bpp, y, (size_t)stride * bpp, (size_t)w * bpp, h,
+                                 hipMemcpyHostToDevice, c->stream));
+    }
     if ((st = join_upload(c, *pb, 0)) || (st = after_readers(c, *pb, c->stream)))
         return st;
-    if ((st = build_pyramid(c, pb, c->staging, w, w, h, ten_bit)))
+    if ((st = dv ? build_pyramid_host(c, pb, dv, stride, w, h, c->stream)
+                 : build_pyramid(c, pb, c->staging, w, w, h, ten_bit)))
         return st;
     HIP_TRY(hipStreamSynchronize(c->stream));
     return SVTME_OK;
@@ -618,6 +660,16 @@ extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, co
         return st;
     if (!pb->ready)
         HIP_TRY(hipEventCreateWithFlags(&pb->ready, hipEventDisableTiming));
+    // a page-locked plane the device can read: the pyramid build reads it over PCIe
+    // itself (no DMA into a staging plane, no second pass over it)
+    const uint8_t *dy = device_view(c, y);
+    if (dy && zero_copy_ok(y, stride, pb)) {
+        if ((st = build_pyramid_host(c, pb, dy, stride, w, h, c->ustream)))
+            return st;
+        HIP_TRY(hipEventRecord(pb->ready, c->ustream));
+        pb->pending = (1u << SVTME_LANES) - 1u;
+        return SVTME_OK;
+    }
     // one linear copy of the span from the first to the last sample (rows keep their
     // stride; a padded encoder plane's margins ride along): a 2D copy out of
     // pageable memory goes row by row

@@ -28,16 +28,22 @@ __global__ void __launch_bounds__(256) k_build_full(const void *__restrict__ src
         return;
     const int ry = idx / dw_per_row, rx4 = (idx - ry * dw_per_row) * 4;
     const int y  = clampi(ry - top, 0, h - 1);
+    const int x0 = rx4 - left;
     uint32_t v   = 0;
+    const uint8_t *p8 = (const uint8_t *)src + (size_t)y * src_stride + x0;
+    if (!TEN_BIT && x0 >= 0 && x0 + 3 < w && ((uintptr_t)p8 & 3) == 0) {
+        v = *(const uint32_t *)p8; // interior: one dword (a plane read over PCIe moves a quarter of the requests)
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int x = clampi(rx4 + k - left, 0, w - 1);
-        uint32_t p;
-        if (TEN_BIT)
-            p = (uint32_t)(((const uint16_t *)src)[(size_t)y * src_stride + x] >> 2);
-        else
-            p = ((const uint8_t *)src)[(size_t)y * src_stride + x];
-        v |= p << (8 * k);
+        for (int k = 0; k < 4; k++) {
+            const int x = clampi(x0 + k, 0, w - 1);
+            uint32_t p;
+            if (TEN_BIT)
+                p = (uint32_t)(((const uint16_t *)src)[(size_t)y * src_stride + x] >> 2);
+            else
+                p = ((const uint8_t *)src)[(size_t)y * src_stride + x];
+            v |= p << (8 * k);
+        }
     }
     uint32_t *row = (uint32_t *)(dst.base - (size_t)top * dst.stride - left);
     row[idx]      = v;
@@ -62,6 +68,54 @@ __global__ void __launch_bounds__(256) k_build_down(DevPlane prev, DevPlane dst,
     }
     uint32_t *row = (uint32_t *)(dst.base - (size_t)top * dst.stride - left);
     row[idx]      = v;
+}
+
+// level 0's interior straight from a page-locked host plane (read over PCIe):
+// a few workgroups stream the rows in 16-byte chunks (two chunks in flight per
+// thread), so the upload holds a handful of the GPU's workgroup slots while it
+// waits on PCIe instead of a grid's worth; k_build_full then pads the plane from
+// its own interior. src, src_stride, dst and dst_stride are 4-byte aligned.
+#define HOST_ROWS_WGS 128
+__global__ void __launch_bounds__(256) k_host_rows(const uint8_t *__restrict__ src, uint32_t src_stride, int w, int h,
+                                                   uint8_t *__restrict__ dst, uint32_t dst_stride) {
+    const int chunks  = (w + 15) >> 4;
+    const int total   = chunks * h;
+    const int step    = (int)gridDim.x * 256;
+    auto copy = [&](int i, uint32_t (&v)[4], bool load) {
+        const int y = i / chunks, x = (i - y * chunks) * 16;
+        const uint32_t *s = (const uint32_t *)(src + (size_t)y * src_stride + x);
+        uint32_t *d       = (uint32_t *)(dst + (size_t)y * dst_stride + x);
+        const int nb      = min(16, w - x);
+        if (nb == 16) {
+            if (load) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) v[k] = s[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) d[k] = v[k];
+            }
+        } else if (!load) { // the row's last partial chunk, bytewise
+            const uint8_t *sb = (const uint8_t *)s;
+            uint8_t *db       = (uint8_t *)d;
+            for (int k = 0; k < nb; k++) db[k] = sb[k];
+        }
+    };
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += 2 * step) {
+        uint32_t a[4], b[4];
+        const bool two = i + step < total;
+        copy(i, a, true);
+        if (two)
+            copy(i + step, b, true);
+        copy(i, a, false);
+        if (two)
+            copy(i + step, b, false);
+    }
+}
+
+extern "C" hipError_t svtme_launch_host_rows(const uint8_t *src, uint32_t src_stride, int w, int h, uint8_t *dst,
+                                             uint32_t dst_stride, hipStream_t s) {
+    hipLaunchKernelGGL(k_host_rows, dim3(HOST_ROWS_WGS), dim3(256), 0, s, src, src_stride, w, h, dst, dst_stride);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t svtme_launch_build_full(const void *src, uint32_t src_stride, int w, int h, int ten_bit,
