@@ -75,7 +75,9 @@ __global__ void __launch_bounds__(256) k_build_down(DevPlane prev, DevPlane dst,
 // thread), so the upload holds a handful of the GPU's workgroup slots while it
 // waits on PCIe instead of a grid's worth; k_build_full then pads the plane from
 // its own interior. src, src_stride, dst and dst_stride are 4-byte aligned.
+#ifndef HOST_ROWS_WGS
 #define HOST_ROWS_WGS 128
+#endif
 __global__ void __launch_bounds__(256) k_host_rows(const uint8_t *__restrict__ src, uint32_t src_stride, int w, int h,
                                                    uint8_t *__restrict__ dst, uint32_t dst_stride) {
     const int chunks  = (w + 15) >> 4;
