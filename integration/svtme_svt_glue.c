@@ -100,6 +100,7 @@
 EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
                                         uint32_t b64_origin_y, MeContext *me_ctx, EbPictureBufferDesc *input_ptr);
 void svtme_glue_prefetch_pa(PictureParentControlSet *pcs);
+void svtme_glue_prefetch_tf(PictureParentControlSet *centre);
 void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDesc *full);
 void svtme_glue_release(void);
 void svt_aom_setup_rtcd_hip_parity(void);
@@ -470,6 +471,12 @@ void svtme_job_from_tf(svtme_job *job, const PictureParentControlSet *centre, co
     job->me_type               = SVTME_ME_MCTF;
     job->tf_me_exit_th         = me->tf_me_exit_th;
     svtme_controls_from_me_context(&job->ctrl, me);
+    /* svt_aom_sig_deriv_me_tf leaves these two PA-ME candidate controls as the ME
+     * thread's last PA picture set them; a TF job has no candidate arrays
+     * (motion_estimation.c:3126), so they do not change it: zero, so that the
+     * same pair is the same job whichever thread asks for it */
+    job->ctrl.prune_me_candidates_th     = 0;
+    job->ctrl.use_best_unipred_cand_only = 0;
 }
 
 /* ==========================================================================
@@ -1418,6 +1425,101 @@ void svtme_glue_prefetch_pa(PictureParentControlSet *pcs) {
     pthread_mutex_unlock(&G.mu);
 }
 
+/* Picture decision has posted the temporal-filtering tasks of `centre`
+ * (pd_process.c:3404-3426): every (central, reference) pair of its window is
+ * known (tf_window: the filter's frame order and outlier skips, all computed
+ * by picture decision), so their jobs go to the GPU in one launch now, built
+ * as the TF code will build them (svt_aom_sig_deriv_me_tf, me_process.c:123;
+ * the filter's controls, temporal_filtering.c:4112; create_me_context_and_
+ * picture_control's FULL_SAD HME and set_hme_search_params_mctf(ctx, 0),
+ * :2759-2767, 3127-3168). The ME threads' calls then find them as for PA. */
+#define GLUE_TF_LAUNCH 4
+void svtme_glue_prefetch_tf(PictureParentControlSet *centre) {
+    pthread_once(&G.once, glue_init);
+    if (!G.ctx || !G.prefetch || !G.tf_batch || !centre || pcs_slot(centre) < 0 || !centre->tf_ctrls.enabled ||
+        !centre->temp_filt_pcs_list || !centre->enhanced_unscaled_pic || !centre->pa_ref_pic_wrapper)
+        return;
+    static __thread MeContext *me;
+    if (!me && !(me = (MeContext *)calloc(1, sizeof(MeContext))))
+        return;
+    svt_aom_sig_deriv_me_tf(centre, me);
+    me->tf_ctrls                    = centre->tf_ctrls;
+    me->hme_search_method           = FULL_SAD_SEARCH;
+    me->hme_l0_sa.sa_min            = me->hme_l0_sa_default_tf.sa_min;
+    me->hme_l0_sa.sa_max            = me->hme_l0_sa_default_tf.sa_max;
+    me->me_type                     = ME_MCTF;
+    me->num_of_list_to_search       = 1;
+    me->num_of_ref_pic_to_search[0] = 1;
+    me->num_of_ref_pic_to_search[1] = 0;
+    me->temporal_layer_index        = centre->temporal_layer_index;
+    me->is_ref                      = centre->is_ref;
+    me->tf_me_exit_th               = centre->tf_ctrls.me_exit_th;
+    me->me_ds_ref_array[0][0].picture_number = 0;
+    svtme_job tmpl;
+    svtme_job_from_tf(&tmpl, centre, me, centre->enhanced_unscaled_pic);
+    tmpl.ref_picture_number[0][0] = ~0ull; /* (tf_window skips the template's own reference) */
+    svtme_job pairs[SVTME_MAX_BATCH_JOBS];
+    const EbPaReferenceObject *po[SVTME_MAX_BATCH_JOBS];
+    const int np = tf_window(centre, me, &tmpl, pairs, po, SVTME_MAX_BATCH_JOBS);
+    if (np <= 0)
+        return;
+    GlueJob *js[SVTME_MAX_BATCH_JOBS];
+    const EbPaReferenceObject *objs[SVTME_MAX_BATCH_JOBS];
+    int n = 0;
+    pthread_mutex_lock(&G.mu);
+    for (int k = 0; k < np; k++) {
+        if (job_find(&pairs[k])) /* (already running) */
+            continue;
+        GlueJob *x = job_new(centre, &pairs[k], 0);
+        job_unlink(x); /* listed once submitted */
+        if (buf_take(x, (size_t)x->n_sb * x->stride, buf_worst(x->n_sb))) {
+            job_free(x);
+            break;
+        }
+        objs[n] = po[k];
+        js[n++] = x;
+    }
+    pthread_mutex_unlock(&G.mu);
+    if (!n)
+        return;
+    /* launches of at most GLUE_TF_LAUNCH pairs on alternating lanes: the window's
+     * first pairs (the filter's first calls) are ready before the whole window is */
+    uint64_t tickets[SVTME_MAX_BATCH_JOBS] = {0};
+    int rc = 0, launches = 0;
+    pthread_mutex_lock(&G.gpu);
+    for (int k0 = 0; k0 < n && !rc; k0 += GLUE_TF_LAUNCH) {
+        const int m = n - k0 < GLUE_TF_LAUNCH ? n - k0 : GLUE_TF_LAUNCH;
+        /* the launch's job 0 takes its reference planes through the context, as the TF code sets them */
+        me->me_ds_ref_array[0][0].picture_ptr           = objs[k0]->input_padded_pic;
+        me->me_ds_ref_array[0][0].quarter_picture_ptr   = objs[k0]->quarter_downsampled_picture_ptr;
+        me->me_ds_ref_array[0][0].sixteenth_picture_ptr = objs[k0]->sixteenth_downsampled_picture_ptr;
+        me->me_ds_ref_array[0][0].picture_number        = objs[k0]->picture_number;
+        rc = submit_jobs(js + k0, objs + k0, m, centre, me, tickets + k0);
+        launches += !rc;
+    }
+    pthread_mutex_unlock(&G.gpu);
+    pthread_mutex_lock(&G.mu);
+    G.n.launches += launches;
+    for (int k = 0; k < n; k++) {
+        GlueJob *j = js[k];
+        if (!tickets[k]) { /* (its launch failed: the SB calls start their own job) */
+            j->state = -1;
+            job_free(j);
+            continue;
+        }
+        j->ticket     = tickets[k];
+        j->prefetched = 1;
+        G.n.prefetched++;
+        G.n.tf_batched += k > 0;
+        j->next = G.jobs;
+        G.jobs  = j;
+        if (job_find(&j->job) != j)
+            j->stale = 1;
+    }
+    settle_prefetched(pick_stale, 0);
+    pthread_mutex_unlock(&G.mu);
+}
+
 EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b64_index, uint32_t b64_origin_x,
                                         uint32_t b64_origin_y, MeContext *me_ctx, EbPictureBufferDesc *input_ptr) {
     pthread_once(&G.once, glue_init);
@@ -1461,7 +1563,8 @@ EbErrorType svtme_motion_estimation_b64(PictureParentControlSet *pcs, uint32_t b
         if (!rk)
             G.n.job_sbs += j->n_sb;
         if (G.trace_path) {
-            const GlueTrace t = {j->job.picture_number, 0, j->n_sb, inflight, 0, t_start, t_start, t_done, 0, gms, cms};
+            const GlueTrace t = {j->job.picture_number, j->job.me_type == SVTME_ME_MCTF, j->n_sb, inflight, 0,
+                                 t_start, t_start, t_done, 0, gms, cms};
             trace_add(&t);
         }
         j->state = rk ? -1 : 1;
@@ -1626,6 +1729,8 @@ EbErrorType __wrap_svt_post_full_object(EbObjectWrapper *object_ptr) {
             const PictureDecisionResults *r = (const PictureDecisionResults *)object_ptr->object_ptr;
             if (r->task_type == TASK_PAME && r->segment_index == 0)
                 svtme_glue_prefetch_pa((PictureParentControlSet *)r->pcs_wrapper->object_ptr);
+            else if (r->task_type == TASK_TFME && r->segment_index == 0)
+                svtme_glue_prefetch_tf((PictureParentControlSet *)r->pcs_wrapper->object_ptr);
             break;
         } else if (__atomic_load_n(&g_enc[i].pa_res, __ATOMIC_ACQUIRE) == res) {
             const PictureAnalysisResults *r = (const PictureAnalysisResults *)object_ptr->object_ptr;

@@ -53,18 +53,19 @@ def test_two_encoders_in_one_process(case, workdir):
 
 
 @pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
-@pytest.mark.parametrize("case", ["ra360_p12", "360p_p8_lowdelay", "240p_p8_ragged"])
-def test_pa_jobs_prefetched_at_picture_decision(case, workdir):
+@pytest.mark.parametrize("case", ["ra360_p12", "360p_p8_lowdelay", "240p_p8_ragged", "360p_p4"])
+def test_jobs_prefetched_at_picture_decision(case, workdir):
     """Every PA-ME job is submitted when picture decision posts the picture's ME
-    tasks (pd_process.c:3544-3556), built from the encoder's own
-    svt_aom_sig_deriv_me into a scratch context: the ME threads' first SB call
-    finds that very job (field for field), none is left unused, and the
+    tasks (pd_process.c:3544-3556), and every TF-ME pair of a window when it
+    posts the window's filtering tasks (:3404-3426), built from the encoder's
+    own svt_aom_sig_deriv_me[_tf] into a scratch context: the ME threads' SB
+    calls find those very jobs (field for field), none is left unused, and the
     bitstream is unchanged; SVTME_GLUE_PREFETCH=0 submits at the first SB call."""
     r = E.check(case, "ora", workdir)
-    assert r["prefetched"] == r["pa_jobs"] > 0 and r["prefetch_hits"] == r["prefetched"], r
+    assert r["prefetched"] == r["pa_jobs"] + r["tf_jobs"] > 0 and r["prefetch_hits"] == r["prefetched"], r
     assert r["unused_jobs"] == 0 and r["fallback_sbs"] == 0
     r0 = E.check(case, "ora", workdir, env_extra={"SVTME_GLUE_PREFETCH": "0"})
-    assert r0["prefetched"] == 0 and r0["pa_jobs"] == r["pa_jobs"]
+    assert r0["prefetched"] == 0 and r0["pa_jobs"] == r["pa_jobs"] and r0["tf_jobs"] == r["tf_jobs"]
 
 
 def _no_rtcd_registered(r):
