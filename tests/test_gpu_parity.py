@@ -95,6 +95,51 @@ def test_pyramid_parity(svtme, gpu):
         gpu.release(77)
 
 
+def test_zero_copy_upload_parity(svtme, gpu):
+    """Uploads from page-locked memory (the GPU streams the host plane itself,
+    k_host_rows) equal the reference's pyramid like the DMA path's, at widths
+    that leave a partial 16-byte chunk per row, with the plane at an offset
+    inside a larger pinned buffer and a padded stride, synchronous and
+    asynchronous; an unaligned pinned source (odd byte offset) falls back to
+    the DMA and still matches; so does a context with SVTME_UPLOAD_ZERO_COPY=0."""
+    import os
+
+    import torch
+
+    S = svtme
+    dma_ctx = None
+    try:
+        os.environ["SVTME_UPLOAD_ZERO_COPY"] = "0"
+        dma_ctx = S.GpuME(0)
+    finally:
+        del os.environ["SVTME_UPLOAD_ZERO_COPY"]
+    try:
+        for (w, h, pad, off) in ((426, 240, 2, 0), (1000, 562, 72, 4 * 1000 + 8), (72, 40, 12, 0),
+                                 (328, 200, 5, 1)):
+            f = S.Synth(w, h).frame(5)
+            stride = w + pad
+            buf = torch.zeros(off + stride * h + 64, dtype=torch.uint8).pin_memory()
+            view = buf[off:off + stride * h].view(h, stride)
+            view[:, :w] = torch.from_numpy(np.ascontiguousarray(f))
+            ptr = buf.data_ptr() + off
+            ref = S.build_host_pyramid(f, "oracle")
+            gpu.upload_async(78, ptr, w, h, stride)
+            gpu._check(gpu.lib.svtme_picture_upload(gpu.ctx, 79, ptr, stride, w, h), "svtme_picture_upload")
+            dma_ctx.upload_async(80, ptr, w, h, stride)
+            gpu.sync()
+            dma_ctx.sync()
+            for lv, name in enumerate(("full", "quarter", "sixteenth")):
+                exp = getattr(ref, name)
+                assert np.array_equal(gpu.download(78, lv), exp), (w, h, pad, off, name, "async")
+                assert np.array_equal(gpu.download(79, lv), exp), (w, h, pad, off, name, "sync")
+                assert np.array_equal(dma_ctx.download(80, lv), exp), (w, h, pad, off, name, "dma")
+            for pn in (78, 79):
+                gpu.release(pn)
+            dma_ctx.release(80)
+    finally:
+        dma_ctx.close()
+
+
 def test_10bit_msb_parity(svtme, gpu):
     S = svtme
     w, h = 640, 360
