@@ -1,6 +1,7 @@
 # VALU / SALU / LDS instruction counts of the k_hme stop-after builds (scripts/build_phase_libs.sh):
 # the differences between consecutive builds are the phases' instruction counts.
 # usage: WL=4k_p8 P=1 [PMC="SQ_... TA_..."] [O=${O:-gpurun_out/phase_pmc}] bash scripts/gpu_phase_pmc.sh
+# then: python3 scripts/phase_pmc_summary.py $O (per-SB counts per phase, JSON)
 cd "$GRAFT_REPO_ROOT"
 WL=${WL:-4k_p8}; P=${P:-1}
 O=${O:-gpurun_out/phase_pmc}

@@ -66,6 +66,47 @@ def main():
         out["runs"].append({"gap_ms": gap, **{f"{k}_p50": q(c, 50) for c, k in enumerate(("submit", "wait", "job", "gpu", "copy"))},
                             **{f"{k}_p90": q(c, 90) for c, k in enumerate(("submit", "wait", "job", "gpu", "copy"))},
                             "served_sb_per_s": round(S.sb_total(wl["w"], wl["h"]) / (float(np.mean(a[:, 2])) * 1e-3), 1)})
+    # TF windows: n (central, reference) pairs in one svtme_submit_pictures_packed_async, as the glue's
+    # tf_window submits them (whole records, no SB results)
+    for t in (4, 5, 6, 9, 10, 11, 12):
+        if t not in (7, 8):
+            gpu.upload(t, W.workload_frame(name, syn, t))
+    Lt = S.PackLayout()
+    Lt.n_pus, Lt.max_cand, Lt.max_refs, Lt.full_records, Lt.sb_results = 0, 0, 0, 1, 0
+    lib.svtme_submit_pictures_packed_async.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(S.Job),
+                                                       C.POINTER(S.PackLayout), C.POINTER(C.c_void_p),
+                                                       C.POINTER(C.c_uint64)]
+    lib.svtme_submit_pictures_packed_async.restype = C.c_int32
+    tfbytes = S.sb_total(wl["w"], wl["h"]) * S.packed_sb_bytes(Lt, 1)
+    tbufs = [lib.svtme_host_alloc(tfbytes) for _ in range(8)]
+    out["tf_windows"] = []
+    for npairs in (1, 2, 4, 8):
+        base = W.workload_job("4k_tf_p8")
+        refs = [4, 5, 6, 7, 9, 10, 11, 12][:npairs]
+        jobs = []
+        for r in refs:
+            j = W.workload_job("4k_tf_p8")
+            j.ref_picture_number[0][0] = r
+            jobs.append(j)
+        arr_j = (S.Job * npairs)(*jobs)
+        arr_l = (S.PackLayout * npairs)(*([Lt] * npairs))
+        arr_p = (C.c_void_p * npairs)(*tbufs[:npairs])
+        rec = []
+        for i in range(25):
+            tks = (C.c_uint64 * npairs)()
+            t0 = time.perf_counter()
+            gpu._check(lib.svtme_submit_pictures_packed_async(gpu.ctx, i & 1, npairs, arr_j, arr_l, arr_p, tks), "tf submit")
+            t1 = time.perf_counter()
+            for k in range(npairs):
+                gpu._check(lib.svtme_ticket_wait(gpu.ctx, tks[k]), "tf wait")
+            t2 = time.perf_counter()
+            rec.append(((t1 - t0) * 1e3, (t2 - t0) * 1e3))
+        a = np.array(rec[5:])
+        out["tf_windows"].append({"pairs": npairs, "submit_p50": round(float(np.median(a[:, 0])), 4),
+                                  "job_p50": round(float(np.median(a[:, 1])), 4)})
+        del base
+    for b in tbufs:
+        lib.svtme_host_free(b)
     print(json.dumps(out))
     for b in bufs:
         lib.svtme_host_free(b)
