@@ -30,10 +30,11 @@ if [ -d "$REF/Source" ]; then
          -I$REF/third_party/fastfeat -I$ENC/gen -I$ROOT/include"
     gcc $SAN -std=gnu99 -fPIC -ffunction-sections -DSVTME_GLUE_WRAP -DEXCLUDE_HASH=0 -DREPRODUCIBLE_BUILDS=0 \
         -DEN_AVX512_SUPPORT=0 -DHAVE_CPUINFO=0 -DNDEBUG $INC -c -o "$OUT/glue.o" "$ROOT/integration/svtme_svt_glue.c"
+    # (the wraps of oracle/encoder.mk's WRAP)
     gcc -fsanitize=address,undefined -o "$OUT/svtav1enc_ora" "$ENC"/obj/Source/App/*.o \
         "$ENC"/obj/third_party/safestringlib/*.o "$OUT/glue.o" "$ENC/libsvtenc.a" \
         -Wl,--wrap=svt_aom_motion_estimation_b64 -Wl,--wrap=svt_aom_downsample_filtering_input_picture \
-        -Wl,--wrap=svt_av1_enc_deinit -Wl,--wrap=svt_aom_picture_analysis_result_creator \
+        -Wl,--wrap=svt_av1_enc_deinit -Wl,--wrap=svt_av1_enc_init \
         -Wl,--wrap=svt_post_full_object \
         -L"$OUT" -loraclejob -Wl,-rpath,"$OUT" -Wl,--gc-sections -lpthread -lm
 fi

@@ -1129,7 +1129,7 @@ __device__ unsigned long long g_clock_bins[4096][3];
 #define HME_STOP(k)
 #endif
 
-#define HQ 3  // position quads per HME-L2 tile (8-wide areas at any alignment: 2 or 3 quads)
+#define HQ 2  // position quads per HME-L2 tile (rows realigned to position 0: 8-wide areas = 2 quads)
 #define HQ1 2 // position quads per HME-L1 tile (rows realigned to position 0: 8-wide areas = 2 quads)
 #define HQ16 2 // position quads per 1/16 tile (interior windows are dword aligned: 8/16/32 wide = 2/4/8 quads)
 
@@ -1365,7 +1365,10 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
 // block (LDS, rows 64 bytes apart) at HQ quads of position row y of a
 // full-resolution window (HME-L2): block rows 2g, 2g + 1 of lane g = lane & 15;
 // the 16 lanes of a row then sum their partial SADs (DPP) and every lane
-// returns the row's minimum key.
+// returns the row's minimum key. Rows are realigned to position 0 of the
+// window (a0 = its dword-aligned base, sh = its byte offset; v_alignbyte), so
+// an 8-wide area is 2 quads at any alignment: 32 qsads per block row instead
+// of the 48 of 3 unaligned quads, for 18 v_alignbyte.
 __device__ __forceinline__ unsigned long long hme_tile64(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                          int y, int kh2, const uint8_t (*src)[64]) {
     const int g = threadIdx.x & 15;
@@ -1381,6 +1384,9 @@ __device__ __forceinline__ unsigned long long hme_tile64(const uint8_t *a0, int 
             uint32_t d[20];
 #pragma unroll
             for (int v = 0; v < 5; v++) d[4 * v] = L[v].x, d[4 * v + 1] = L[v].y, d[4 * v + 2] = L[v].z, d[4 * v + 3] = L[v].w;
+            constexpr int ND = HQ + 16; // realigned dwords the qsad pairs read
+#pragma unroll
+            for (int j = 0; j < ND; j++) d[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], (uint32_t)sh);
 #pragma unroll
             for (int j4 = 0; j4 < 4; j4++) {
                 const uint4 sv = ((const uint4 *)src[k])[j4];
@@ -1403,8 +1409,8 @@ __device__ __forceinline__ unsigned long long hme_tile64(const uint8_t *a0, int 
         for (int e = 0; e < 4; e++) {
             // the row's 16 lanes: quad xor 1 / 2, row_half_mirror, row_mirror
             const uint32_t v = dpp_add<0x140>(dpp_add<0x141>(dpp_add<0x4E>(dpp_add<0xB1>(a[e]))));
-            const int x      = 4 * (q0 + qq) - sh + e;
-            if (x >= 0 && x < sa_w)
+            const int x      = 4 * (q0 + qq) + e;
+            if (x < sa_w)
                 mt = min_u32(mt, (v << 13) | (uint32_t)x);
         }
     }
@@ -4274,7 +4280,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                         e.sh              = (uint8_t)((uintptr_t)w0 & 3);
                         e.a0              = w0 - e.sh;
                         e.sa_w            = sw;
-                        e.ncols           = (int16_t)((((e.sh + sw + 3) >> 2) + HQ - 1) / HQ);
+                        e.ncols           = (int16_t)((((sw + 3) >> 2) + HQ - 1) / HQ); // realigned rows
                         e.ncm             = magic_u32((uint32_t)e.ncols);
                         e.id              = (uint8_t)lane;
                         items             = e.ncols * shh;
