@@ -934,9 +934,16 @@ static void pin_span(const void *p, uint64_t bytes, int slot) {
         G.n_regs++;
     } else
         G.n.unpinned++;
+    const double t1 = now_s();
     G.n.registrations++;
-    G.n.register_s += now_s() - t0;
+    G.n.register_s += t1 - t0;
     pthread_mutex_unlock(&G.reg);
+    if (G.trace_path) { /* (tf 3: a registration, beside the jobs and uploads it may hold up) */
+        const GlueTrace t = {0, 3, 0, 0, 0, t0, t0, t1, t1 - t0, 0, 0, 0, 0};
+        pthread_mutex_lock(&G.mu);
+        trace_add(&t);
+        pthread_mutex_unlock(&G.mu);
+    }
 }
 
 /* the span of the rows an upload of the w x h visible samples of `full` reads */

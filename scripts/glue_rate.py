@@ -35,21 +35,26 @@ def main():
         g = got["glue"]
         with open(trace) as fh:
             lines = [json.loads(line) for line in fh if line.strip()]
-        jobs = [t for t in lines if t["tf"] != 2]
+        jobs = [t for t in lines if t["tf"] < 2]
         ups = [t for t in lines if t["tf"] == 2]  # uploads (start create_ms, end done_ms)
+        regs = [t for t in lines if t["tf"] == 3]  # page-lockings of encoder buffers (hipHostRegister)
         w, h, frames, preset = E.CASES[case][:4]
         r = {"case": case, "size": f"{w}x{h}", "frames": frames, "preset": preset,
              "identical": got["md5"] == ref["md5"], "md5": got["md5"], "ref_seconds": ref["seconds"],
-             "gpu_encoder_seconds": got["seconds"], **g, "jobs": jobs, "uploads_trace": ups}
+             "gpu_encoder_seconds": got["seconds"], **g, "jobs": jobs, "uploads_trace": ups,
+             "registrations_trace": regs}
         lat = sorted(j["done_ms"] - j["create_ms"] for j in jobs)
         # jobs above 1 ms and the uploads that overlapped them (a stall's candidates)
         r["long_jobs"] = [{"pn": j["pn"], "tf": j["tf"], "ms": round(j["done_ms"] - j["create_ms"], 3),
                            "gpu_ms": j.get("gpu_ms"), "copy_ms": j.get("copy_ms"),
                            "uploads_overlapping": [u["pn"] for u in ups
-                                                   if u["create_ms"] < j["done_ms"] and u["done_ms"] > j["create_ms"]]}
+                                                   if u["create_ms"] < j["done_ms"] and u["done_ms"] > j["create_ms"]],
+                           "registrations_overlapping": [round(u["done_ms"] - u["create_ms"], 3) for u in regs
+                                                         if u["create_ms"] < j["done_ms"] and u["done_ms"] > j["create_ms"]]}
                           for j in jobs if j["done_ms"] - j["create_ms"] > 1.0]
         r["max_job_ms"] = round(lat[-1], 3)
-        print(json.dumps({k: v for k, v in r.items() if k not in ("jobs", "uploads_trace")}), flush=True)
+        print(json.dumps({k: v for k, v in r.items() if k not in ("jobs", "uploads_trace", "registrations_trace")}),
+              flush=True)
         print(f"  job latency ms: min {lat[0]:.3f} median {lat[len(lat) // 2]:.3f} max {lat[-1]:.3f}; "
               f"submit part median {sorted(j['submitted_ms'] - j['create_ms'] for j in jobs)[len(jobs) // 2]:.3f}",
               flush=True)
