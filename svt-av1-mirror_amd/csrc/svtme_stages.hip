@@ -1361,21 +1361,21 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
     return ((unsigned long long)(mt >> 15) << 32) | ((unsigned long long)(uint32_t)y << 16) | (mt & 0x7FFFu);
 }
 
-// One sixteenth of the SADs of the 64 x kh2 (sub) full-resolution source
+// One eighth of the SADs of the 64 x kh2 (sub) full-resolution source
 // block (LDS, rows 64 bytes apart) at HQ quads of position row y of a
-// full-resolution window (HME-L2): block rows 2g, 2g + 1 of lane g = lane & 15;
-// the 16 lanes of a row then sum their partial SADs (DPP) and every lane
+// full-resolution window (HME-L2): block rows 4g .. 4g + 3 of lane g = lane & 7;
+// the 8 lanes of a row then sum their partial SADs (DPP) and every lane
 // returns the row's minimum key. Rows are realigned to position 0 of the
 // window (a0 = its dword-aligned base, sh = its byte offset; v_alignbyte), so
 // an 8-wide area is 2 quads at any alignment: 32 qsads per block row instead
 // of the 48 of 3 unaligned quads, for 18 v_alignbyte.
 __device__ __forceinline__ unsigned long long hme_tile64(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
                                                          int y, int kh2, const uint8_t (*src)[64]) {
-    const int g = threadIdx.x & 15;
+    const int g = threadIdx.x & 7;
     unsigned long long acc[HQ] = {};
 #pragma unroll
-    for (int kk = 0; kk < 2; kk++) {
-        const int k = 2 * g + kk;
+    for (int kk = 0; kk < 4; kk++) {
+        const int k = 4 * g + kk;
         if (k < kh2) {
             const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)(y + 2 * k) * stride) + q0;
             u32x4a4 L[5];
@@ -1407,8 +1407,8 @@ __device__ __forceinline__ unsigned long long hme_tile64(const uint8_t *a0, int 
         qsad_unpack(acc[qq], a);
 #pragma unroll
         for (int e = 0; e < 4; e++) {
-            // the row's 16 lanes: quad xor 1 / 2, row_half_mirror, row_mirror
-            const uint32_t v = dpp_add<0x140>(dpp_add<0x141>(dpp_add<0x4E>(dpp_add<0xB1>(a[e]))));
+            // the row's 8 lanes: quad xor 1 / 2, row_half_mirror
+            const uint32_t v = dpp_add<0x141>(dpp_add<0x4E>(dpp_add<0xB1>(a[e])));
             const int x      = 4 * (q0 + qq) + e;
             if (x < sa_w)
                 mt = min_u32(mt, (v << 13) | (uint32_t)x);
@@ -4302,16 +4302,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         }
         __syncthreads();
         {
-            const int nlanes = 16 * sh.u.a.nitems1, nsrch = sh.u.a.nsrch1;
+            const int nlanes = 8 * sh.u.a.nitems1, nsrch = sh.u.a.nsrch1;
             const int pstride = dj.cur.lv[0].stride;
             const int kh2     = (int)(G.bh >> 1);
-            for (int it16 = tid; it16 < nlanes; it16 += 256) {
-                const int it    = it16 >> 4;
+            for (int it8 = tid; it8 < nlanes; it8 += 256) {
+                const int it    = it8 >> 3;
                 const HSrch1 &e = sh.u.a.s1[find_search(sh.u.a.s1, nsrch, it)];
                 const int local = it - e.item0;
                 const int y = mdiv(local, e.ncm), col = local - y * e.ncols;
                 const unsigned long long kk = hme_tile64(e.a0, pstride, HQ * col, e.sh, e.sa_w, y, kh2, sh.u.a.src1);
-                if ((it16 & 15) == 0 && kk != ~0ull)
+                if ((it8 & 7) == 0 && kk != ~0ull)
                     atomicMin(&sh.u.a.key1[e.id], kk);
             }
         }
