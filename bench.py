@@ -6,6 +6,14 @@ references (L0 distance 1, 2; L1 distance 1, 2) with the preset-8 controls of
 svt_aom_sig_deriv_me. Pyramids of the pictures and their references are
 resident in HBM before the timed region (the PA stage builds them once per
 picture). --workload picks another BASELINE config (svt-av1-mirror_amd/workloads.py).
+A step writes the whole output of svt_aom_motion_estimation_b64 for every SB
+(motion_estimation.c:3076-3153): the per-reference records (best MV + SAD of
+the 85 PUs, HME / zz state) AND the per-SB results (candidate arrays,
+me_distortion, distortions, GM flags: svtme_sb_result, :2520-3007), which is
+what cpu_baseline times. Consecutive steps rotate over distinct resident job
+sets (--job-sets, each with pictures and references of its own), so every step
+publishes a new job table and reads pyramids the previous steps did not: the
+steps' working set (1.8 GB at 4K) is far beyond the 256 MiB Infinity Cache.
 
 One step, on N GPUs (one process per GPU, torch.distributed over RCCL): 4 N
 pictures (the encoder keeps several look-ahead pictures' ME in flight; the
@@ -15,8 +23,8 @@ r searches chunk r of every picture in ONE launch (svtme_submit_batch_device),
 then each picture's chunks go to the rank that owns it (rank j owns pictures
 4j..4j+3: the process whose picture-level consumers read every SB of them) in
 one all_to_all_single per step over RCCL (device buffers, on a communication
-stream overlapped with the next step's ME): 4 (N-1)/N pictures' records per
-rank per step. --exchange allgather gives every rank every picture instead
+stream overlapped with the next step's ME): 4 (N-1)/N pictures' records and
+per-SB results per rank per step. --exchange allgather gives every rank every picture instead
 (SURVEY.md 8(e)'s all_gather_into_tensor; N x the bytes per rank, the 8K
 single-picture band split's exchange, and the fallback when the pictures of
 a step do not divide over the ranks). Per-GPU work is four pictures' worth of
@@ -131,8 +139,15 @@ def main():
     ap.add_argument("--no-single-picture", "--no-alt-mode", dest="no_alt", action="store_true",
                     help="skip the timing of the other picture count (batched / single picture)")
     ap.add_argument("--no-upload", action="store_true", help="skip the host-upload (PCIe-inclusive) timing")
-    ap.add_argument("--no-sb-results", action="store_true",
-                    help="skip the timing of the same steps with the per-SB results (candidates, distortions) written")
+    ap.add_argument("--no-records-only", action="store_true",
+                    help="skip the secondary timing of the same steps writing the records alone (no per-SB results)")
+    ap.add_argument("--records-only", action="store_true",
+                    help="the timed steps write the records alone (default: records + per-SB results, the whole "
+                         "output of svt_aom_motion_estimation_b64)")
+    ap.add_argument("--job-sets", type=int, default=0,
+                    help="distinct resident job sets the steps rotate over (each with its own pictures and "
+                         "references): every step publishes a new job table and reads pyramids the previous "
+                         "steps did not (default: max(2, 8 / N), 32 pictures' pyramids per rank)")
     ap.add_argument("--lanes", type=int, default=2, choices=(1, 2),
                     help="submission lanes the timed steps alternate over (svtme_submit_batch_device_lane); the "
                          "overlapped two-lane rate is reported beside the one-lane value")
@@ -190,19 +205,33 @@ def main():
     gpu = S.GpuME(local_rank)
     syn = S.Synth(Wd, Ht)
     offs = sorted(set((0,) + tuple(t - 8 for t in wl["l0"]) + tuple(t - 8 for t in wl["l1"])))
-    jobs = []
-    for p in range(max(P, P_alt)):
-        t0 = 8 + PICTURE_STRIDE * p
-        for o in offs:
-            t = t0 + o
-            gpu.upload(t, W.workload_frame(name, syn, t))
-        job = W.workload_job(name, base=PICTURE_STRIDE * p, sb_begin=begin, sb_count=count)
-        jobs.append(job)
+    PM = max(P, P_alt)
+    # NS distinct job sets, each PM pictures with references of their own (picture numbers = content
+    # times t = base + 8 + offset), all resident; step i submits set i % NS, so every step publishes
+    # its own job table and the steps' working set (NS x PM x 5 pyramids, 1.8 GB at 4K) is far
+    # larger than the 256 MiB Infinity Cache, as in an encode where each picture is searched once.
+    # Set 0's picture 0 is the workload's own job (base 0), the one the CPU baseline checks.
+    NS = args.job_sets or max(2, 8 // world)
+    sets = []
+    for si in range(NS):
+        js = []
+        for p in range(PM):
+            base = PICTURE_STRIDE * (si * PM + p)
+            for o in offs:
+                t = 8 + base + o
+                gpu.upload(t, W.workload_frame(name, syn, t))
+            js.append(W.workload_job(name, base=base, sb_begin=begin, sb_count=count))
+        sets.append(js)
+    jobs = sets[0]
     R = S.ref_slots(jobs[0])
     rec = S.REF_RECORD_DTYPE.itemsize
-    chunk_bytes = slots * R * rec
+    sbsz = S.SB_RESULT_DTYPE.itemsize
+    with_sb = jobs[0].me_type != S.ME_MCTF and not args.records_only  # TF-ME jobs have no per-SB results
+    # one picture's chunk: its records, then (PA-ME) its per-SB results; both go to the owner rank
+    rec_bytes = slots * R * rec
+    chunk_bytes = rec_bytes + (slots * sbsz if with_sb else 0)
+    chunk_bytes = (chunk_bytes + 255) & ~255
     dev = torch.device("cuda", local_rank)
-    PM = max(P, P_alt)
     local = [torch.zeros(PM * chunk_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
     # the owner exchange needs each step's pictures to divide over the ranks
     owner = world > 1 and args.exchange == "owner" and P % world == 0 and P_alt % world == 0
@@ -220,18 +249,22 @@ def main():
     LP = min(args.launch_pictures or MAX_BATCH, MAX_BATCH)
     nlaunch = [0]
 
-    def step(i, n_pic=P, nl=NL, lp=LP):
+    def step(i, n_pic=P, nl=NL, lp=LP, sb=None):
         b = i & 1
+        sb = with_sb if sb is None else sb
+        js = sets[i % NS]
         if used[b] and world > 1:
             for l in range(nl):
                 exts[l].wait_event(g_done[b])  # the gather of step i-2 has read local[b]
         lanes_used = set()
+        base = local[b].data_ptr()
         for g0 in range(0, n_pic, lp):  # at most SVTME_MAX_BATCH_JOBS jobs per launch
             g1 = min(n_pic, g0 + lp)
             lane = nlaunch[0] % nl  # two lanes: consecutive launches alternate, their kernels overlap on the GPU
             nlaunch[0] += 1
             lanes_used.add(lane)
-            gpu.submit_batch_device(jobs[g0:g1], [local[b].data_ptr() + p * chunk_bytes for p in range(g0, g1)],
+            gpu.submit_batch_device(js[g0:g1], [base + p * chunk_bytes for p in range(g0, g1)],
+                                    [base + p * chunk_bytes + rec_bytes for p in range(g0, g1)] if sb else None,
                                     lane=lane)
         if world > 1:
             for l in sorted(lanes_used):
@@ -297,35 +330,22 @@ def main():
             ta = torch.tensor([alt_ms], dtype=torch.float64, device=dev)
             dist.all_reduce(ta, op=dist.ReduceOp.MAX)
             alt_ms = float(ta.item())
-    # the same steps with the per-SB results written too (svtme_sb_result: candidate
-    # arrays, me_distortion, GM flags, motion_estimation.c:2520-3007), which the
-    # encoder's PA-ME consumer reads beside the records; `value` is the records alone
-    # (the north star's best MV + SAD per PU)
-    sb_ms = None
-    if not args.no_sb_results and jobs[0].me_type != S.ME_MCTF:
-        sbsz = S.SB_RESULT_DTYPE.itemsize
-        lsb = torch.zeros(P * count * sbsz, dtype=torch.uint8, device=dev)
-
-        def step_sb(i):
-            b = i & 1
-            for g0 in range(0, P, LP):
-                g1 = min(P, g0 + LP)
-                lane = nlaunch[0] % NL
-                nlaunch[0] += 1
-                gpu.submit_batch_device(jobs[g0:g1], [local[b].data_ptr() + p * chunk_bytes for p in range(g0, g1)],
-                                        [lsb.data_ptr() + p * count * sbsz for p in range(g0, g1)], lane=lane)
+    # secondary: the same steps writing the records alone (the north star's best MV + SAD per PU,
+    # without the candidate arrays / distortions / GM flags of svtme_sb_result)
+    ro_ms = None
+    if with_sb and not args.no_records_only:
         for i in range(args.warmup):
-            step_sb(i)
+            step(i, sb=False)
         fence()
         t0s = time.perf_counter()
         for i in range(args.steps):
-            step_sb(args.warmup + i)
+            step(args.warmup + i, sb=False)
         fence()
-        sb_ms = (time.perf_counter() - t0s) / args.steps * 1e3
+        ro_ms = (time.perf_counter() - t0s) / args.steps * 1e3
         if world > 1:
-            ts = torch.tensor([sb_ms], dtype=torch.float64, device=dev)
+            ts = torch.tensor([ro_ms], dtype=torch.float64, device=dev)
             dist.all_reduce(ts, op=dist.ReduceOp.MAX)
-            sb_ms = float(ts.item())
+            ro_ms = float(ts.item())
     # secondary: the same steps in steady state (the clocks ramp over the first ~25 ms of
     # load): 300 more untimed steps, then --steady-steps timed; never `value`
     steady = None
@@ -491,13 +511,19 @@ def main():
     if args.band_steps > 0:
         band = band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, args.band_steps, fence)
 
-    recs = None
-    if world == 1:
+    recs = sbres = None
+    if world == 1:  # the workload's own job (set 0, picture 0), as the timed steps run it, for the parity check
+        chk = torch.zeros(chunk_bytes, dtype=torch.uint8, device=dev)
+        gpu.submit_batch_device([sets[0][0]], [chk.data_ptr()], [chk.data_ptr() + rec_bytes] if with_sb else None,
+                                lane=0)
         gpu.sync()
-        recs = np.frombuffer(local[0][:chunk_bytes].cpu().numpy().tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n_sb, R)
+        raw = chk.cpu().numpy()
+        recs = np.frombuffer(raw[:n_sb * R * rec].tobytes(), dtype=S.REF_RECORD_DTYPE).reshape(n_sb, R)
+        if with_sb:
+            sbres = np.frombuffer(raw[rec_bytes:rec_bytes + n_sb * sbsz].tobytes(), dtype=S.SB_RESULT_DTYPE)
     cpu_baseline = parity = ref_absdiff = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu_baseline, parity, ref_absdiff = cpu_leg(S, W, name, recs, args.cpu_seconds)
+        cpu_baseline, parity, ref_absdiff = cpu_leg(S, W, name, recs, sbres, args.cpu_seconds)
     valu_sad = {"achieved_T_absdiff_s": round(sad_rate, 2), "peak": SAD_PEAK_T, "frac": round(sad_rate / SAD_PEAK_T, 4),
                 "absdiff_per_sb_ref": W.ABSDIFF_PER_SB_REF[wl["windows"]],
                 "note": "SURVEY.md 8(d) nominal absdiff (distance-1 windows, no early exit) per launch / pass time"}
@@ -526,7 +552,8 @@ def main():
             "unit": "SB/s",
             "n_gpus": world,
             "ranks": {"world_size_env": world, "process_group": dist.get_world_size() if dist else 1,
-                      "backend": (dist.get_backend() if dist else None),
+                      "backend": (dist.get_backend() if dist else "none (N = 1: no collective)"),
+                      "rccl_version": rccl_version(torch),
                       "devices": devices},
             "steps": args.steps,
             "warmup": args.warmup,
@@ -545,17 +572,19 @@ def main():
                                       f"rank r searches chunk r of all {P} pictures in {-(-P // LP)} launch(es) per step" +
                                       (f", launches of {min(LP, P)} picture(s) alternating the two submission lanes"
                                        if NL > 1 else "") +
-                                      (f", record exchange over RCCL: {exchange}" if world > 1 else "")},
+                                      (f", record exchange over {'RCCL' if dist.get_backend() == 'nccl' else dist.get_backend()}"
+                                       f": {exchange}" if world > 1 else "")},
             "overlapped": None if alt_ms is None else {
                 "pictures_per_step": P_alt, "lanes": 2, "ms_per_step": round(alt_ms, 4),
                 "value": round(n_sb * P_alt / (alt_ms * 1e-3), 1),
                 "algorithmic_hbm_gbps": round(bps * n_sb * P_alt / (alt_ms * 1e-3) / 1e9, 1),
                 "note": "one picture per GPU per step, consecutive steps alternating the two submission lanes "
                         "(svtme_submit_batch_device_lane): kernels of consecutive steps overlap, wall clock"},
-            "with_sb_results": None if sb_ms is None else {
-                "ms_per_step": round(sb_ms, 4), "value": round(n_sb * P / (sb_ms * 1e-3), 1),
-                "note": "the same steps writing the per-SB results too (svtme_sb_result: candidate arrays, "
-                        "me_distortion, GM flags) that the encoder's PA-ME consumer reads beside the records"},
+            "records_only": None if ro_ms is None else {
+                "ms_per_step": round(ro_ms, 4), "value": round(n_sb * P / (ro_ms * 1e-3), 1),
+                "sb_results_cost": round(ms_per_step / ro_ms - 1.0, 4),
+                "note": "the same steps writing the records alone (no svtme_sb_result); `value` writes both, the "
+                        "whole output of svt_aom_motion_estimation_b64 that cpu_baseline times"},
             "steady_state": steady,
             "upload": upload,
             "sb_ref_per_s": round(value * R, 1),
@@ -588,6 +617,15 @@ def main():
     gpu.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def rccl_version(torch):
+    """The RCCL (torch.cuda.nccl) version this torch build links, as a string."""
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception as e:  # noqa: BLE001 (reported, not fatal)
+        return f"unavailable ({type(e).__name__})"
 
 
 def gather_devices(dist, local_rank, dev):
@@ -744,7 +782,7 @@ def band_8k_leg(gpu, S, W, D, dist, world, rank, dev, exts, comm, steps, fence):
                     "timed alone"}
 
 
-def cpu_leg(S, W, name, gpu_recs, cpu_seconds):
+def cpu_leg(S, W, name, gpu_recs, gpu_sbres, cpu_seconds):
     """The reference's own ME (motion_estimation.c + its AVX2 kernels, compiled
     from source into oracle/_ref) on this host, whole-picture passes of the same
     job; the C restatement (oracle) when oracle/_ref is absent."""
@@ -763,9 +801,10 @@ def cpu_leg(S, W, name, gpu_recs, cpu_seconds):
     job = W.workload_job(name)
     n_sb = S.sb_total(job.width, job.height)
     t0 = time.perf_counter()
-    recs, _ = S.run_checker(job, pyr[8], refs, checker, nthreads=threads, with_sb_results=False)
+    recs, sbr = S.run_checker(job, pyr[8], refs, checker, nthreads=threads, with_sb_results=gpu_sbres is not None)
     first = time.perf_counter() - t0
-    parity = not S.compare_records(recs, gpu_recs)
+    # records and (PA-ME) the per-SB results, byte for byte against the reference's
+    parity = not S.compare_records(recs, gpu_recs, sbr, gpu_sbres)
     # the absolute differences the reference's searches evaluate on this job (early exits and
     # pruning included), counted by the oracle's restatement of them: the real SAD work
     absdiff = None

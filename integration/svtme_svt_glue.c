@@ -150,6 +150,19 @@ static GlueEnc g_enc[GLUE_MAX_ENC];
 static pthread_mutex_t g_enc_mu = PTHREAD_MUTEX_INITIALIZER;
 static unsigned long long g_n_encoders, g_n_released; /* slots taken; pictures released at teardowns (g_enc_mu) */
 
+/* slots in use: GLUE_MAX_ENC, or fewer with SVTME_GLUE_MAX_ENC (tests: an encoder
+ * beyond the cap runs the encoder's own ME, and must not disturb the others) */
+static int enc_cap(void) {
+    static int cap;
+    int c = __atomic_load_n(&cap, __ATOMIC_ACQUIRE);
+    if (!c) {
+        const char *e = getenv("SVTME_GLUE_MAX_ENC");
+        c             = e && atoi(e) > 0 && atoi(e) < GLUE_MAX_ENC ? atoi(e) : GLUE_MAX_ENC;
+        __atomic_store_n(&cap, c, __ATOMIC_RELEASE);
+    }
+    return c;
+}
+
 /* the slot of an encoder, taken on first sight; -1 when every slot is taken */
 static int enc_slot(const void *enc_ctx, const void *pa_res, const void *pd_res) {
     if (!enc_ctx)
@@ -162,7 +175,7 @@ static int enc_slot(const void *enc_ctx, const void *pa_res, const void *pd_res)
     for (int i = 0; i < GLUE_MAX_ENC && k < 0; i++)
         if (g_enc[i].enc_ctx == enc_ctx)
             k = i;
-    for (int i = 0; i < GLUE_MAX_ENC && k < 0; i++)
+    for (int i = 0; i < enc_cap() && k < 0; i++)
         if (!g_enc[i].enc_ctx) {
             k = i;
             __atomic_store_n(&g_enc[i].enc_ctx, enc_ctx, __ATOMIC_RELEASE);
@@ -1174,7 +1187,12 @@ static EbPaReferenceObject *pa_object(const PictureParentControlSet *pcs) {
  * scaled pictures) only mark the resident copy out of date. */
 void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDesc *full) {
     pthread_once(&G.once, glue_init);
-    if (!G.ctx)
+    /* one slot lookup; an encoder without a slot (more than GLUE_MAX_ENC live) runs
+     * the encoder's own ME for every picture (svtme_motion_estimation_b64), so its
+     * pictures are never resident: nothing to pin, upload or mark stale, and its
+     * numbers must not alias slot 0's namespace */
+    const int slot = G.ctx ? pcs_slot(pcs) : -1;
+    if (slot < 0)
         return;
     const EbPictureBufferDesc *pa = pcs->pa_ref_pic_wrapper ? pa_object(pcs)->input_padded_pic : NULL;
     const int eager = G.eager && full && pa && full->buffer_y == pa->buffer_y && full->stride_y == pa->stride_y &&
@@ -1184,11 +1202,11 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
         if (G.pin) {
             uint64_t span;
             const uint8_t *y = span_of(pa, pcs->aligned_width, pcs->aligned_height, &span);
-            pin_span(y, span, pcs_slot(pcs));
+            pin_span(y, span, slot);
         }
         buf_prefill(pcs->aligned_width, pcs->aligned_height); /* (once; timed as prefill_ms) */
     }
-    const uint64_t pn = ns_pn(pcs_slot(pcs), pcs->picture_number);
+    const uint64_t pn = ns_pn(slot, pcs->picture_number);
     pthread_mutex_lock(&G.gpu);
     GluePic *p = pic_find(pn);
     if (p && !p->dirty) {

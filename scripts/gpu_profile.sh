@@ -10,10 +10,10 @@ export TMPDIR=/tmp
   cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo; } > $O/host.txt 2>&1
 timeout -k 10 300 python3 -u bench.py --workload $WL --steps 50 --warmup 10 ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err || { echo "bench failed"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/kt" -o run --output-format csv -- python3 bench.py --workload $WL --steps 50 --warmup 10 --no-cpu-baseline --no-single-picture --no-upload --no-sb-results --band-steps 0 --lanes 1 > $O/kt.log 2>&1 || { echo "rocprof kt failed"; tail -20 $O/kt.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/kt" -o run --output-format csv -- python3 bench.py --workload $WL --steps 50 --warmup 10 --no-cpu-baseline --no-single-picture --no-upload --no-records-only --band-steps 0 --lanes 1 > $O/kt.log 2>&1 || { echo "rocprof kt failed"; tail -20 $O/kt.log; exit 1; }
 run_pass() {
   name=$1; shift
-  timeout -s KILL 120 rocprofv3 --kernel-trace --kernel-include-regex "k_stage|k_hme|k_fp|k_l0|k_l1" --pmc "$@" -d "$GRAFT_REPO_ROOT/$O/pmc_$name" -o run --output-format csv -- python3 bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --no-single-picture --no-upload --no-sb-results --band-steps 0 --lanes 1 > $O/pmc_$name.log 2>&1 || { echo "pass $name failed $?"; tail -20 $O/pmc_$name.log; return 1; }
+  timeout -s KILL 120 rocprofv3 --kernel-trace --kernel-include-regex "k_stage|k_hme|k_fp|k_l0|k_l1" --pmc "$@" -d "$GRAFT_REPO_ROOT/$O/pmc_$name" -o run --output-format csv -- python3 bench.py --workload $WL --steps 5 --warmup 2 --no-cpu-baseline --no-single-picture --no-upload --no-records-only --band-steps 0 --lanes 1 > $O/pmc_$name.log 2>&1 || { echo "pass $name failed $?"; tail -20 $O/pmc_$name.log; return 1; }
 }
 run_pass sq1 SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU && \
 run_pass sq2 SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH && \

@@ -1072,60 +1072,13 @@ __device__ __forceinline__ SlotCentre final_centre(const svtme_job &job, const B
 // a v_min3 per position pair); the row, then the lane's best widen to the
 // 64-bit sad << 32 | y << 16 | x order of the reference's scan.
 // ----------------------------------------------------------------------------
-// Diagnostic build (-DSVTME_STAMPS, scripts/hme_stamps.py): thread 0 of every
-// k_hme workgroup records the shader clock at each phase boundary.
-#ifdef SVTME_STAMPS
-__device__ unsigned long long g_hme_stamps[1 << 17][16];
-// slots 0-7 shader clock per phase; 8 / 9 the 100 MHz real-time clock at the
-// first / latest stamp; 10 XCC_ID, 11 HW_ID (CU, SE) register values; 12-15
-// HW_ID of waves 0-3
-#define HME_STAMP(k)                                                                                                   \
-    do {                                                                                                               \
-        if (threadIdx.x == 0 && blockIdx.x < (1u << 17)) {                                                             \
-            g_hme_stamps[blockIdx.x][k] = __builtin_readcyclecounter();                                                \
-            g_hme_stamps[blockIdx.x][(k) == 0 ? 8 : 9] = __builtin_amdgcn_s_memrealtime();                             \
-            if ((k) == 0) {                                                                                            \
-                g_hme_stamps[blockIdx.x][10] = (unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11));                   \
-                g_hme_stamps[blockIdx.x][11] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));                    \
-            }                                                                                                          \
-        }                                                                                                              \
-        if ((k) == 0 && (threadIdx.x & 63) == 0 && blockIdx.x < (1u << 17))                                            \
-            g_hme_stamps[blockIdx.x][12 + (threadIdx.x >> 6)] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));   \
-    } while (0)
-#elif defined(SVTME_STOP_AFTER) // diagnostic build (scripts/gpu_phase_cost.sh): k_hme ends after that phase
-#define HME_STAMP(k)                                                                                                   \
-    do {                                                                                                               \
-        if ((k) == SVTME_STOP_AFTER)                                                                                   \
-            return;                                                                                                    \
-    } while (0)
-#elif defined(SVTME_CLOCKBINS) // diagnostic build (scripts/clock_probe.py): in-kernel clock over time
-// thread 0 of every k_hme workgroup adds its shader cycles (s_memtime) and its
-// 100 MHz real-time ticks (s_memrealtime) from start to end into the bin of its
-// start time (2^13 ticks = 81.92 us per bin, 4096 bins = 335 ms before wrapping):
-// cycles / ticks x 100 MHz is the clock the workgroups ran at in that bin
-__device__ unsigned long long g_clock_bins[4096][3];
-#define HME_STAMP(k)                                                                                                   \
-    do {                                                                                                               \
-        if (threadIdx.x == 0) {                                                                                        \
-            if ((k) == 0) {                                                                                            \
-                clk_c0 = __builtin_readcyclecounter();                                                                 \
-                clk_r0 = __builtin_amdgcn_s_memrealtime();                                                             \
-            } else if ((k) == 7) {                                                                                     \
-                const unsigned long long c1 = __builtin_readcyclecounter(), r1 = __builtin_amdgcn_s_memrealtime();     \
-                const int bin = (int)((clk_r0 >> 13) & 4095);                                                          \
-                atomicAdd(&g_clock_bins[bin][0], c1 - clk_c0);                                                         \
-                atomicAdd(&g_clock_bins[bin][1], r1 - clk_r0);                                                         \
-                atomicAdd(&g_clock_bins[bin][2], 1ull);                                                                \
-            }                                                                                                          \
-        }                                                                                                              \
-    } while (0)
-#else
+// Phase hooks of k_hme. The diagnostic builds (scripts/build_diag_lib.sh) force-
+// include csrc/diag/svtme_diag.h, which defines them (phase stamps, stop-after
+// builds, clock bins); the product build has none of that code.
+#ifndef HME_STAMP
 #define HME_STAMP(k)
 #endif
-// extra stop points of the SVTME_STOP_AFTER builds (no stamp slot)
-#if defined(SVTME_STOP_AFTER) && !defined(SVTME_STAMPS)
-#define HME_STOP(k) HME_STAMP(k)
-#else
+#ifndef HME_STOP
 #define HME_STOP(k)
 #endif
 
@@ -1214,24 +1167,6 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
 #pragma unroll
         for (int qq = 0; qq < HQ16; qq++) acc[t][qq] = 0;
     Row8 buf[3];
-#if defined(SVTME_DIAG_A1) && SVTME_DIAG_A1 == 1 // diagnostic: every lane reads the first lane's rows (broadcast loads)
-#define row8 row8_diag
-    auto row8_diag = [&](const uint8_t *, int st, int ro, int q) {
-        typedef __attribute__((address_space(1))) const u32x2a4 gu2;
-        const uint32_t *rp = (const uint32_t *)(uni_ptr(a0) + (ptrdiff_t)__builtin_amdgcn_readfirstlane(ro) * st) +
-                             __builtin_amdgcn_readfirstlane(q);
-        return Row8{ldg4(rp), *(gu2 *)(uintptr_t)(rp + 4)};
-    };
-#elif defined(SVTME_DIAG_A1) && SVTME_DIAG_A1 == 2 // diagnostic: no loads, rows synthesised in registers
-#define row8 row8_diag
-    auto row8_diag = [&](const uint8_t *, int, int ro, int q) {
-        const uint32_t x = (uint32_t)ro * 2654435761u + (uint32_t)q;
-        Row8 r;
-        r.lo = u32x4a4{x, x ^ 0x5A5A5A5Au, x + 0x01010101u, x >> 3};
-        r.hi = u32x2a4{x * 3u, x ^ 0x33333333u};
-        return r;
-    };
-#endif
     buf[0] = row8(a0, stride, min(yf, ylast), q0);
     buf[1] = row8(a0, stride, min(yf + 2, ylast), q0);
 #pragma unroll
@@ -1288,9 +1223,6 @@ __device__ __forceinline__ unsigned long long hme_tile16(const uint8_t *a0, int 
     }
     return best;
 }
-#ifdef row8
-#undef row8
-#endif
 
 // One quarter of the SADs of the 32 x kh1 (sub) quarter-resolution source
 // block (LDS, rows 32 bytes apart) at HQ1 quads of position row y of a 1/4
@@ -3944,9 +3876,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     const int kh  = (int)(G.bh >> 2) >> 1; // 1/16 block rows (sub)
     const int kh1 = (int)(G.bh >> 2);      // 1/4 block rows (sub): (bh / 2) / 2
     const bool zz_on = c.me_early_exit_th || c.me_safe_limit_zz_th;
-#ifdef SVTME_CLOCKBINS
-    unsigned long long clk_c0 = 0, clk_r0 = 0;
-#endif
     HME_STAMP(0);
 
     // ---- phase 0 (independent work of all waves):
@@ -4038,11 +3967,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                                             : !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th));
         const unsigned long long m = __ballot(nd);
         if (lane == 0)
-#ifdef SVTME_DIAG_NO_L1_PREHME // diagnostic (wrong results): no list-1 pre-HME search, the cost of those tiles
-            sh.u.a.need = (uint32_t)m & ~0x5500u;
-#else
             sh.u.a.need = (uint32_t)m;
-#endif
     }
     __syncthreads();
     HME_PRIO_LO();
@@ -4389,19 +4314,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     stage_e_body(sh.u.st, sh.csl, gj, sb_local, G, vmask, sh.cin, &sh.u.st.keys[0][0], false);
     HME_STAMP(7);
 }
-
-#ifdef SVTME_STAMPS
-extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks) {
-    if (nblocks > (1u << 17))
-        nblocks = 1u << 17;
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 16 * sizeof(unsigned long long));
-}
-#endif
-#ifdef SVTME_CLOCKBINS
-extern "C" int svtme_debug_clock_bins(unsigned long long *out) {
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_clock_bins), sizeof(g_clock_bins));
-}
-#endif
 
 } // namespace svtme
 

@@ -53,6 +53,24 @@ def test_two_encoders_in_one_process(case, workdir):
 
 
 @pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
+def test_encoder_beyond_slot_cap(workdir):
+    """More live encoders than the glue has slots (SVTME_GLUE_MAX_ENC=1 lowers the
+    cap of GLUE_MAX_ENC for the test): the second channel gets no slot, so it runs
+    the encoder's own ME for every SB and its pictures never become resident --
+    none pinned, uploaded or marked stale under the first encoder's picture
+    numbers (its re-decimations used to alias slot 0's namespace). Both
+    bitstreams equal the reference's, the first encoder's every job passes
+    SVTME_GLUE_VERIFY, and only the second's SBs fall back."""
+    case = "360p_p8_2ch"
+    ref = E.encode("ref", case, workdir)
+    one = E.encode("ora", case, workdir, {"SVTME_GLUE_MAX_ENC": "1"})
+    g = one["glue"]
+    assert one["md5"] == ref["md5"]
+    assert g["encoders"] == 1 and g["sbs"] > 0 and g["fallback_sbs"] > 0, g
+    assert g["verified_job_planes"] >= 3 * (g["pa_jobs"] + g["tf_jobs"]), g
+
+
+@pytest.mark.skipif(not (E.available("ref") and E.available("ora")), reason="encoders built by oracle/encoder.mk")
 @pytest.mark.parametrize("case", ["ra360_p12", "360p_p8_lowdelay", "240p_p8_ragged", "360p_p4"])
 def test_jobs_prefetched_at_picture_decision(case, workdir):
     """Every PA-ME job is submitted when picture decision posts the picture's ME
