@@ -10,10 +10,11 @@ A step writes the whole output of svt_aom_motion_estimation_b64 for every SB
 (motion_estimation.c:3076-3153): the per-reference records (best MV + SAD of
 the 85 PUs, HME / zz state) AND the per-SB results (candidate arrays,
 me_distortion, distortions, GM flags: svtme_sb_result, :2520-3007), which is
-what cpu_baseline times. Consecutive steps rotate over distinct resident job
-sets (--job-sets, each with pictures and references of its own), so every step
-publishes a new job table and reads pyramids the previous steps did not: the
-steps' working set (1.8 GB at 4K) is far beyond the 256 MiB Infinity Cache.
+what cpu_baseline times. The steps' pictures are consecutive pictures of one
+sequence (each the current picture once, the reference of its neighbours),
+all resident; consecutive steps take the next pictures (24 sets, --job-sets),
+so every step publishes a new job table and the pyramids the steps read
+(1.1 GB at 4K) are far beyond the 256 MiB Infinity Cache.
 
 One step, on N GPUs (one process per GPU, torch.distributed over RCCL): 4 N
 pictures (the encoder keeps several look-ahead pictures' ME in flight; the
@@ -77,7 +78,6 @@ STAGE_BYTES_P8 = {"k_stage_a": (2176, 6808), "k_stage_d": (0, 0), "k_stage_b": (
                   "k_stage_c1": (0, 4686), "k_stage_e": (0, 680), "k_hme": (2688, 12112)}
 # the whole pass in k_hme (fused full-pel + decode): every byte of the pass
 STAGE_BYTES_P8_ALL = (2688, 16798 + 680)
-PICTURE_STRIDE = 32  # picture p of a step pans from t = 8 + 32 p (distinct content per picture)
 PICTURES_PER_GPU = 4  # pictures of one step per GPU, one batched launch (--pictures overrides)
 MAX_BATCH = 16  # SVTME_MAX_BATCH_JOBS (include/svtme.h): jobs of one batched launch
 
@@ -145,9 +145,9 @@ def main():
                     help="the timed steps write the records alone (default: records + per-SB results, the whole "
                          "output of svt_aom_motion_estimation_b64)")
     ap.add_argument("--job-sets", type=int, default=0,
-                    help="distinct resident job sets the steps rotate over (each with its own pictures and "
-                         "references): every step publishes a new job table and reads pyramids the previous "
-                         "steps did not (default: max(2, 8 / N), 32 pictures' pyramids per rank)")
+                    help="job sets the steps rotate over: consecutive pictures of one sequence, each resident "
+                         "once (default 24: more than the 16 job tables the library keeps, so every step "
+                         "publishes its table)")
     ap.add_argument("--lanes", type=int, default=2, choices=(1, 2),
                     help="submission lanes the timed steps alternate over (svtme_submit_batch_device_lane); the "
                          "overlapped two-lane rate is reported beside the one-lane value")
@@ -206,22 +206,21 @@ def main():
     syn = S.Synth(Wd, Ht)
     offs = sorted(set((0,) + tuple(t - 8 for t in wl["l0"]) + tuple(t - 8 for t in wl["l1"])))
     PM = max(P, P_alt)
-    # NS distinct job sets, each PM pictures with references of their own (picture numbers = content
-    # times t = base + 8 + offset), all resident; step i submits set i % NS, so every step publishes
-    # its own job table and the steps' working set (NS x PM x 5 pyramids, 1.8 GB at 4K) is far
-    # larger than the 256 MiB Infinity Cache, as in an encode where each picture is searched once.
-    # Set 0's picture 0 is the workload's own job (base 0), the one the CPU baseline checks.
-    NS = args.job_sets or max(2, 8 // world)
-    sets = []
-    for si in range(NS):
-        js = []
-        for p in range(PM):
-            base = PICTURE_STRIDE * (si * PM + p)
-            for o in offs:
-                t = 8 + base + o
-                gpu.upload(t, W.workload_frame(name, syn, t))
-            js.append(W.workload_job(name, base=base, sb_begin=begin, sb_count=count))
-        sets.append(js)
+    # The pictures of the steps form one sequence, as an encoder's do: picture i (of NS x PM) is
+    # frame 8 + i searched against frames 8 + i -+ 1, 2 (picture numbers = content times, so the
+    # reference distances, and with them the search areas, are the workload's); consecutive
+    # pictures share references, every picture is resident once. Step k submits set k % NS, the
+    # pictures [PM (k % NS), PM (k % NS + 1)): with NS > 16 (the library's job-table ring) every
+    # step publishes a new job table, and the sequence's pyramids (1.1 GB at 4K) are far beyond
+    # the 256 MiB Infinity Cache. Picture 0 is the workload's own job (base 0), the one the CPU
+    # baseline checks.
+    NS = args.job_sets or 24
+    lo_t = 8 + min(offs)
+    hi_t = 8 + NS * PM - 1 + max(offs)
+    for t in range(lo_t, hi_t + 1):
+        gpu.upload(t, W.workload_frame(name, syn, t))
+    sets = [[W.workload_job(name, base=si * PM + p, sb_begin=begin, sb_count=count) for p in range(PM)]
+            for si in range(NS)]
     jobs = sets[0]
     R = S.ref_slots(jobs[0])
     rec = S.REF_RECORD_DTYPE.itemsize
@@ -347,26 +346,44 @@ def main():
             dist.all_reduce(ts, op=dist.ReduceOp.MAX)
             ro_ms = float(ts.item())
     # secondary: the same steps in steady state (the clocks ramp over the first ~25 ms of
-    # load): 300 more untimed steps, then --steady-steps timed; never `value`
+    # load): 300 more untimed steps, then --steady-steps timed in blocks that
+    # alternate the whole output and the records alone (their ratio: the cost of the per-SB
+    # results at equal clocks); never `value`
     steady = None
     if args.steady_steps > 0:
         for i in range(300):
             step(i)
         fence()
-        t0s = time.perf_counter()
-        for i in range(args.steady_steps):
-            step(300 + i)
-        fence()
-        st_ms = (time.perf_counter() - t0s) / args.steady_steps * 1e3
+        blk = max(1, args.steady_steps // 4)
+        t_sb = t_ro = 0.0
+        for r in range(4):
+            sb_blk = with_sb and r % 2 == 1  # records-only blocks first, the whole output second
+            fence()
+            t0s = time.perf_counter()
+            for i in range(blk):
+                step(300 + r * blk + i, sb=sb_blk)
+            fence()
+            dt = time.perf_counter() - t0s
+            if sb_blk or not with_sb:
+                t_sb += dt
+            else:
+                t_ro += dt
+        nb = 2 if with_sb else 4
+        st_ms = t_sb / (nb * blk) * 1e3
+        ro_st = t_ro / (2 * blk) * 1e3 if with_sb else None
         if world > 1:
-            ts = torch.tensor([st_ms], dtype=torch.float64, device=dev)
+            ts = torch.tensor([st_ms, ro_st or 0.0], dtype=torch.float64, device=dev)
             dist.all_reduce(ts, op=dist.ReduceOp.MAX)
-            st_ms = float(ts.item())
+            st_ms, ro_st = float(ts[0].item()), (float(ts[1].item()) if with_sb else None)
         steady = {"ms_per_step": round(st_ms, 4), "value": round(n_sb * P / (st_ms * 1e-3), 1),
-                  "untimed_steps_before": 300, "steps": args.steady_steps,
+                  "untimed_steps_before": 300, "steps": nb * blk,
+                  "records_only": None if ro_st is None else {
+                      "ms_per_step": round(ro_st, 4), "value": round(n_sb * P / (ro_st * 1e-3), 1),
+                      "sb_results_cost": round(st_ms / ro_st - 1.0, 4)},
                   "note": "the main line's steps after the GPU has been busy for ~60 ms (clocks ramped: in-kernel "
-                          "clock 2.24 -> 2.38 GHz over the first 12 ms of load, profiles/r05_warmup/); a "
-                          "secondary figure, `value` is the driver's window"}
+                          "clock 2.24 -> 2.38 GHz over the first 12 ms of load, profiles/r05_warmup/), in blocks "
+                          "alternating the whole output and the records alone; a secondary figure, `value` is "
+                          "the driver's window"}
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)

@@ -693,6 +693,7 @@ static struct {
         unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
         unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job, registrations;
         unsigned long long tf_batched, unused_jobs, launches, prefetched, prefetch_hits, prefetch_ready;
+        unsigned long long init_registrations; /* PA pool buffers page-locked at svt_av1_enc_init */
         double upload_s, submit_s, wait_s, job_s, busy_s, eager_s, prefill_s, register_s;
     } n;
 } G = {PTHREAD_ONCE_INIT, PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_MUTEX_INITIALIZER,
@@ -751,13 +752,14 @@ static void glue_stats_at_exit(void) {
             "\"eager_upload_ms\": %.3f, \"served_sb_per_s_with_uploads\": %.1f, \"prefill_ms\": %.3f, "
             "\"registrations\": %llu, \"register_ms\": %.3f, \"encoders\": %llu, \"released_at_teardown\": %llu, "
             "\"tf_batched\": %llu, \"unused_jobs\": %llu, \"launches\": %llu, \"prefetched\": %llu, "
-            "\"prefetch_hits\": %llu, \"prefetch_ready\": %llu}\n",
+            "\"prefetch_hits\": %llu, \"prefetch_ready\": %llu, \"init_registrations\": %llu}\n",
             G.ctx != NULL, G.n.pa_jobs, G.n.tf_jobs, G.n.sbs, G.n.fallback_sbs, G.n.uploads, G.n.invalidations,
             G.n.evictions, G.n.verified, G.n.verified_job, G.n.stale, G.n.unpinned, G.rtcd0[0] != NULL ? GLUE_RTCD_N : 0, changed, hip, G.n.job_sbs,
             G.n.max_inflight, 1e3 * G.n.upload_s, 1e3 * G.n.submit_s, 1e3 * G.n.wait_s,
             jobs ? 1e3 * G.n.job_s / (double)jobs : 0.0, 1e3 * G.n.busy_s, rate, G.n.eager_uploads, 1e3 * G.n.eager_s,
             rate_up, 1e3 * G.n.prefill_s, G.n.registrations, 1e3 * G.n.register_s, g_n_encoders, g_n_released,
-            G.n.tf_batched, G.n.unused_jobs, G.n.launches, G.n.prefetched, G.n.prefetch_hits, G.n.prefetch_ready);
+            G.n.tf_batched, G.n.unused_jobs, G.n.launches, G.n.prefetched, G.n.prefetch_hits, G.n.prefetch_ready,
+            G.n.init_registrations);
     fclose(f);
 }
 
@@ -1715,13 +1717,34 @@ static const void *handle_enc_ctx(const EbComponentType *c) {
                                                                   : NULL;
 }
 
-/* a new encoder: its slot, and the resource its picture analysis posts its results to */
+/* a new encoder: its slot, and the resource its picture analysis posts its results to.
+ * With page-locked uploads (SVTME_GLUE_PIN=1) every buffer of the encoder's PA
+ * reference pool (created by svt_av1_enc_init, enc_handle.c:1226-1300, 1727) is
+ * page-locked here, before the first picture: hipHostRegister takes 2-3 ms per 4K
+ * buffer and holds up the HIP calls of other threads while it runs, so locking
+ * them on first upload (the analysis threads, racing the first uploads and jobs)
+ * made the encode's first uploads wait milliseconds each. */
 EbErrorType __wrap_svt_av1_enc_init(EbComponentType *svt_enc_component) {
     const EbErrorType e = __real_svt_av1_enc_init(svt_enc_component);
     if (e == EB_ErrorNone) {
         const EbEncHandle *h = (const EbEncHandle *)svt_enc_component->p_component_private;
-        (void)enc_slot(handle_enc_ctx(svt_enc_component), h->picture_analysis_results_resource_ptr,
-                       h->picture_decision_results_resource_ptr);
+        const int slot       = enc_slot(handle_enc_ctx(svt_enc_component), h->picture_analysis_results_resource_ptr,
+                                        h->picture_decision_results_resource_ptr);
+        pthread_once(&G.once, glue_init);
+        const EbSystemResource *pool = h->pa_reference_picture_pool_ptr_array
+                                           ? h->pa_reference_picture_pool_ptr_array[0]
+                                           : NULL;
+        if (slot >= 0 && G.ctx && G.pin && G.eager && pool)
+            for (uint32_t i = 0; i < pool->object_total_count; i++) {
+                const EbPaReferenceObject *o = (const EbPaReferenceObject *)pool->wrapper_ptr_pool[i]->object_ptr;
+                const EbPictureBufferDesc *d = o ? o->input_padded_pic : NULL;
+                if (!d || !d->buffer_y || !d->max_width || !d->max_height)
+                    continue;
+                uint64_t span;
+                const uint8_t *y = span_of(d, d->max_width, d->max_height, &span);
+                pin_span(y, span, slot);
+                G.n.init_registrations++;
+            }
     }
     return e;
 }

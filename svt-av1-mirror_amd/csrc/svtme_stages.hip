@@ -1401,11 +1401,11 @@ struct StC {
     uint32_t nxm[16];
     int32_t nreq, nfp, k32, fp_items;
     FpRef fp[8];
-    unsigned long long keys[8][SVTME_PU_COUNT];
+    // the 85-PU argmin keys by slot; once decoded into rec, the svtme_sb_result image (finish_sb)
+    __attribute__((aligned(16))) unsigned long long keys[8][SVTME_PU_COUNT];
     // per slot, the image of its svtme_ref_record: best_sad [0, 85), best_mv [85, 170),
     // the tail [170, 176) (filled as the record is written): one 16-byte copy per lane
     __attribute__((aligned(16))) uint32_t rec[8][176];
-    uint32_t me_distortion[SVTME_PU_COUNT];
     uint8_t cand0[SVTME_PU_COUNT + 3];
     uint32_t gm_cnt[2][4][2][2];
     uint32_t wm[8]; // magic_u32 of each slot's full-pel width (key decode)
@@ -1591,232 +1591,252 @@ __device__ void fullpel(StC &st, const DevPlane &C, uint32_t ox, uint32_t oy) {
 }
 
 // Candidate arrays + distortions + GM detection for one SB, all threads
-// (motion_estimation.c:2532-3007). Thread n builds Z-order PU n.
+// (motion_estimation.c:2532-3007). Thread n builds Z-order PU n. The result is
+// assembled in an LDS image laid over st.keys (dead once the keys are decoded
+// into st.rec), then leaves in one pass of 16-byte stores: no zero fill of the
+// HBM copy, no scattered byte stores to HBM.
 __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
+    static_assert(sizeof(svtme_sb_result) % 4 == 0 && sizeof(svtme_sb_result) <= sizeof(st.keys) &&
+                      sizeof(st.keys) % 16 == 0, "svtme_sb_result image over st.keys");
+    constexpr int NDW = (int)(sizeof(svtme_sb_result) / 4);
     const svtme_job &job = dj.job;
     const int tid = threadIdx.x;
     const int nl = job.num_lists, nr0 = job.num_refs[0], nr1 = nl == 2 ? job.num_refs[1] : 0;
-    svtme_sb_result *o = dj.out_sb + sb_local;
-    uint32_t *ow = (uint32_t *)o; // zero the result (sizeof is a multiple of 4)
-    for (int i = tid; i < (int)(sizeof(svtme_sb_result) / 4); i += 256) ow[i] = 0;
+    uint32_t *img      = (uint32_t *)&st.keys[0][0];
+    svtme_sb_result *o = (svtme_sb_result *)img;
+    for (int i = tid; i < (NDW + 3) / 4; i += 256) ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    if (job.me_type == SVTME_ME_MCTF) // no candidates / distortions (motion_estimation.c:3126)
-        return;
-    const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
-    const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
-    if (mode != 2 && tid < npus)
-        o->total_me_candidate_index[tid] = 1; // memset(..., 1, number_of_pus)
-    __syncthreads();
-    if (tid < SVTME_PU_COUNT) {
-        const int n   = tid;
-        const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
-        if (mode == 0) { // construct_me_candidate_array_single_ref
-            const int pu         = c_z_to_raster[n];
-            st.me_distortion[pu] = st.rec[0][n];
-            st.cand0[pu]         = 0;
-            if (st.do_ref[0] && use) {
-                o->me_candidate_array[pu][0] = mk_cand(0, 0, 0, 0, 0);
-                o->me_mv_array[pu][0]        = st.rec[0][SVTME_PU_COUNT + n];
-            }
-        } else if (mode == 1) { // construct_me_candidate_array_mrp_off
-            const int pu        = c_z_to_raster[n];
-            uint32_t nlist      = nl;
-            const uint8_t org0  = st.do_ref[0], org1 = nl == 1 ? 0 : st.do_ref[4];
-            if (nlist < 2 || !st.do_ref[4])
-                nlist = 1;
-            const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
-            uint8_t off  = 0;
-            uint32_t blk = (org0 ? 1u : 0u) | (org1 ? 2u : 0u); // bit li
-            const uint32_t s0 = st.rec[0][n], s1 = st.rec[4][n];
-            const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
-            st.me_distortion[pu] = best;
-            int min_list         = -1;
-            if (job.ctrl.use_best_unipred_cand_only && (blk & 3u) == 3u)
-                min_list = s0 < s1 ? 0 : 1;
-            uint8_t c0 = 0;
-            for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
-                if (!((blk >> li) & 1u))
-                    continue;
-                if (prune_th > 0) {
-                    const uint32_t dd = (st.rec[li * 4][n] - best) * 100;
-                    if (dd > best * prune_th) {
-                        blk &= ~(1u << li);
-                        continue;
-                    }
+    if (job.me_type != SVTME_ME_MCTF) { // (MCTF: no candidates / distortions, motion_estimation.c:3126)
+        const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
+        const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
+        if (tid < SVTME_PU_COUNT) {
+            const int n   = tid;
+            const int pu  = c_z_to_raster[n]; // (a permutation: thread n owns PU pu's entries)
+            const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
+            if (mode != 2) // memset(total_me_candidate_index, 1, number_of_pus)
+                o->total_me_candidate_index[pu] = pu < npus ? 1 : 0;
+            if (mode == 0) { // construct_me_candidate_array_single_ref
+                o->me_distortion[pu] = st.rec[0][n];
+                st.cand0[pu]         = 0;
+                if (st.do_ref[0] && use) {
+                    o->me_candidate_array[pu][0] = mk_cand(0, 0, 0, 0, 0);
+                    o->me_mv_array[pu][0]        = st.rec[0][SVTME_PU_COUNT + n];
                 }
-                if (min_list != -1 && min_list != li) {
-                    if (use)
-                        o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
-                    continue;
-                }
-                if (use) {
-                    const uint8_t cb               = mk_cand(li, 0, 0, li == 0 ? li : 24, li == 1 ? li : 24);
-                    o->me_candidate_array[pu][off] = cb;
-                    if (off == 0)
-                        c0 = cb;
-                    o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
-                }
-                off++;
-            }
-            if ((blk & 3u) == 3u && use) {
-                const uint8_t cb               = mk_cand(2, 0, 0, 0, 1);
-                o->me_candidate_array[pu][off] = cb;
-                if (off == 0)
-                    c0 = cb;
-                o->total_me_candidate_index[pu] = (uint8_t)(off + 1);
-            }
-            st.cand0[pu] = c0;
-        } else { // construct_me_candidate_array
-            const int pu = (n > 4) ? c_z_to_raster[n] : n;
-            uint8_t off  = 0;
-            uint32_t blk = 0; // bit li * 4 + r
-            const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
-            uint32_t best = U32MAX;
-            for (int li = 0; li < nl; li++)
-                for (int r = 0; r < (li ? nr1 : nr0); r++) {
-                    if (!st.do_ref[li * 4 + r])
-                        continue;
-                    blk |= 1u << (li * 4 + r);
-                    best = min_u32(best, st.rec[li * 4 + r][n]);
-                }
-            st.me_distortion[pu] = best;
-            uint8_t c0 = 0;
-            for (int li = 0; li < nl && (use || off == 0); ++li)
-                for (int r = 0; r < (li ? nr1 : nr0) && (use || off == 0); ++r) {
-                    if (!((blk >> (li * 4 + r)) & 1u))
+            } else if (mode == 1) { // construct_me_candidate_array_mrp_off
+                uint32_t nlist     = nl;
+                const uint8_t org0 = st.do_ref[0], org1 = nl == 1 ? 0 : st.do_ref[4];
+                if (nlist < 2 || !st.do_ref[4])
+                    nlist = 1;
+                const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
+                uint8_t off  = 0;
+                uint32_t blk = (org0 ? 1u : 0u) | (org1 ? 2u : 0u); // bit li
+                const uint32_t s0 = st.rec[0][n], s1 = st.rec[4][n];
+                const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
+                o->me_distortion[pu] = best;
+                int min_list         = -1;
+                if (job.ctrl.use_best_unipred_cand_only && (blk & 3u) == 3u)
+                    min_list = s0 < s1 ? 0 : 1;
+                uint8_t c0 = 0;
+                for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
+                    if (!((blk >> li) & 1u))
                         continue;
                     if (prune_th > 0) {
-                        const uint32_t dd = (st.rec[li * 4 + r][n] - best) * 100;
+                        const uint32_t dd = (st.rec[li * 4][n] - best) * 100;
                         if (dd > best * prune_th) {
-                            blk &= ~(1u << (li * 4 + r));
+                            blk &= ~(1u << li);
                             continue;
                         }
                     }
+                    if (min_list != -1 && min_list != li) {
+                        if (use)
+                            o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
+                        continue;
+                    }
                     if (use) {
-                        const uint8_t cb               = mk_cand(li, r, r, li == 0 ? li : 24, li == 1 ? li : 24);
+                        const uint8_t cb               = mk_cand(li, 0, 0, li == 0 ? li : 24, li == 1 ? li : 24);
                         o->me_candidate_array[pu][off] = cb;
                         if (off == 0)
                             c0 = cb;
-                        o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.rec[li * 4 + r][SVTME_PU_COUNT + n];
+                        o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
                     }
                     off++;
                 }
-            if (nl == 2 && use) {
-                for (int a2 = 0; a2 < nr0; a2++)
-                    for (int b2 = 0; b2 < nr1; b2++) {
-                        if (job.only_l_bwd && (a2 > 0 || b2 > 0))
-                            continue;
-                        if (((blk >> a2) & 1u) && ((blk >> (4 + b2)) & 1u)) {
-                            const uint8_t cb = mk_cand(2, a2, b2, 0, 1);
-                            if (off == 0)
-                                c0 = cb;
-                            o->me_candidate_array[pu][off++] = cb;
-                        }
-                    }
-                if (!job.only_l_bwd)
-                    for (int a2 = 1; a2 < nr0; a2++)
-                        if ((blk & 1u) && ((blk >> a2) & 1u)) {
-                            const uint8_t cb = mk_cand(2, 0, a2, 0, 0);
-                            if (off == 0)
-                                c0 = cb;
-                            o->me_candidate_array[pu][off++] = cb;
-                        }
-                if (!job.only_l_bwd && nr1 == 3 && ((blk >> 4) & 1u) && ((blk >> 6) & 1u)) {
-                    const uint8_t cb = mk_cand(2, 0, 2, 1, 1);
+                if ((blk & 3u) == 3u && use) {
+                    const uint8_t cb               = mk_cand(2, 0, 0, 0, 1);
+                    o->me_candidate_array[pu][off] = cb;
                     if (off == 0)
                         c0 = cb;
-                    o->me_candidate_array[pu][off++] = cb;
+                    o->total_me_candidate_index[pu] = (uint8_t)(off + 1);
                 }
+                st.cand0[pu] = c0;
+            } else { // construct_me_candidate_array
+                uint8_t off  = 0;
+                uint32_t blk = 0; // bit li * 4 + r
+                const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
+                uint32_t best = U32MAX;
+                for (int li = 0; li < nl; li++)
+                    for (int r = 0; r < (li ? nr1 : nr0); r++) {
+                        if (!st.do_ref[li * 4 + r])
+                            continue;
+                        blk |= 1u << (li * 4 + r);
+                        best = min_u32(best, st.rec[li * 4 + r][n]);
+                    }
+                o->me_distortion[pu] = best;
+                uint8_t c0 = 0;
+                for (int li = 0; li < nl && (use || off == 0); ++li)
+                    for (int r = 0; r < (li ? nr1 : nr0) && (use || off == 0); ++r) {
+                        if (!((blk >> (li * 4 + r)) & 1u))
+                            continue;
+                        if (prune_th > 0) {
+                            const uint32_t dd = (st.rec[li * 4 + r][n] - best) * 100;
+                            if (dd > best * prune_th) {
+                                blk &= ~(1u << (li * 4 + r));
+                                continue;
+                            }
+                        }
+                        if (use) {
+                            const uint8_t cb               = mk_cand(li, r, r, li == 0 ? li : 24, li == 1 ? li : 24);
+                            o->me_candidate_array[pu][off] = cb;
+                            if (off == 0)
+                                c0 = cb;
+                            o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.rec[li * 4 + r][SVTME_PU_COUNT + n];
+                        }
+                        off++;
+                    }
+                if (nl == 2 && use) {
+                    for (int a2 = 0; a2 < nr0; a2++)
+                        for (int b2 = 0; b2 < nr1; b2++) {
+                            if (job.only_l_bwd && (a2 > 0 || b2 > 0))
+                                continue;
+                            if (((blk >> a2) & 1u) && ((blk >> (4 + b2)) & 1u)) {
+                                const uint8_t cb = mk_cand(2, a2, b2, 0, 1);
+                                if (off == 0)
+                                    c0 = cb;
+                                o->me_candidate_array[pu][off++] = cb;
+                            }
+                        }
+                    if (!job.only_l_bwd)
+                        for (int a2 = 1; a2 < nr0; a2++)
+                            if ((blk & 1u) && ((blk >> a2) & 1u)) {
+                                const uint8_t cb = mk_cand(2, 0, a2, 0, 0);
+                                if (off == 0)
+                                    c0 = cb;
+                                o->me_candidate_array[pu][off++] = cb;
+                            }
+                    if (!job.only_l_bwd && nr1 == 3 && ((blk >> 4) & 1u) && ((blk >> 6) & 1u)) {
+                        const uint8_t cb = mk_cand(2, 0, 2, 1, 1);
+                        if (off == 0)
+                            c0 = cb;
+                        o->me_candidate_array[pu][off++] = cb;
+                    }
+                }
+                if (use)
+                    o->total_me_candidate_index[pu] = off;
+                st.cand0[pu] = use ? c0 : 0;
             }
-            if (use)
-                o->total_me_candidate_index[pu] = off;
-            st.cand0[pu] = use ? c0 : 0;
+        }
+        __syncthreads();
+        // compute_distortion (motion_estimation.c:2964-3007): wave 0, lane-parallel sums
+        if (tid < 64) {
+            const int lane = tid;
+            const uint32_t d8v  = o->me_distortion[21 + lane];
+            const uint32_t d16v = lane < 16 ? o->me_distortion[5 + lane] : 0;
+            const uint32_t d32v = lane < 4 ? o->me_distortion[1 + lane] : 0;
+            const uint32_t d8 = wave_sum_u32(d8v), d16 = wave_sum_u32(d16v), d32 = wave_sum_u32(d32v);
+            const uint32_t d64 = o->me_distortion[0];
+            const uint64_t mean = d8 / 64;
+            const int64_t diff  = (int64_t)d8v - (int64_t)mean;
+            const uint64_t sq1  = (uint64_t)(diff * diff); // < 2^42: 24-bit limbs sum exactly in 32 bits
+            const uint64_t sq   = ((uint64_t)wave_sum_u32((uint32_t)(sq1 >> 24)) << 24) +
+                                (uint64_t)wave_sum_u32((uint32_t)(sq1 & 0xFFFFFFu));
+            if (lane == 0) {
+                o->me_8x8_cost_variance = (uint32_t)(sq / 64);
+                o->rc_me_distortion     = (job.input_resolution <= 2) ? d8 : d16;
+                const uint32_t pix      = bw * bh;
+                o->me_64x64_distortion  = (d64 * 4096u) / pix;
+                o->me_32x32_distortion  = (d32 * 4096u) / pix;
+                o->me_16x16_distortion  = (d16 * 4096u) / pix;
+                o->me_8x8_distortion    = (d8 * 4096u) / pix;
+            }
+        }
+        // perform_gm_detection (motion_estimation.c:2838-2961): wave 1 beside wave 0,
+        // one lane per block; the direction counters are LDS adds, the stationary
+        // count a ballot
+        if (job.gm_enabled && (tid >> 6) == 1) {
+            const int lane = tid & 63;
+            uint32_t *cntf = &st.gm_cnt[0][0][0][0];
+            if (lane < 32)
+                cntf[lane] = 0;
+            wave_lds_fence();
+            const bool low  = job.input_resolution <= 2;
+            const int n_blk = low ? 64 : 16;
+            bool stat       = false;
+            if (lane < n_blk) {
+                uint8_t n = (uint8_t)(low ? 21 + lane : 5 + lane);
+                if (low && !job.enable_me_8x8) {
+                    if (n >= 21)
+                        n = c_8x8_to_16x16[n - 21];
+                    if (!job.enable_me_16x16 && n >= 5)
+                        n = c_16x16_to_32x32[n - 5];
+                }
+                if (!low && !job.enable_me_16x16 && n >= 5)
+                    n = c_16x16_to_32x32[n - 5];
+                const uint8_t cb = st.cand0[n];
+                const int dir = cb & 3, r0 = (cb >> 2) & 3, r1 = (cb >> 4) & 3, l0 = (cb >> 6) & 1, l1 = (cb >> 7) & 1;
+                const int li = (dir == 0 || dir == 2) ? l0 : l1;
+                const int ri = (dir == 0 || dir == 2) ? r0 : r1;
+                int active_th;
+                if (low) {
+                    const uint64_t a2 = job.picture_number, b2 = st.refpic[li * 4 + ri];
+                    const uint16_t dist = (uint16_t)absi((int16_t)((a2 > b2 ? a2 : b2) - (a2 < b2 ? a2 : b2)));
+                    active_th = job.gm_use_distance_based_active_th ? max(dist >> 1, 4) : 4;
+                } else {
+                    const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - st.refpic[li * 4 + ri]));
+                    active_th = job.gm_use_distance_based_active_th ? max(dist * 16, 32) : 32;
+                }
+                const uint32_t mv = st.rec[li * 4 + ri][SVTME_PU_COUNT + n];
+                const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4;
+                uint32_t(*cnt)[4][2][2] = st.gm_cnt;
+                if (mx < -active_th)
+                    atomicAdd(&cnt[li][ri][0][0], 1u);
+                else if (mx > active_th)
+                    atomicAdd(&cnt[li][ri][0][1], 1u);
+                if (my < -active_th)
+                    atomicAdd(&cnt[li][ri][1][0], 1u);
+                else if (my > active_th)
+                    atomicAdd(&cnt[li][ri][1][1], 1u);
+                const int stt = low ? 0 : 4;
+                stat          = absi(mx) <= stt && absi(my) <= stt;
+            }
+            const uint64_t stationary = (uint64_t)__popcll(__ballot(stat)), tot = (uint64_t)n_blk;
+            wave_lds_fence();
+            const bool over = lane < 32 && cntf[lane] > (tot / 2);
+            const bool any  = __ballot(over) != 0ull;
+            if (lane == 0) {
+                if (stationary > ((tot * 5) / 100))
+                    o->stationary_block_present = 1;
+                if (any)
+                    o->rc_me_allow_gm = 1;
+            }
         }
     }
     __syncthreads();
-    if (tid < SVTME_PU_COUNT)
-        o->me_distortion[tid] = st.me_distortion[tid];
-    // compute_distortion (motion_estimation.c:2964-3007): wave 0, lane-parallel sums
-    if (tid < 64) {
-        const int lane = tid;
-        const uint32_t d8v  = st.me_distortion[21 + lane];
-        const uint32_t d16v = lane < 16 ? st.me_distortion[5 + lane] : 0;
-        const uint32_t d32v = lane < 4 ? st.me_distortion[1 + lane] : 0;
-        const uint32_t d8 = wave_sum_u32(d8v), d16 = wave_sum_u32(d16v), d32 = wave_sum_u32(d32v);
-        const uint32_t d64 = st.me_distortion[0];
-        const uint64_t mean = d8 / 64;
-        const int64_t diff  = (int64_t)d8v - (int64_t)mean;
-        const uint64_t sq1  = (uint64_t)(diff * diff); // < 2^42: 24-bit limbs sum exactly in 32 bits
-        const uint64_t sq   = ((uint64_t)wave_sum_u32((uint32_t)(sq1 >> 24)) << 24) +
-                            (uint64_t)wave_sum_u32((uint32_t)(sq1 & 0xFFFFFFu));
-        if (lane == 0) {
-            o->me_8x8_cost_variance = (uint32_t)(sq / 64);
-            o->rc_me_distortion     = (job.input_resolution <= 2) ? d8 : d16;
-            const uint32_t pix      = bw * bh;
-            o->me_64x64_distortion  = (d64 * 4096u) / pix;
-            o->me_32x32_distortion  = (d32 * 4096u) / pix;
-            o->me_16x16_distortion  = (d16 * 4096u) / pix;
-            o->me_8x8_distortion    = (d8 * 4096u) / pix;
-        }
+    // the image to HBM: the result is 4-byte aligned (sizeof 4796), so up to 3
+    // head dwords, then 16-byte stores, then the tail dwords
+    uint32_t *ow    = (uint32_t *)(dj.out_sb + sb_local);
+    const int head  = (int)((16u - ((uint32_t)(uintptr_t)ow & 15u)) & 15u) >> 2;
+    const int n16   = (NDW - head) >> 2;
+    const int tail0 = head + 4 * n16;
+    for (int i = tid; i < n16; i += 256) {
+        const uint32_t *v = img + head + 4 * i;
+        *(uint4 *)(ow + head + 4 * i) = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    // perform_gm_detection (motion_estimation.c:2838-2961): wave 0, one lane per
-    // block; the direction counters are LDS adds, the stationary count a ballot
-    if (job.gm_enabled && tid < 64) {
-        const int lane = tid;
-        uint32_t *cntf = &st.gm_cnt[0][0][0][0];
-        if (lane < 32)
-            cntf[lane] = 0;
-        wave_lds_fence();
-        const bool low  = job.input_resolution <= 2;
-        const int n_blk = low ? 64 : 16;
-        bool stat       = false;
-        if (lane < n_blk) {
-            uint8_t n = (uint8_t)(low ? 21 + lane : 5 + lane);
-            if (low && !job.enable_me_8x8) {
-                if (n >= 21)
-                    n = c_8x8_to_16x16[n - 21];
-                if (!job.enable_me_16x16 && n >= 5)
-                    n = c_16x16_to_32x32[n - 5];
-            }
-            if (!low && !job.enable_me_16x16 && n >= 5)
-                n = c_16x16_to_32x32[n - 5];
-            const uint8_t cb = st.cand0[n];
-            const int dir = cb & 3, r0 = (cb >> 2) & 3, r1 = (cb >> 4) & 3, l0 = (cb >> 6) & 1, l1 = (cb >> 7) & 1;
-            const int li = (dir == 0 || dir == 2) ? l0 : l1;
-            const int ri = (dir == 0 || dir == 2) ? r0 : r1;
-            int active_th;
-            if (low) {
-                const uint64_t a2 = job.picture_number, b2 = st.refpic[li * 4 + ri];
-                const uint16_t dist = (uint16_t)absi((int16_t)((a2 > b2 ? a2 : b2) - (a2 < b2 ? a2 : b2)));
-                active_th = job.gm_use_distance_based_active_th ? max(dist >> 1, 4) : 4;
-            } else {
-                const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - st.refpic[li * 4 + ri]));
-                active_th = job.gm_use_distance_based_active_th ? max(dist * 16, 32) : 32;
-            }
-            const uint32_t mv = st.rec[li * 4 + ri][SVTME_PU_COUNT + n];
-            const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4;
-            uint32_t(*cnt)[4][2][2] = st.gm_cnt;
-            if (mx < -active_th)
-                atomicAdd(&cnt[li][ri][0][0], 1u);
-            else if (mx > active_th)
-                atomicAdd(&cnt[li][ri][0][1], 1u);
-            if (my < -active_th)
-                atomicAdd(&cnt[li][ri][1][0], 1u);
-            else if (my > active_th)
-                atomicAdd(&cnt[li][ri][1][1], 1u);
-            const int stt = low ? 0 : 4;
-            stat          = absi(mx) <= stt && absi(my) <= stt;
-        }
-        const uint64_t stationary = (uint64_t)__popcll(__ballot(stat)), tot = (uint64_t)n_blk;
-        wave_lds_fence();
-        const bool over = lane < 32 && cntf[lane] > (tot / 2);
-        const bool any  = __ballot(over) != 0ull;
-        if (lane == 0) {
-            if (stationary > ((tot * 5) / 100))
-                o->stationary_block_present = 1;
-            if (any)
-                o->rc_me_allow_gm = 1;
-        }
+    if (tid >= 256 - 8) { // the last lanes of wave 3 (the 16-byte pass leaves them idle on its second round)
+        const int j = tid - (256 - 8); // head: j < head, tail: tail0 + (j - 4)
+        if (j < head)
+            ow[j] = img[j];
+        else if (j >= 4 && tail0 + (j - 4) < NDW)
+            ow[tail0 + (j - 4)] = img[tail0 + (j - 4)];
     }
 }
 
