@@ -296,6 +296,8 @@ svtme_status svtme_picture_upload_async(svtme_ctx *ctx, uint64_t picture_number,
  * SVTME_UPLOAD_SLOTS, each reused once its DMA has run), outside the context
  * lock, then the DMA and the pyramid build are queued as in
  * svtme_picture_upload_async; `y` may change as soon as the call returns.
+ * With more than SVTME_UPLOAD_SLOTS callers at once, a caller waits for a slot
+ * (released as soon as its rows are staged and its DMA queued).
  * Page-locking the caller's memory instead (svtme_host_register) makes it a
  * driver user-pointer mapping, which the kernel may invalidate at any time
  * (NUMA balancing, page migration, compaction); every invalidation evicts the

@@ -191,6 +191,7 @@ struct svtme_ctx {
     hipStream_t dstream = nullptr; // packed outputs to host memory, created on first use
     std::mutex mu;
     std::condition_variable retired; // a ticket was retired (svtme_ticket_wait)
+    std::condition_variable up_free; // a staging slot of svtme_picture_upload_copy_async was released
 };
 
 extern "C" uint32_t svtme_sb_total(uint32_t width, uint32_t height) {
@@ -696,19 +697,21 @@ extern "C" svtme_status svtme_picture_upload_copy_async(svtme_ctx *c, uint64_t p
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_upload_copy_async: bad arguments");
     svtme_ctx::UpSlot *u = nullptr;
     {
-        std::lock_guard<std::mutex> lk(c->mu);
+        std::unique_lock<std::mutex> lk(c->mu);
         HIP_TRY(hipSetDevice(c->device));
         const svtme_status us = ensure_ustream(c);
         if (us)
             return us;
-        for (int k = 0; k < SVTME_UPLOAD_SLOTS && !u; k++) {
-            svtme_ctx::UpSlot &x = c->up[(c->up_next + k) % SVTME_UPLOAD_SLOTS];
-            if (!x.busy)
-                u = &x;
-        }
-        if (!u)
-            return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "svtme_picture_upload_copy_async: %d uploads being staged",
-                        SVTME_UPLOAD_SLOTS);
+        // every slot being filled by other threads: wait for one (each is released
+        // once its rows are staged and its DMA queued, a bounded time)
+        c->up_free.wait(lk, [&] {
+            for (int k = 0; k < SVTME_UPLOAD_SLOTS && !u; k++) {
+                svtme_ctx::UpSlot &x = c->up[(c->up_next + k) % SVTME_UPLOAD_SLOTS];
+                if (!x.busy)
+                    u = &x;
+            }
+            return u != nullptr;
+        });
         c->up_next = (uint32_t)(u - c->up + 1) % SVTME_UPLOAD_SLOTS;
         u->busy    = true;
         if (!u->done)
@@ -730,16 +733,21 @@ extern "C" svtme_status svtme_picture_upload_copy_async(svtme_ctx *c, uint64_t p
     if (e != hipSuccess) {
         std::lock_guard<std::mutex> lk(c->mu);
         u->busy = false;
+        c->up_free.notify_all();
         return fail(SVTME_ERR_INSUFFICIENT_RESOURCES, "svtme_picture_upload_copy_async: staging: %s",
                     hipGetErrorString(e));
     }
     for (uint32_t r = 0; r < h; r++)
         memcpy((uint8_t *)u->h + (size_t)r * w, y + (size_t)r * stride, w);
     std::lock_guard<std::mutex> lk(c->mu);
-    struct Release { // the slot is free again however this returns
+    struct Release { // the slot is free again however this returns (c->mu held)
+        svtme_ctx *c;
         svtme_ctx::UpSlot *u;
-        ~Release() { u->busy = false; }
-    } rel{u};
+        ~Release() {
+            u->busy = false;
+            c->up_free.notify_all();
+        }
+    } rel{c, u};
     const bool resident = c->pics.count(pn) != 0;
     PicBuf *pb;
     svtme_status st;

@@ -18,10 +18,13 @@
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 // level 0: from the caller's picture (8-bit or 10-bit MSB), pad-to-8 + edge replicate.
-// One thread writes 4 bytes of the padded plane (margins included).
+// One thread writes 4 bytes of the padded plane (margins included). pad_only: src
+// is the plane's own interior (k_host_rows wrote it in place), so the dwords
+// wholly inside it are left alone and only the margins are written (src aliases
+// dst: no __restrict__).
 template <bool TEN_BIT>
-__global__ void __launch_bounds__(256) k_build_full(const void *__restrict__ src, uint32_t src_stride, int w, int h,
-                                                    DevPlane dst, int left, int top, int rows) {
+__global__ void __launch_bounds__(256) k_build_full(const void *src, uint32_t src_stride, int w, int h, DevPlane dst,
+                                                    int left, int top, int rows, int pad_only) {
     const int dw_per_row = dst.stride >> 2;
     const int idx        = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= dw_per_row * rows)
@@ -29,9 +32,12 @@ __global__ void __launch_bounds__(256) k_build_full(const void *__restrict__ src
     const int ry = idx / dw_per_row, rx4 = (idx - ry * dw_per_row) * 4;
     const int y  = clampi(ry - top, 0, h - 1);
     const int x0 = rx4 - left;
+    const bool in_x = x0 >= 0 && x0 + 3 < w;
+    if (pad_only && in_x && ry >= top && ry - top < h)
+        return;
     uint32_t v   = 0;
     const uint8_t *p8 = (const uint8_t *)src + (size_t)y * src_stride + x0;
-    if (!TEN_BIT && x0 >= 0 && x0 + 3 < w && ((uintptr_t)p8 & 3) == 0) {
+    if (!TEN_BIT && in_x && ((uintptr_t)p8 & 3) == 0) {
         v = *(const uint32_t *)p8; // interior: one dword (a plane read over PCIe moves a quarter of the requests)
     } else {
 #pragma unroll
@@ -123,12 +129,14 @@ extern "C" hipError_t svtme_launch_host_rows(const uint8_t *src, uint32_t src_st
 extern "C" hipError_t svtme_launch_build_full(const void *src, uint32_t src_stride, int w, int h, int ten_bit,
                                               DevPlane dst, int left, int top, int rows, hipStream_t s) {
     const int n = (dst.stride >> 2) * rows;
+    // in place (the interior already in the plane): margins only
+    const int pad_only = !ten_bit && (const uint8_t *)src == dst.base && src_stride == (uint32_t)dst.stride;
     if (ten_bit)
         hipLaunchKernelGGL(k_build_full<true>, dim3((n + 255) / 256), dim3(256), 0, s, src, src_stride, w, h, dst,
-                           left, top, rows);
+                           left, top, rows, 0);
     else
         hipLaunchKernelGGL(k_build_full<false>, dim3((n + 255) / 256), dim3(256), 0, s, src, src_stride, w, h, dst,
-                           left, top, rows);
+                           left, top, rows, pad_only);
     return hipGetLastError();
 }
 

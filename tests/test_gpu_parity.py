@@ -403,6 +403,41 @@ def test_picture_upload_async(svtme, gpu):
         gpu.release(pn)
 
 
+@pytest.mark.gpu
+def test_picture_upload_copy_async_many_threads(svtme, gpu):
+    """More concurrent svtme_picture_upload_copy_async callers than staging slots
+    (SVTME_UPLOAD_SLOTS = 4): 12 threads upload at once (ctypes drops the GIL in
+    the call), every call succeeds -- a caller waits for a free slot instead of
+    failing -- and every pyramid equals the reference's."""
+    import threading
+
+    S = svtme
+    w, h = 328, 200
+    syn = S.Synth(w, h)
+    ts = list(range(60, 72))
+    frames = {t: syn.frame(t) for t in ts}
+    errs, go = [], threading.Barrier(len(ts))
+
+    def up(t):
+        try:
+            go.wait()
+            gpu.upload_copy_async(7000 + t, frames[t])
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append((t, repr(e)))
+    th = [threading.Thread(target=up, args=(t,)) for t in ts]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    gpu.sync()
+    for t in ts:
+        p = S.build_host_pyramid(frames[t], "oracle")
+        for lv, name in enumerate(("full", "quarter", "sixteenth")):
+            assert np.array_equal(gpu.download(7000 + t, lv), getattr(p, name)), (t, name)
+        gpu.release(7000 + t)
+
+
 def test_picture_upload_copy_async_and_pool(svtme, gpu):
     """svtme_picture_upload_copy_async: the rows go through the library's own
     page-locked staging ring (the caller's buffer is never page-locked), so the
