@@ -1,7 +1,8 @@
 """Per-phase timing of k_hme from a diagnostic build (-DSVTME_STAMPS).
 
 Build (container):  bash scripts/build_diag_lib.sh stamp -DSVTME_STAMPS
-Run (GPU box):      python3 scripts/hme_stamps.py [workload] [pictures]
+Run (GPU box):      python3 scripts/hme_stamps.py [workload] [pictures] [records]
+                    (records: the records alone; default the whole output, as bench.py times it)
 
 Thread 0 of every k_hme workgroup stamps the shader clock at 7 points: start,
 after A0 (zz), after the A1 table, after A1 tiles, after D + L1 table, after
@@ -20,7 +21,8 @@ sys.path.insert(0, os.path.join(ROOT, "svt-av1-mirror_amd"))
 import svtme as S  # noqa: E402
 import workloads as W  # noqa: E402
 
-PHASES = ["A0 (job, zz, A1 table)", "zz decisions", "A1 tiles", "D + L1 table", "L1 (+L2) tiles", "centre + full-pel", "E (prune, records)"]
+PHASES = ["A0 (job, zz, A1 table)", "zz decisions", "A1 tiles", "D + L1 table", "L1 (+L2) tiles", "final centre",
+          "full-pel", "E (prune, records, SB results)"]
 
 
 def main():
@@ -41,12 +43,14 @@ def main():
 
     R = S.ref_slots(jobs[0])
     bufs = [torch.zeros(n_sb * R * S.REF_RECORD_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for _ in jobs]
+    sbb = None if (len(sys.argv) > 3 and sys.argv[3] == "records") else \
+        [torch.zeros(n_sb * S.SB_RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda") for _ in jobs]
     for _ in range(5):
-        gpu.submit_batch_device(jobs, [b.data_ptr() for b in bufs])
+        gpu.submit_batch_device(jobs, [b.data_ptr() for b in bufs], None if sbb is None else [b.data_ptr() for b in sbb])
     gpu.sync()
     lib = S.load_product()
     nb = n_sb * P
-    st = np.zeros((nb, 16), np.uint64)
+    st = np.zeros((nb, 20), np.uint64)
     fn = lib.svtme_debug_hme_stamps
     fn.argtypes = [C.c_void_p, C.c_uint32]
     fn.restype = C.c_int
@@ -55,9 +59,9 @@ def main():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{name}_x{P}.npy"), st)
     rt, ids, st_w = st[:, 8:10], st[:, 10:12], st[:, 12:16]
-    st = st[:, :8]
-    if not st[:, 7].any():  # HME-only build: the last stamp is 6
-        st = st[:, :7]
+    st = np.concatenate([st[:, :6], st[:, 16:17], st[:, 6:8]], axis=1)  # ... L1, centre, full-pel, E
+    if not st[:, 8].any():  # HME-only build: the last stamp is 6
+        st = st[:, :6]
     d = np.diff(st, axis=1)
     print(f"{name} x{P}: {nb} workgroups, per-WG total mean {np.mean(st[:, -1] - st[:, 0]):.0f} cycles "
           f"(stamps are per-XCD clocks: no launch span)")

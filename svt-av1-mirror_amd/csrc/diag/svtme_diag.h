@@ -15,10 +15,10 @@
 #include <stdint.h>
 
 #ifdef SVTME_STAMPS
-__device__ unsigned long long g_hme_stamps[1 << 17][16];
+__device__ unsigned long long g_hme_stamps[1 << 17][20];
 // slots 0-7 shader clock per phase; 8 / 9 the 100 MHz real-time clock at the
 // first / latest stamp; 10 XCC_ID, 11 HW_ID (CU, SE) register values; 12-15
-// HW_ID of waves 0-3
+// HW_ID of waves 0-3; 16 shader clock after the final search centre (HME_STOP(55))
 #define HME_STAMP(k)                                                                                                   \
     do {                                                                                                               \
         if (threadIdx.x == 0 && blockIdx.x < (1u << 17)) {                                                             \
@@ -32,10 +32,15 @@ __device__ unsigned long long g_hme_stamps[1 << 17][16];
         if ((k) == 0 && (threadIdx.x & 63) == 0 && blockIdx.x < (1u << 17))                                            \
             g_hme_stamps[blockIdx.x][12 + (threadIdx.x >> 6)] = (unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11));   \
     } while (0)
+#define HME_STOP(k)                                                                                                    \
+    do {                                                                                                               \
+        if ((k) == 55 && threadIdx.x == 0 && blockIdx.x < (1u << 17))                                                  \
+            g_hme_stamps[blockIdx.x][16] = __builtin_readcyclecounter();                                               \
+    } while (0)
 extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks) {
     if (nblocks > (1u << 17))
         nblocks = 1u << 17;
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 16 * sizeof(unsigned long long));
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 20 * sizeof(unsigned long long));
 }
 #elif defined(SVTME_STOP_AFTER)
 #define HME_STAMP(k)                                                                                                   \

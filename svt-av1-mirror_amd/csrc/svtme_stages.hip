@@ -1593,177 +1593,197 @@ __device__ void fullpel(StC &st, const DevPlane &C, uint32_t ox, uint32_t oy) {
 // Candidate arrays + distortions + GM detection for one SB, all threads
 // (motion_estimation.c:2532-3007). Thread n builds Z-order PU n. The result is
 // assembled in an LDS image laid over st.keys (dead once the keys are decoded
-// into st.rec), then leaves in one pass of 16-byte stores: no zero fill of the
-// HBM copy, no scattered byte stores to HBM.
+// into st.rec; stage_c_tail zeroes it beside the record stores). After one
+// barrier, waves 2-3 store the image up to me_distortion in 16-byte pieces while
+// wave 0 (compute_distortion) and wave 1 (GM detection) finish the last words
+// and store them themselves: no zero fill of the HBM copy, no scattered byte
+// stores to HBM, one barrier.
 __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
     static_assert(sizeof(svtme_sb_result) % 4 == 0 && sizeof(svtme_sb_result) <= sizeof(st.keys) &&
                       sizeof(st.keys) % 16 == 0, "svtme_sb_result image over st.keys");
-    constexpr int NDW = (int)(sizeof(svtme_sb_result) / 4);
+    static_assert(offsetof(svtme_sb_result, me_8x8_cost_variance) ==
+                          offsetof(svtme_sb_result, me_distortion) + 4 * SVTME_PU_COUNT &&
+                      offsetof(svtme_sb_result, stationary_block_present) ==
+                          offsetof(svtme_sb_result, me_8x8_cost_variance) + 24 &&
+                      sizeof(svtme_sb_result) == offsetof(svtme_sb_result, stationary_block_present) + 8,
+                  "svtme_sb_result tail: 6 distortion words, then the GM flag bytes and padding");
+    constexpr int NIMG = (int)(offsetof(svtme_sb_result, me_8x8_cost_variance) / 4); // words stored from the image
+    constexpr int WDIST = NIMG, WGM = NIMG + 6;                                         // tail words
     const svtme_job &job = dj.job;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     const int nl = job.num_lists, nr0 = job.num_refs[0], nr1 = nl == 2 ? job.num_refs[1] : 0;
+    const bool mctf = job.me_type == SVTME_ME_MCTF; // (no candidates / distortions, motion_estimation.c:3126)
     uint32_t *img      = (uint32_t *)&st.keys[0][0];
     svtme_sb_result *o = (svtme_sb_result *)img;
-    for (int i = tid; i < (NDW + 3) / 4; i += 256) ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    if (job.me_type != SVTME_ME_MCTF) { // (MCTF: no candidates / distortions, motion_estimation.c:3126)
+    uint32_t *ow       = (uint32_t *)(dj.out_sb + sb_local);
+    if (!mctf && tid < SVTME_PU_COUNT) {
         const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
         const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
-        if (tid < SVTME_PU_COUNT) {
-            const int n   = tid;
-            const int pu  = c_z_to_raster[n]; // (a permutation: thread n owns PU pu's entries)
-            const int use = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
-            if (mode != 2) // memset(total_me_candidate_index, 1, number_of_pus)
-                o->total_me_candidate_index[pu] = pu < npus ? 1 : 0;
-            if (mode == 0) { // construct_me_candidate_array_single_ref
-                o->me_distortion[pu] = st.rec[0][n];
-                st.cand0[pu]         = 0;
-                if (st.do_ref[0] && use) {
-                    o->me_candidate_array[pu][0] = mk_cand(0, 0, 0, 0, 0);
-                    o->me_mv_array[pu][0]        = st.rec[0][SVTME_PU_COUNT + n];
+        const int n    = tid;
+        const int pu   = c_z_to_raster[n]; // (a permutation: thread n owns PU pu's entries)
+        const int use  = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
+        if (mode != 2) // memset(total_me_candidate_index, 1, number_of_pus)
+            o->total_me_candidate_index[pu] = pu < npus ? 1 : 0;
+        if (mode == 0) { // construct_me_candidate_array_single_ref
+            o->me_distortion[pu] = st.rec[0][n];
+            st.cand0[pu]         = 0;
+            if (st.do_ref[0] && use) {
+                o->me_candidate_array[pu][0] = mk_cand(0, 0, 0, 0, 0);
+                o->me_mv_array[pu][0]        = st.rec[0][SVTME_PU_COUNT + n];
+            }
+        } else if (mode == 1) { // construct_me_candidate_array_mrp_off
+            uint32_t nlist     = nl;
+            const uint8_t org0 = st.do_ref[0], org1 = nl == 1 ? 0 : st.do_ref[4];
+            if (nlist < 2 || !st.do_ref[4])
+                nlist = 1;
+            const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
+            uint8_t off  = 0;
+            uint32_t blk = (org0 ? 1u : 0u) | (org1 ? 2u : 0u); // bit li
+            const uint32_t s0 = st.rec[0][n], s1 = st.rec[4][n];
+            const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
+            o->me_distortion[pu] = best;
+            int min_list         = -1;
+            if (job.ctrl.use_best_unipred_cand_only && (blk & 3u) == 3u)
+                min_list = s0 < s1 ? 0 : 1;
+            uint8_t c0 = 0;
+            for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
+                if (!((blk >> li) & 1u))
+                    continue;
+                if (prune_th > 0) {
+                    const uint32_t dd = (st.rec[li * 4][n] - best) * 100;
+                    if (dd > best * prune_th) {
+                        blk &= ~(1u << li);
+                        continue;
+                    }
                 }
-            } else if (mode == 1) { // construct_me_candidate_array_mrp_off
-                uint32_t nlist     = nl;
-                const uint8_t org0 = st.do_ref[0], org1 = nl == 1 ? 0 : st.do_ref[4];
-                if (nlist < 2 || !st.do_ref[4])
-                    nlist = 1;
-                const uint32_t prune_th = (org0 && org1) ? (uint32_t)job.ctrl.prune_me_candidates_th : 0;
-                uint8_t off  = 0;
-                uint32_t blk = (org0 ? 1u : 0u) | (org1 ? 2u : 0u); // bit li
-                const uint32_t s0 = st.rec[0][n], s1 = st.rec[4][n];
-                const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
-                o->me_distortion[pu] = best;
-                int min_list         = -1;
-                if (job.ctrl.use_best_unipred_cand_only && (blk & 3u) == 3u)
-                    min_list = s0 < s1 ? 0 : 1;
-                uint8_t c0 = 0;
-                for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
-                    if (!((blk >> li) & 1u))
-                        continue;
-                    if (prune_th > 0) {
-                        const uint32_t dd = (st.rec[li * 4][n] - best) * 100;
-                        if (dd > best * prune_th) {
-                            blk &= ~(1u << li);
-                            continue;
-                        }
-                    }
-                    if (min_list != -1 && min_list != li) {
-                        if (use)
-                            o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
-                        continue;
-                    }
-                    if (use) {
-                        const uint8_t cb               = mk_cand(li, 0, 0, li == 0 ? li : 24, li == 1 ? li : 24);
-                        o->me_candidate_array[pu][off] = cb;
-                        if (off == 0)
-                            c0 = cb;
+                if (min_list != -1 && min_list != li) {
+                    if (use)
                         o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
-                    }
-                    off++;
+                    continue;
                 }
-                if ((blk & 3u) == 3u && use) {
-                    const uint8_t cb               = mk_cand(2, 0, 0, 0, 1);
+                if (use) {
+                    const uint8_t cb               = mk_cand(li, 0, 0, li == 0 ? li : 24, li == 1 ? li : 24);
                     o->me_candidate_array[pu][off] = cb;
                     if (off == 0)
                         c0 = cb;
-                    o->total_me_candidate_index[pu] = (uint8_t)(off + 1);
+                    o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
                 }
-                st.cand0[pu] = c0;
-            } else { // construct_me_candidate_array
-                uint8_t off  = 0;
-                uint32_t blk = 0; // bit li * 4 + r
-                const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
-                uint32_t best = U32MAX;
-                for (int li = 0; li < nl; li++)
-                    for (int r = 0; r < (li ? nr1 : nr0); r++) {
-                        if (!st.do_ref[li * 4 + r])
-                            continue;
-                        blk |= 1u << (li * 4 + r);
-                        best = min_u32(best, st.rec[li * 4 + r][n]);
+                off++;
+            }
+            if ((blk & 3u) == 3u && use) {
+                const uint8_t cb               = mk_cand(2, 0, 0, 0, 1);
+                o->me_candidate_array[pu][off] = cb;
+                if (off == 0)
+                    c0 = cb;
+                o->total_me_candidate_index[pu] = (uint8_t)(off + 1);
+            }
+            st.cand0[pu] = c0;
+        } else { // construct_me_candidate_array (:2532-2835), the slots' SADs in registers
+            // slot s = li * 4 + r searched (do_ref) for r < nr[li]; the best SAD over them
+            // (a slot without do_ref takes no part)
+            static_assert(offsetof(StC, do_ref) % 4 == 0, "StC::do_ref: two dword reads");
+            const uint32_t dr0 = ((const uint32_t *)st.do_ref)[0], dr1 = ((const uint32_t *)st.do_ref)[1];
+            uint32_t sad[8], blk = 0, best = U32MAX;
+#pragma unroll
+            for (int s2 = 0; s2 < 8; s2++) {
+                const int r = s2 & 3;
+                const bool in = (s2 < 4 ? r < nr0 : r < nr1) && (((s2 < 4 ? dr0 : dr1) >> (8 * r)) & 0xFFu);
+                sad[s2]       = in ? st.rec[s2][n] : U32MAX;
+                blk |= in ? 1u << s2 : 0u;
+                best = min_u32(best, sad[s2]);
+            }
+            o->me_distortion[pu] = best;
+            // pruning of the unipred candidates (each against the best alone)
+            const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
+            if (prune_th > 0) {
+#pragma unroll
+                for (int s2 = 0; s2 < 8; s2++)
+                    if (((blk >> s2) & 1u) && (sad[s2] - best) * 100 > best * prune_th)
+                        blk &= ~(1u << s2);
+            }
+            // the first candidate (GM detection reads it; 0 for a PU without
+            // candidates), then, for a PU with candidates, the whole list: unipred in (list, ref) order with their MVs,
+            // bipred (L0 x L1), L0-L0 (0, a), L1-L1 (0, 2)
+            const int first = blk ? __builtin_ctz(blk) : -1;
+            st.cand0[pu]    = !use || first < 0 ? 0 : mk_cand(first >> 2, first & 3, first & 3, first < 4 ? 0 : 24,
+                                                              first < 4 ? 24 : 1);
+            if (use) {
+                uint8_t *ca = o->me_candidate_array[pu];
+                int off     = 0;
+#pragma unroll
+                for (int s2 = 0; s2 < 8; s2++)
+                    if ((blk >> s2) & 1u) {
+                        const int li = s2 >> 2, r = s2 & 3;
+                        ca[off++]    = mk_cand(li, r, r, li == 0 ? 0 : 24, li == 1 ? 1 : 24);
+                        o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.rec[s2][SVTME_PU_COUNT + n];
                     }
-                o->me_distortion[pu] = best;
-                uint8_t c0 = 0;
-                for (int li = 0; li < nl && (use || off == 0); ++li)
-                    for (int r = 0; r < (li ? nr1 : nr0) && (use || off == 0); ++r) {
-                        if (!((blk >> (li * 4 + r)) & 1u))
-                            continue;
-                        if (prune_th > 0) {
-                            const uint32_t dd = (st.rec[li * 4 + r][n] - best) * 100;
-                            if (dd > best * prune_th) {
-                                blk &= ~(1u << (li * 4 + r));
-                                continue;
-                            }
-                        }
-                        if (use) {
-                            const uint8_t cb               = mk_cand(li, r, r, li == 0 ? li : 24, li == 1 ? li : 24);
-                            o->me_candidate_array[pu][off] = cb;
-                            if (off == 0)
-                                c0 = cb;
-                            o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.rec[li * 4 + r][SVTME_PU_COUNT + n];
-                        }
-                        off++;
-                    }
-                if (nl == 2 && use) {
+                if (nl == 2) {
                     for (int a2 = 0; a2 < nr0; a2++)
-                        for (int b2 = 0; b2 < nr1; b2++) {
-                            if (job.only_l_bwd && (a2 > 0 || b2 > 0))
-                                continue;
-                            if (((blk >> a2) & 1u) && ((blk >> (4 + b2)) & 1u)) {
-                                const uint8_t cb = mk_cand(2, a2, b2, 0, 1);
-                                if (off == 0)
-                                    c0 = cb;
-                                o->me_candidate_array[pu][off++] = cb;
-                            }
-                        }
-                    if (!job.only_l_bwd)
+                        for (int b2 = 0; b2 < nr1; b2++)
+                            if ((!job.only_l_bwd || (a2 == 0 && b2 == 0)) && ((blk >> a2) & 1u) &&
+                                ((blk >> (4 + b2)) & 1u))
+                                ca[off++] = mk_cand(2, a2, b2, 0, 1);
+                    if (!job.only_l_bwd) {
                         for (int a2 = 1; a2 < nr0; a2++)
-                            if ((blk & 1u) && ((blk >> a2) & 1u)) {
-                                const uint8_t cb = mk_cand(2, 0, a2, 0, 0);
-                                if (off == 0)
-                                    c0 = cb;
-                                o->me_candidate_array[pu][off++] = cb;
-                            }
-                    if (!job.only_l_bwd && nr1 == 3 && ((blk >> 4) & 1u) && ((blk >> 6) & 1u)) {
-                        const uint8_t cb = mk_cand(2, 0, 2, 1, 1);
-                        if (off == 0)
-                            c0 = cb;
-                        o->me_candidate_array[pu][off++] = cb;
+                            if ((blk & 1u) && ((blk >> a2) & 1u))
+                                ca[off++] = mk_cand(2, 0, a2, 0, 0);
+                        if (nr1 == 3 && ((blk >> 4) & 1u) && ((blk >> 6) & 1u))
+                            ca[off++] = mk_cand(2, 0, 2, 1, 1);
                     }
                 }
-                if (use)
-                    o->total_me_candidate_index[pu] = off;
-                st.cand0[pu] = use ? c0 : 0;
+                o->total_me_candidate_index[pu] = (uint8_t)off;
             }
         }
-        __syncthreads();
-        // compute_distortion (motion_estimation.c:2964-3007): wave 0, lane-parallel sums
-        if (tid < 64) {
-            const int lane = tid;
+    }
+    __syncthreads();
+    if (wid >= 2) {
+        // the image up to me_distortion: the result is 4-byte aligned (sizeof 4796),
+        // so up to 3 head words, 16-byte stores, up to 3 tail words
+        const int t     = tid - 128;
+        const int head  = (int)((16u - ((uint32_t)(uintptr_t)ow & 15u)) & 15u) >> 2;
+        const int n16   = (NIMG - head) >> 2;
+        const int tail0 = head + 4 * n16;
+        for (int i = t; i < n16; i += 128) {
+            const uint32_t *v = img + head + 4 * i;
+            *(uint4 *)(ow + head + 4 * i) = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        if (t >= 128 - 8) { // head: j < head, tail: tail0 + (j - 4)
+            const int j = t - (128 - 8);
+            if (j < head)
+                ow[j] = img[j];
+            else if (j >= 4 && tail0 + (j - 4) < NIMG)
+                ow[tail0 + (j - 4)] = img[tail0 + (j - 4)];
+        }
+    } else if (wid == 0) {
+        // compute_distortion (motion_estimation.c:2964-3007): lane-parallel sums; the 6 words to HBM
+        uint32_t w6 = 0;
+        if (!mctf) {
             const uint32_t d8v  = o->me_distortion[21 + lane];
             const uint32_t d16v = lane < 16 ? o->me_distortion[5 + lane] : 0;
             const uint32_t d32v = lane < 4 ? o->me_distortion[1 + lane] : 0;
             const uint32_t d8 = wave_sum_u32(d8v), d16 = wave_sum_u32(d16v), d32 = wave_sum_u32(d32v);
-            const uint32_t d64 = o->me_distortion[0];
+            const uint32_t d64  = o->me_distortion[0];
             const uint64_t mean = d8 / 64;
             const int64_t diff  = (int64_t)d8v - (int64_t)mean;
             const uint64_t sq1  = (uint64_t)(diff * diff); // < 2^42: 24-bit limbs sum exactly in 32 bits
             const uint64_t sq   = ((uint64_t)wave_sum_u32((uint32_t)(sq1 >> 24)) << 24) +
                                 (uint64_t)wave_sum_u32((uint32_t)(sq1 & 0xFFFFFFu));
-            if (lane == 0) {
-                o->me_8x8_cost_variance = (uint32_t)(sq / 64);
-                o->rc_me_distortion     = (job.input_resolution <= 2) ? d8 : d16;
-                const uint32_t pix      = bw * bh;
-                o->me_64x64_distortion  = (d64 * 4096u) / pix;
-                o->me_32x32_distortion  = (d32 * 4096u) / pix;
-                o->me_16x16_distortion  = (d16 * 4096u) / pix;
-                o->me_8x8_distortion    = (d8 * 4096u) / pix;
-            }
+            const uint32_t pix  = bw * bh;
+            w6 = lane == 0 ? (uint32_t)(sq / 64)                                     // me_8x8_cost_variance
+                 : lane == 1 ? ((job.input_resolution <= 2) ? d8 : d16)              // rc_me_distortion
+                 : lane == 2 ? (d64 * 4096u) / pix                                   // me_64x64_distortion
+                 : lane == 3 ? (d32 * 4096u) / pix                                   // me_32x32_distortion
+                 : lane == 4 ? (d16 * 4096u) / pix                                   // me_16x16_distortion
+                             : (d8 * 4096u) / pix;                                   // me_8x8_distortion
         }
-        // perform_gm_detection (motion_estimation.c:2838-2961): wave 1 beside wave 0,
-        // one lane per block; the direction counters are LDS adds, the stationary
-        // count a ballot
-        if (job.gm_enabled && (tid >> 6) == 1) {
-            const int lane = tid & 63;
+        if (lane < 6)
+            ow[WDIST + lane] = w6;
+    } else {
+        // perform_gm_detection (motion_estimation.c:2838-2961): one lane per block; the
+        // direction counters are LDS adds, the stationary count a ballot; the flag
+        // bytes (stationary_block_present, rc_me_allow_gm) and the padding to HBM
+        uint32_t flags = 0;
+        if (!mctf && job.gm_enabled) {
             uint32_t *cntf = &st.gm_cnt[0][0][0][0];
             if (lane < 32)
                 cntf[lane] = 0;
@@ -1812,31 +1832,10 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             wave_lds_fence();
             const bool over = lane < 32 && cntf[lane] > (tot / 2);
             const bool any  = __ballot(over) != 0ull;
-            if (lane == 0) {
-                if (stationary > ((tot * 5) / 100))
-                    o->stationary_block_present = 1;
-                if (any)
-                    o->rc_me_allow_gm = 1;
-            }
+            flags = (stationary > ((tot * 5) / 100) ? 1u : 0u) | (any ? 1u << 8 : 0u);
         }
-    }
-    __syncthreads();
-    // the image to HBM: the result is 4-byte aligned (sizeof 4796), so up to 3
-    // head dwords, then 16-byte stores, then the tail dwords
-    uint32_t *ow    = (uint32_t *)(dj.out_sb + sb_local);
-    const int head  = (int)((16u - ((uint32_t)(uintptr_t)ow & 15u)) & 15u) >> 2;
-    const int n16   = (NDW - head) >> 2;
-    const int tail0 = head + 4 * n16;
-    for (int i = tid; i < n16; i += 256) {
-        const uint32_t *v = img + head + 4 * i;
-        *(uint4 *)(ow + head + 4 * i) = make_uint4(v[0], v[1], v[2], v[3]);
-    }
-    if (tid >= 256 - 8) { // the last lanes of wave 3 (the 16-byte pass leaves them idle on its second round)
-        const int j = tid - (256 - 8); // head: j < head, tail: tail0 + (j - 4)
-        if (j < head)
-            ow[j] = img[j];
-        else if (j >= 4 && tail0 + (j - 4) < NDW)
-            ow[tail0 + (j - 4)] = img[tail0 + (j - 4)];
+        if (lane < 2)
+            ow[WGM + lane] = lane == 0 ? flags : 0u;
     }
 }
 
@@ -1907,7 +1906,10 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
             ((uint4 *)(out + k))[q] = v;
         }
     }
-    if (dj.out_sb) {
+    if (dj.out_sb) { // the svtme_sb_result image (finish_sb) starts zeroed
+        uint32_t *img = (uint32_t *)&st.keys[0][0];
+        for (int i = tid; i < (int)(sizeof(svtme_sb_result) + 15) / 16; i += 256)
+            ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
         finish_sb(st, dj, sb_local, bw, bh);
     }
