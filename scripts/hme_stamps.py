@@ -59,6 +59,7 @@ def main():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{name}_x{P}.npy"), st)
     rt, ids, st_w = st[:, 8:10], st[:, 10:12], st[:, 12:16]
+    esub = st[:, [6, 17, 18, 19, 7]]  # stage E: decode + prune, records, image zero, SB results
     st = np.concatenate([st[:, :6], st[:, 16:17], st[:, 6:8]], axis=1)  # ... L1, centre, full-pel, E
     if not st[:, 8].any():  # HME-only build: the last stamp is 6
         st = st[:, :6]
@@ -68,6 +69,11 @@ def main():
     for k, ph in enumerate(PHASES[: d.shape[1]]):
         v = d[:, k]
         print(f"  {ph:14s} mean {v.mean():8.0f}  p50 {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}  max {v.max():8.0f}")
+    if esub[:, 1:].all():
+        de = np.diff(esub, axis=1)
+        for k, ph in enumerate(["E: decode + me_prune_ref", "E: records", "E: zero SB image", "E: SB results"]):
+            v = de[:, k]
+            print(f"    {ph:24s} mean {v.mean():8.0f}  p50 {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}")
     # the 100 MHz real-time clock is chip-wide: launch span, start / end spread
     t0 = rt[:, 0].min()
     s0, s1 = (rt[:, 0] - t0) * 10.0, (rt[:, 1] - t0) * 10.0  # ns

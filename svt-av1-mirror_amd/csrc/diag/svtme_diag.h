@@ -37,6 +37,12 @@ __device__ unsigned long long g_hme_stamps[1 << 17][20];
         if ((k) == 55 && threadIdx.x == 0 && blockIdx.x < (1u << 17))                                                  \
             g_hme_stamps[blockIdx.x][16] = __builtin_readcyclecounter();                                               \
     } while (0)
+// stage E's sub-phases (stage_c_tail): 17 after me_prune_ref, 18 after the records, 19 after the image zeroing
+#define HME_SUB(k)                                                                                                     \
+    do {                                                                                                               \
+        if (threadIdx.x == 0 && blockIdx.x < (1u << 17))                                                               \
+            g_hme_stamps[blockIdx.x][k] = __builtin_readcyclecounter();                                                \
+    } while (0)
 extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks) {
     if (nblocks > (1u << 17))
         nblocks = 1u << 17;

@@ -1081,6 +1081,9 @@ __device__ __forceinline__ SlotCentre final_centre(const svtme_job &job, const B
 #ifndef HME_STOP
 #define HME_STOP(k)
 #endif
+#ifndef HME_SUB
+#define HME_SUB(k)
+#endif
 
 #define HQ 2  // position quads per HME-L2 tile (rows realigned to position 0: 8-wide areas = 2 quads)
 #define HQ1 2 // position quads per HME-L1 tile (rows realigned to position 0: 8-wide areas = 2 quads)
@@ -1876,6 +1879,7 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
         }
     }
     __syncthreads();
+    HME_SUB(17);
 
     // ---- records (sb_count x R, slots in list-0-then-list-1 order): the LDS record
     // images, 44 16-byte pieces each (704 bytes), the tail words and the SADs of an
@@ -1906,11 +1910,13 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
             ((uint4 *)(out + k))[q] = v;
         }
     }
+    HME_SUB(18);
     if (dj.out_sb) { // the svtme_sb_result image (finish_sb) starts zeroed
         uint32_t *img = (uint32_t *)&st.keys[0][0];
         for (int i = tid; i < (int)(sizeof(svtme_sb_result) + 15) / 16; i += 256)
             ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
+        HME_SUB(19);
         finish_sb(st, dj, sb_local, bw, bh);
     }
 }
