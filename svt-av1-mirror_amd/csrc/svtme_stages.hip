@@ -1296,21 +1296,25 @@ __device__ __forceinline__ unsigned long long hme_tile32q(const uint8_t *a0, int
     return ((unsigned long long)(mt >> 15) << 32) | ((unsigned long long)(uint32_t)y << 16) | (mt & 0x7FFFu);
 }
 
+#define HL2_PITCH 96 // bytes per LDS row of HME-L2's full-resolution source block (64 used)
 // One eighth of the SADs of the 64 x kh2 (sub) full-resolution source
-// block (LDS, rows 64 bytes apart) at HQ quads of position row y of a
-// full-resolution window (HME-L2): block rows 4g .. 4g + 3 of lane g = lane & 7;
+// block (LDS, rows HL2_PITCH bytes apart) at HQ quads of position row y of a
+// full-resolution window (HME-L2): block rows g + 8j of lane g = lane & 7;
 // the 8 lanes of a row then sum their partial SADs (DPP) and every lane
 // returns the row's minimum key. Rows are realigned to position 0 of the
 // window (a0 = its dword-aligned base, sh = its byte offset; v_alignbyte), so
 // an 8-wide area is 2 quads at any alignment: 32 qsads per block row instead
 // of the 48 of 3 unaligned quads, for 18 v_alignbyte.
 __device__ __forceinline__ unsigned long long hme_tile64(const uint8_t *a0, int stride, int q0, int sh, int sa_w,
-                                                         int y, int kh2, const uint8_t (*src)[64]) {
+                                                         int y, int kh2, const uint8_t (*src)[HL2_PITCH]) {
     const int g = threadIdx.x & 7;
     unsigned long long acc[HQ] = {};
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) {
-        const int k = 4 * g + kk;
+        // block rows g, g + 8, g + 16, g + 24: the 8 rows a ds_read_b128 lane group reads at
+        // once are HL2_PITCH = 96 bytes (24 banks) apart, 8 disjoint 4-bank sets (rows 4g + kk,
+        // 64 bytes apart, all fell on the same 4 banks: 8-way conflicts)
+        const int k = g + 8 * kk;
         if (k < kh2) {
             const uint32_t *rp = (const uint32_t *)(a0 + (ptrdiff_t)(y + 2 * k) * stride) + q0;
             u32x4a4 L[5];
@@ -1393,6 +1397,7 @@ struct StC {
     uint64_t hme_sad[8];
     uint32_t zz[8];
     uint32_t reduce_div[8];
+    uint32_t sum8[8]; // per slot: the sum of its 64 8x8 best SADs (me_prune_ref), when stage_e_body made it
     int16_t sc_x[8], sc_y[8];
     uint8_t do_ref[8], searched[8], in_round[8];
     uint8_t tf_exit; // MCTF HME-only exit (motion_estimation.c:3109-3113)
@@ -1772,12 +1777,13 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             const uint64_t sq   = ((uint64_t)wave_sum_u32((uint32_t)(sq1 >> 24)) << 24) +
                                 (uint64_t)wave_sum_u32((uint32_t)(sq1 & 0xFFFFFFu));
             const uint32_t pix  = bw * bh;
-            w6 = lane == 0 ? (uint32_t)(sq / 64)                                     // me_8x8_cost_variance
-                 : lane == 1 ? ((job.input_resolution <= 2) ? d8 : d16)              // rc_me_distortion
-                 : lane == 2 ? (d64 * 4096u) / pix                                   // me_64x64_distortion
-                 : lane == 3 ? (d32 * 4096u) / pix                                   // me_32x32_distortion
-                 : lane == 4 ? (d16 * 4096u) / pix                                   // me_16x16_distortion
-                             : (d8 * 4096u) / pix;                                   // me_8x8_distortion
+            // (d * 4096) / pix in 32-bit arithmetic, one division per lane (a shift for a whole SB)
+            const uint32_t dd = lane == 2 ? d64 : lane == 3 ? d32 : lane == 4 ? d16 : d8;
+            const uint32_t x  = dd * 4096u;
+            const uint32_t nd = pix == 4096u ? x >> 12 : x / pix;
+            w6 = lane == 0 ? (uint32_t)(sq / 64)                        // me_8x8_cost_variance
+                 : lane == 1 ? ((job.input_resolution <= 2) ? d8 : d16) // rc_me_distortion
+                             : nd;                                      // me_{64x64,32x32,16x16,8x8}_distortion
         }
         if (lane < 6)
             ow[WDIST + lane] = w6;
@@ -1809,12 +1815,16 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                 const int li = (dir == 0 || dir == 2) ? l0 : l1;
                 const int ri = (dir == 0 || dir == 2) ? r0 : r1;
                 int active_th;
+                uint64_t rp = 0; // ref_picture_number[li][ri]: uniform loads, a per-lane select
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    rp = (li * 4 + ri == q) ? job.ref_picture_number[q >> 2][q & 3] : rp;
                 if (low) {
-                    const uint64_t a2 = job.picture_number, b2 = st.refpic[li * 4 + ri];
+                    const uint64_t a2 = job.picture_number, b2 = rp;
                     const uint16_t dist = (uint16_t)absi((int16_t)((a2 > b2 ? a2 : b2) - (a2 < b2 ? a2 : b2)));
                     active_th = job.gm_use_distance_based_active_th ? max(dist >> 1, 4) : 4;
                 } else {
-                    const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - st.refpic[li * 4 + ri]));
+                    const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - rp));
                     active_th = job.gm_use_distance_based_active_th ? max(dist * 16, 32) : 32;
                 }
                 const uint32_t mv = st.rec[li * 4 + ri][SVTME_PU_COUNT + n];
@@ -1845,6 +1855,8 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
 // me_prune_ref, the per-reference records and the candidate arrays /
 // distortions / GM detection of one SB from its searched best SADs and MVs
 // (motion_estimation.c:1522-1565, 2520-3007); all threads of the workgroup
+// SUMS: st.sum8 holds the 8x8 sums of the searched slots (stage_e_body made them)
+template <bool SUMS>
 __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh, uint32_t vmask) {
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
@@ -1856,12 +1868,17 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
         // the 64 8x8 best SADs of every searched slot, summed across the wave
         // (searched == do_ref outside MCTF: each SAD < 2^15, the sum fits 32 bits)
         uint32_t sum8 = 0;
-        for (int k = 0; k < 8; k++) {
-            if (!(slot_valid(vmask, k) && st.do_ref[k]))
-                continue; // wave-uniform
-            const uint32_t t = wave_sum_u32(st.rec[k][21 + lane]);
-            if (lane == k)
-                sum8 = t;
+        if (SUMS) {
+            if (s < 8)
+                sum8 = st.sum8[s];
+        } else {
+            for (int k = 0; k < 8; k++) {
+                if (!(slot_valid(vmask, k) && st.do_ref[k]))
+                    continue; // wave-uniform
+                const uint32_t t = wave_sum_u32(st.rec[k][21 + lane]);
+                if (lane == k)
+                    sum8 = t;
+            }
         }
         uint64_t v  = ~0ull;
         if (s < 8) {
@@ -2145,7 +2162,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             fullpel<SUB_ME>(st, C, ox, oy);
     }
 
-    stage_c_tail(st, dj, sb_local, bw, bh, vmask);
+    stage_c_tail<false>(st, dj, sb_local, bw, bh, vmask);
 }
 
 // ----------------------------------------------------------------------------
@@ -3623,71 +3640,76 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 // Per SB: decode the argmin keys kb[k][85] of the R records (slot state cin[k])
 // into best SAD / MV per PU (strict-< first minimum in search order), then
 // stage_c_tail; all threads of the workgroup. reset: leave kb at ~0 (banded
-// jobs merge into it with atomic min).
+// jobs merge into it with atomic min). Wavefront w decodes the records w, w + 4
+// whole (its lanes the 64 8x8 PUs, then 21 the larger ones) and sums the 8x8
+// best SADs of each for me_prune_ref on the way (st.sum8): no serial sums later.
 __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const DevJob &dj, uint32_t sb_local,
                                              const SbGeo &G, uint32_t vmask, const CSlot *cin,
                                              unsigned long long *kb, bool reset) {
     const svtme_job &job = dj.job;
-    const int tid        = threadIdx.x;
-    const int R          = (int)dj.R;
-    if (tid < 8) { // slot tid
-        st.pl[tid][0]  = dj.ref[tid >> 2][tid & 3].lv[0];
-        st.dist[tid]   = ref_dist_const(job, tid >> 2, tid & 3);
-        st.refpic[tid] = job.ref_picture_number[tid >> 2][tid & 3];
-    }
-    if (tid == 0)
-        st.tf_exit = 0;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const int R = (int)dj.R, nr0 = job.num_refs[0];
+    // the slot state in one pass: slot tid's record (k), or the defaults of a slot without one
     if (tid < 8) {
-        st.searched[tid] = 0;
-        st.do_ref[tid]   = 0;
-        st.hme_sad[tid]  = U32MAX;
-        st.zz[tid]       = U32MAX;
-        st.sc_x[tid] = st.sc_y[tid] = 0;
+        const int s    = tid;
+        const int k    = s < 4 ? s : nr0 + (s - 4);
+        const bool has = s < 4 ? s < nr0 : k < R;
+        CSlot v{};
+        if (has)
+            v = cin[k];
+        csl[s]         = v;
+        st.wm[s]       = has && v.searched ? magic_u32((uint32_t)max(1, (int)v.w)) : 0u;
+        st.hme_sad[s]  = has ? v.hme_sad : U32MAX;
+        st.zz[s]       = has ? v.zz : U32MAX;
+        st.sc_x[s]     = has ? v.sc_x : 0;
+        st.sc_y[s]     = has ? v.sc_y : 0;
+        st.searched[s] = has ? v.searched : 0;
+        st.do_ref[s]   = has ? v.do_ref : 0;
+        st.sum8[s]     = 0;
+        if (s == (nr0 > 0 ? 0 : 4)) // record 0's
+            st.tf_exit = has ? v.tf_exit : 0;
     }
     __syncthreads();
-    if (tid < R) {
-        const int s     = tid < job.num_refs[0] ? tid : 4 + (tid - job.num_refs[0]);
-        const CSlot v   = cin[tid];
-        csl[s]          = v;
-        st.wm[s]        = v.searched ? magic_u32((uint32_t)max(1, (int)v.w)) : 0u;
-        st.hme_sad[s]   = v.hme_sad;
-        st.zz[s]        = v.zz;
-        st.sc_x[s]      = v.sc_x;
-        st.sc_y[s]      = v.sc_y;
-        st.searched[s]  = v.searched;
-        st.do_ref[s]    = v.do_ref;
-        if (tid == 0)
-            st.tf_exit = v.tf_exit;
-    }
-    __syncthreads();
-    for (int e = tid; e < R * SVTME_PU_COUNT; e += 256) {
-        const int kk = e / SVTME_PU_COUNT, pu = e - kk * SVTME_PU_COUNT;
-        const int s  = kk < job.num_refs[0] ? kk : 4 + (kk - job.num_refs[0]);
-        uint32_t sad = U32MAX, mv = 0;
-        if (st.searched[s]) {
-            const unsigned long long key = kb[e];
-            if (reset)
-                kb[e] = ~0ull; // keys rest at ~0 for the next banded job
-            const CSlot &v   = csl[s];
-            const uint32_t o = (uint32_t)key;
-            sad              = (uint32_t)(key >> 32);
-            int16_t mx, my;
-            if (v.probe && o == 0) {
-                mx = v.xc;
-                my = v.yc;
-            } else { // p / w by multiply-high (p * w < 2^32)
-                const int p = (int)o - (int)v.probe;
-                const int q = mdiv(p, st.wm[s]);
-                my          = i16(v.yo + q);
-                mx          = i16(v.xo + (p - q * v.w));
+    for (int kk = wid; kk < R; kk += 4) {
+        const int s      = kk < nr0 ? kk : 4 + (kk - nr0);
+        const bool srch  = st.searched[s] != 0;
+        const CSlot &v   = csl[s];
+        auto decode = [&](int pu, uint32_t &sad, uint32_t &mv) {
+            sad = U32MAX, mv = 0;
+            if (srch) {
+                const size_t e                = (size_t)kk * SVTME_PU_COUNT + pu;
+                const unsigned long long key = kb[e];
+                if (reset)
+                    kb[e] = ~0ull; // keys rest at ~0 for the next banded job
+                const uint32_t o = (uint32_t)key;
+                sad              = (uint32_t)(key >> 32);
+                int16_t mx, my;
+                if (v.probe && o == 0) {
+                    mx = v.xc;
+                    my = v.yc;
+                } else { // p / w by multiply-high (p * w < 2^32)
+                    const int p = (int)o - (int)v.probe;
+                    const int q = mdiv(p, st.wm[s]);
+                    my          = i16(v.yo + q);
+                    mx          = i16(v.xo + (p - q * v.w));
+                }
+                mv = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
             }
-            mv = ((uint32_t)(uint16_t)my << 16) | (uint16_t)mx;
+            st.rec[s][pu]                  = sad;
+            st.rec[s][SVTME_PU_COUNT + pu] = mv;
+        };
+        uint32_t sad, mv;
+        decode(21 + lane, sad, mv); // the 8x8 PUs
+        if (srch) {                 // me_prune_ref's sum (searched == do_ref outside MCTF; < 2^21)
+            const uint32_t t = wave_sum_u32(sad);
+            if (lane == 0)
+                st.sum8[s] = t;
         }
-        st.rec[s][pu] = sad;
-        st.rec[s][SVTME_PU_COUNT + pu]  = mv;
+        if (lane < 21)
+            decode(lane, sad, mv); // 64x64, 32x32, 16x16
     }
     __syncthreads();
-    stage_c_tail(st, dj, sb_local, G.bw, G.bh, vmask);
+    stage_c_tail<true>(st, dj, sb_local, G.bw, G.bh, vmask);
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_e(const DevBatch B) {
@@ -3718,7 +3740,7 @@ struct HmeA { // state of phases A0 .. B
     int16_t hx[32], hy[32];
     uint64_t hsad[32];
     __attribute__((aligned(16))) uint8_t src4[16][32]; // quarter-resolution source, sub rows
-    __attribute__((aligned(16))) uint8_t src1[32][64]; // full-resolution source, sub rows (HME-L2)
+    __attribute__((aligned(16))) uint8_t src1[32][HL2_PITCH]; // full-resolution source, sub rows (HME-L2)
 };
 
 // A1 search table (wave 0): lane = slot * 6 + k, k < 2 pre-HME region k, else
