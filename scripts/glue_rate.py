@@ -53,6 +53,10 @@ def main():
                                                          if u["create_ms"] < j["done_ms"] and u["done_ms"] > j["create_ms"]]}
                           for j in jobs if j["done_ms"] - j["create_ms"] > 1.0]
         r["max_job_ms"] = round(lat[-1], 3)
+        ud = sorted(u["done_ms"] - u["create_ms"] for u in ups)  # each upload call on an analysis thread
+        if ud:
+            r["upload_call_ms"] = {"median": round(ud[len(ud) // 2], 4), "max": round(ud[-1], 3),
+                                   "mean": round(sum(ud) / len(ud), 4), "over_1ms": sum(d > 1.0 for d in ud)}
         print(json.dumps({k: v for k, v in r.items() if k not in ("jobs", "uploads_trace", "registrations_trace")}),
               flush=True)
         print(f"  job latency ms: min {lat[0]:.3f} median {lat[len(lat) // 2]:.3f} max {lat[-1]:.3f}; "

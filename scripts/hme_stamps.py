@@ -50,7 +50,7 @@ def main():
     gpu.sync()
     lib = S.load_product()
     nb = n_sb * P
-    st = np.zeros((nb, 20), np.uint64)
+    st = np.zeros((nb, 24), np.uint64)
     fn = lib.svtme_debug_hme_stamps
     fn.argtypes = [C.c_void_p, C.c_uint32]
     fn.restype = C.c_int
@@ -59,7 +59,7 @@ def main():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{name}_x{P}.npy"), st)
     rt, ids, st_w = st[:, 8:10], st[:, 10:12], st[:, 12:16]
-    esub = st[:, [6, 17, 18, 19, 7]]  # stage E: decode + prune, records, image zero, SB results
+    esub = st[:, [6, 17, 18, 19, 20, 21, 7]]  # stage E: decode + prune, records, image zero, SB results
     st = np.concatenate([st[:, :6], st[:, 16:17], st[:, 6:8]], axis=1)  # ... L1, centre, full-pel, E
     if not st[:, 8].any():  # HME-only build: the last stamp is 6
         st = st[:, :6]
@@ -71,7 +71,8 @@ def main():
         print(f"  {ph:14s} mean {v.mean():8.0f}  p50 {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}  max {v.max():8.0f}")
     if esub[:, 1:].all():
         de = np.diff(esub, axis=1)
-        for k, ph in enumerate(["E: decode + me_prune_ref", "E: records", "E: zero SB image", "E: SB results"]):
+        for k, ph in enumerate(["E: decode + me_prune_ref", "E: records", "E: zero SB image", "E: candidate arrays",
+                                "E: SB results out", "E: end"]):
             v = de[:, k]
             print(f"    {ph:24s} mean {v.mean():8.0f}  p50 {np.median(v):8.0f}  p90 {np.percentile(v, 90):8.0f}")
     # the 100 MHz real-time clock is chip-wide: launch span, start / end spread

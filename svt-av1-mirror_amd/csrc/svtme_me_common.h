@@ -269,6 +269,22 @@ __constant__ uint8_t c_8x8_to_16x16[64] = {5,  5,  6,  6,  7,  7,  8,  8,  5,  5
                                            17, 17, 18, 18, 19, 19, 20, 20, 17, 17, 18, 18, 19, 19, 20, 20};
 __constant__ uint8_t c_16x16_to_32x32[16] = {1, 1, 2, 2, 1, 1, 2, 2, 3, 3, 4, 4, 3, 3, 4, 4};
 
+// c_z_to_raster[n] computed (a per-lane index into __constant__ memory is a vector
+// memory load on the critical path): the 16x16 and 8x8 PUs in Z order are bit-
+// interleaved (x, y) grid positions, row-major in raster order
+__device__ __forceinline__ int z_to_raster(int n) {
+    if (n < 5)
+        return n;
+    if (n < 21) {
+        const int z = n - 5;
+        return 5 + (((z >> 3) & 1) * 2 + ((z >> 1) & 1)) * 4 + ((z >> 2) & 1) * 2 + (z & 1);
+    }
+    const int z = n - 21;
+    const int x = (z & 1) | ((z >> 1) & 2) | ((z >> 2) & 4);
+    const int y = ((z >> 1) & 1) | ((z >> 2) & 2) | ((z >> 3) & 4);
+    return 21 + y * 8 + x;
+}
+
 __device__ __forceinline__ uint8_t mk_cand(int dir, int r0, int r1, int l0, int l1) {
     return (uint8_t)((dir & 3) | ((r0 & 3) << 2) | ((r1 & 3) << 4) | ((l0 & 1) << 6) | ((l1 & 1) << 7));
 }

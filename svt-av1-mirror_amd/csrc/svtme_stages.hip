@@ -657,7 +657,8 @@ __device__ __forceinline__ void dec_zz(Dec &d, const svtme_job &job, const SbGeo
         const bool have = slot_valid(vmask, s) && tl_or_l0(job, s >> 2);
         if (have) {
             zz      = d.a[SVTME_A_ZZ + s].sad << 1;
-            zz      = (zz * 64 * 64) / (G.bw * G.bh);
+            const uint32_t pix = G.bw * G.bh; // (32-bit arithmetic as the reference's; a shift for a whole SB)
+            zz                 = pix == 4096u ? (zz * 64 * 64) >> 12 : (zz * 64 * 64) / pix;
             d.zz[s] = zz;
         }
         const uint32_t best = wave_min_u32(zz);
@@ -1628,7 +1629,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
         const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
         const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
         const int n    = tid;
-        const int pu   = c_z_to_raster[n]; // (a permutation: thread n owns PU pu's entries)
+        const int pu   = z_to_raster(n); // (a permutation: thread n owns PU pu's entries)
         const int use  = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
         if (mode != 2) // memset(total_me_candidate_index, 1, number_of_pus)
             o->total_me_candidate_index[pu] = pu < npus ? 1 : 0;
@@ -1744,6 +1745,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
         }
     }
     __syncthreads();
+    HME_SUB(20);
     if (wid >= 2) {
         // the image up to me_distortion: the result is 4-byte aligned (sizeof 4796),
         // so up to 3 head words, 16-byte stores, up to 3 tail words
@@ -1935,6 +1937,7 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
         __syncthreads();
         HME_SUB(19);
         finish_sb(st, dj, sb_local, bw, bh);
+        HME_SUB(21);
     }
 }
 
