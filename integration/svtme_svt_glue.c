@@ -840,6 +840,20 @@ static void buf_prefill(uint32_t w, uint32_t h) {
     pthread_mutex_unlock(&G.mu);
 }
 
+/* once per process: the upload stream created and one blocking upload of a small
+ * picture under a number no encoder uses (its first kernel launches load the
+ * library's code object), then released */
+static void glue_warm(void) {
+    static int done;
+    static uint8_t plane[64 * 64];
+    if (__atomic_exchange_n(&done, 1, __ATOMIC_ACQ_REL))
+        return;
+    const uint64_t pn = ~(uint64_t)0;
+    (void)svtme_upload_stream(G.ctx);
+    if (svtme_picture_upload(G.ctx, pn, plane, 64, 64, 64) == SVTME_OK)
+        (void)svtme_picture_release(G.ctx, pn);
+}
+
 static int buf_take(GlueJob *j, size_t need, size_t worst) {
     int best = -1;
     for (uint32_t i = 0; i < G.n_pool; i++)
@@ -926,6 +940,12 @@ static int verify_level(uint64_t pn, int level, const EbPictureBufferDesc *d) {
  * frees them. */
 static void pin_span(const void *p, uint64_t bytes, int slot) {
     pthread_mutex_lock(&G.reg);
+    for (uint32_t i = 0; i < G.n_regs; i++) // inside a range locked already (e.g. a whole buffer at encoder init)
+        if ((const uint8_t *)p >= (const uint8_t *)G.regs[i].p &&
+            (const uint8_t *)p + bytes <= (const uint8_t *)G.regs[i].p + G.regs[i].bytes) {
+            pthread_mutex_unlock(&G.reg);
+            return;
+        }
     for (uint32_t i = 0; i < G.n_regs; i++)
         if (G.regs[i].p == p) {
             if (G.regs[i].bytes >= bytes) {
@@ -1718,9 +1738,9 @@ static const void *handle_enc_ctx(const EbComponentType *c) {
 }
 
 /* a new encoder: its slot, and the resource its picture analysis posts its results to.
- * With page-locked uploads (SVTME_GLUE_PIN=1) every buffer of the encoder's PA
- * reference pool (created by svt_av1_enc_init, enc_handle.c:1226-1300, 1727) is
- * page-locked here, before the first picture: hipHostRegister takes 2-3 ms per 4K
+ * With page-locked uploads (SVTME_GLUE_PIN=1) every 8-bit luma buffer of the
+ * encoder's input pool (created by svt_av1_enc_init, enc_handle.c:1773-1787; the
+ * PA reference pictures point at them) is page-locked here, before the first picture: hipHostRegister takes 2-3 ms per 4K
  * buffer and holds up the HIP calls of other threads while it runs, so locking
  * them on first upload (the analysis threads, racing the first uploads and jobs)
  * made the encode's first uploads wait milliseconds each. */
@@ -1731,20 +1751,26 @@ EbErrorType __wrap_svt_av1_enc_init(EbComponentType *svt_enc_component) {
         const int slot       = enc_slot(handle_enc_ctx(svt_enc_component), h->picture_analysis_results_resource_ptr,
                                         h->picture_decision_results_resource_ptr);
         pthread_once(&G.once, glue_init);
-        const EbSystemResource *pool = h->pa_reference_picture_pool_ptr_array
-                                           ? h->pa_reference_picture_pool_ptr_array[0]
-                                           : NULL;
+        // the luma buffers the PA reference pictures read (resource_coordination_process.c:1118-1130
+        // points input_padded_pic->buffer_y at the input's y8b buffer), whole
+        const EbSystemResource *pool = h->input_y8b_buffer_resource_ptr;
         if (slot >= 0 && G.ctx && G.pin && G.eager && pool)
             for (uint32_t i = 0; i < pool->object_total_count; i++) {
-                const EbPaReferenceObject *o = (const EbPaReferenceObject *)pool->wrapper_ptr_pool[i]->object_ptr;
-                const EbPictureBufferDesc *d = o ? o->input_padded_pic : NULL;
-                if (!d || !d->buffer_y || !d->max_width || !d->max_height)
+                const EbBufferHeaderType *hd = (const EbBufferHeaderType *)pool->wrapper_ptr_pool[i]->object_ptr;
+                const EbPictureBufferDesc *d = hd ? (const EbPictureBufferDesc *)hd->p_buffer : NULL;
+                if (!d || !d->buffer_y || !d->luma_size)
                     continue;
-                uint64_t span;
-                const uint8_t *y = span_of(d, d->max_width, d->max_height, &span);
-                pin_span(y, span, slot);
+                pin_span(d->buffer_y, d->luma_size, slot);
                 G.n.init_registrations++;
             }
+        if (slot >= 0 && G.ctx && G.eager) {
+            /* the output pool, device scratch and first pictures' memory, sized for the
+             * encoder's pictures (pcs.c:1217 aligned_width = max_input_luma_width), and the
+             * upload stream and the library's kernels loaded: the first uploads pay none of it */
+            const SequenceControlSet *scs = h->scs_instance_array[0]->scs;
+            buf_prefill(scs->max_input_luma_width, scs->max_input_luma_height);
+            glue_warm();
+        }
     }
     return e;
 }

@@ -216,6 +216,7 @@ svtme_status svtme_picture_upload_copy_async(svtme_ctx *c, uint64_t pn, const ui
     return svtme_picture_upload(c, pn, y, stride, width, height);
 }
 
+void *svtme_upload_stream(svtme_ctx *c) { return c; } // (no streams here: a non-null handle)
 svtme_status svtme_reserve_pictures(svtme_ctx *c, uint32_t width, uint32_t height, uint32_t count) {
     return c && width && height && count <= 4096 ? SVTME_OK : SVTME_ERR_BAD_PARAMETER;
 }

@@ -4010,14 +4010,44 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     // ---- zz decisions; which searches the reference performs (wave 0)
     if (wid == 0) {
         HME_PRIO_HI();
-        if (lane < 8)
-            d.a[SVTME_A_ZZ + lane] = ARes{sh.u.a.zzacc[lane], 0, 0};
-        wave_lds_fence();
-        dec_zz(d, job, G, vmask);
-        const int s    = lane >> 1;
-        const bool act = lane < 16 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && d.do_ref[s];
-        const bool nd  = act && ((lane & 1) ? !(c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2))
-                                            : !(c.me_early_exit_th && d.zz[s] < c.me_early_exit_th));
+        // dec_zz's decisions (init_zz_sad, motion_estimation.c:2382-2437) with the state in
+        // registers, lane = slot: every input read in one batch, cross-lane values by
+        // readlane / ds_bpermute, one LDS write of the results (no LDS round trips)
+        const uint32_t eet = c.me_early_exit_th, slz = c.me_safe_limit_zz_th;
+        const uint32_t zth = c.zz_sad_th;
+        const uint32_t zpct = c.zz_sad_pct;
+        const int tli = job.temporal_layer_index, hl = job.hierarchical_levels, nl = job.num_lists;
+        const bool sbr = job.similar_brightness_refs != 0;
+        const uint32_t acc = sh.u.a.zzacc[lane & 7];
+        const bool have    = slot_valid(vmask, lane) && tl_or_l0(job, lane >> 2);
+        uint32_t zz = U32MAX; // (dec_init's state)
+        bool dref   = true;
+        if (eet || slz) {
+            if (have) {
+                zz                 = acc << 1;
+                const uint32_t pix = G.bw * G.bh; // (32-bit arithmetic as the reference's; a shift for a whole SB)
+                zz                 = pix == 4096u ? (zz * 64 * 64) >> 12 : (zz * 64 * 64) / pix;
+            }
+            const uint32_t best = wave_min_u32(zz);
+            if (have && (lane & 3) > 0 && tli > 0 && best < zth && (uint32_t)((zz - best) * 100u) > (uint32_t)(zpct * best))
+                dref = false;
+            if (slz) {
+                const uint32_t z0 = rl32(zz, 0), z4 = rl32(zz, 4);
+                const bool safe = hl > 0 && nl == 2 && tli >= hl && sbr && z0 < slz && z4 < slz;
+                if (safe && slot_valid(vmask, lane) && (lane & 3) > 0)
+                    dref = false;
+            }
+        }
+        if (lane < 8) {
+            d.zz[lane]     = zz;
+            d.do_ref[lane] = dref ? 1 : 0;
+        }
+        // the searches the reference performs: lane 2s pre-HME, 2s + 1 HME-L0 of slot s
+        const int s       = lane >> 1;
+        const uint32_t zs = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * s, (int)zz);
+        const uint32_t ds = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * s, dref ? 1 : 0);
+        const bool act    = lane < 16 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2) && ds;
+        const bool nd     = act && ((lane & 1) ? !(eet && zs < (eet >> 2)) : !(eet && zs < eet));
         const unsigned long long m = __ballot(nd);
         if (lane == 0)
             sh.u.a.need = (uint32_t)m;
