@@ -27,6 +27,17 @@ SVTME_HD uint16_t ref_dist_const(const svtme_job &j, int l, int r) {
     int64_t d = (int64_t)j.picture_number - (int64_t)j.ref_picture_number[l][r];
     return (uint16_t)(int16_t)(d < 0 ? -d : d);
 }
+// A wave-uniform byte / halfword field of a struct (a job) in global memory, read
+// as the dword that holds it: a scalar load (gfx950 has no scalar sub-dword load,
+// so the field itself would be a vector-memory round trip). SF(job, max_l0).
+template <typename S, typename T>
+__device__ __forceinline__ uint32_t sfld_(const S &obj, const T &f) {
+    static_assert(sizeof(T) <= 2 && alignof(S) >= 4, "sfld_: a byte / halfword of a dword-aligned struct");
+    const uint32_t off = (uint32_t)((const char *)&f - (const char *)&obj);
+    const uint32_t v   = ((const uint32_t *)&obj)[off >> 2] >> (8 * (off & 3));
+    return sizeof(T) == 1 ? (v & 0xFFu) : (v & 0xFFFFu);
+}
+#define SF(obj, field) ::svtme::sfld_((obj), (obj).field)
 __device__ __forceinline__ bool tl_or_l0(const svtme_job &j, int l) { return j.temporal_layer_index > 0 || l == 0; }
 __device__ __forceinline__ bool slot_valid(uint32_t vmask, int s) { return s >= 0 && s < 8 && ((vmask >> s) & 1u); }
 __device__ __forceinline__ uint32_t valid_mask(const svtme_job &job) {

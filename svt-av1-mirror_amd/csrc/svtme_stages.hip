@@ -1418,6 +1418,7 @@ struct StC {
     uint8_t cand0[SVTME_PU_COUNT + 3];
     uint32_t gm_cnt[2][4][2][2];
     uint32_t wm[8]; // magic_u32 of each slot's full-pel width (key decode)
+    uint32_t sink;  // finish_sb's stores that have no target
 };
 
 // Window of one reference: rows h, positions w, dword-aligned quads
@@ -1620,17 +1621,20 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
     constexpr int WDIST = NIMG, WGM = NIMG + 6;                                         // tail words
     const svtme_job &job = dj.job;
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    const int nl = job.num_lists, nr0 = job.num_refs[0], nr1 = nl == 2 ? job.num_refs[1] : 0;
-    const bool mctf = job.me_type == SVTME_ME_MCTF; // (no candidates / distortions, motion_estimation.c:3126)
+    // (the byte fields by scalar dword loads: SF)
+    const int nl = (int)SF(job, num_lists), nr0 = (int)SF(job, num_refs[0]), nr1 = nl == 2 ? (int)SF(job, num_refs[1]) : 0;
+    const bool mctf = SF(job, me_type) == SVTME_ME_MCTF; // (no candidates / distortions, motion_estimation.c:3126)
+    const bool en8 = SF(job, enable_me_8x8) != 0, en16 = SF(job, enable_me_16x16) != 0;
+    const int max_l0 = (int)SF(job, max_l0);
     uint32_t *img      = (uint32_t *)&st.keys[0][0];
     svtme_sb_result *o = (svtme_sb_result *)img;
     uint32_t *ow       = (uint32_t *)(dj.out_sb + sb_local);
     if (!mctf && tid < SVTME_PU_COUNT) {
-        const int npus = job.enable_me_16x16 ? (job.enable_me_8x8 ? 85 : 21) : 5;
+        const int npus = en16 ? (en8 ? 85 : 21) : 5;
         const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
         const int n    = tid;
         const int pu   = z_to_raster(n); // (a permutation: thread n owns PU pu's entries)
-        const int use  = job.enable_me_16x16 ? (job.enable_me_8x8 || n < 21) : n < 5;
+        const int use  = en16 ? (en8 || n < 21) : n < 5;
         if (mode != 2) // memset(total_me_candidate_index, 1, number_of_pus)
             o->total_me_candidate_index[pu] = pu < npus ? 1 : 0;
         if (mode == 0) { // construct_me_candidate_array_single_ref
@@ -1652,7 +1656,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             const uint32_t best = (org0 && org1) ? min_u32(s0, s1) : org0 ? s0 : s1;
             o->me_distortion[pu] = best;
             int min_list         = -1;
-            if (job.ctrl.use_best_unipred_cand_only && (blk & 3u) == 3u)
+            if (SF(job, ctrl.use_best_unipred_cand_only) && (blk & 3u) == 3u)
                 min_list = s0 < s1 ? 0 : 1;
             uint8_t c0 = 0;
             for (int li = 0; (uint32_t)li < nlist && (use || off == 0); ++li) {
@@ -1667,7 +1671,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                 }
                 if (min_list != -1 && min_list != li) {
                     if (use)
-                        o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
+                        o->me_mv_array[pu][li ? max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
                     continue;
                 }
                 if (use) {
@@ -1675,7 +1679,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                     o->me_candidate_array[pu][off] = cb;
                     if (off == 0)
                         c0 = cb;
-                    o->me_mv_array[pu][li ? job.max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
+                    o->me_mv_array[pu][li ? max_l0 : 0] = st.rec[li * 4][SVTME_PU_COUNT + n];
                 }
                 off++;
             }
@@ -1692,55 +1696,86 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             // (a slot without do_ref takes no part)
             static_assert(offsetof(StC, do_ref) % 4 == 0, "StC::do_ref: two dword reads");
             const uint32_t dr0 = ((const uint32_t *)st.do_ref)[0], dr1 = ((const uint32_t *)st.do_ref)[1];
+            const uint32_t slots = UNI((0xFu >> (4 - nr0)) | ((0xFu >> (4 - nr1)) << 4)); // r < nr[li]
             uint32_t sad[8], blk = 0, best = U32MAX;
 #pragma unroll
             for (int s2 = 0; s2 < 8; s2++) {
-                const int r = s2 & 3;
-                const bool in = (s2 < 4 ? r < nr0 : r < nr1) && (((s2 < 4 ? dr0 : dr1) >> (8 * r)) & 0xFFu);
+                sad[s2] = U32MAX;
+                if (!((slots >> s2) & 1u))
+                    continue; // wave-uniform
+                const int r   = s2 & 3;
+                const bool in = (((s2 < 4 ? dr0 : dr1) >> (8 * r)) & 0xFFu) != 0;
                 sad[s2]       = in ? st.rec[s2][n] : U32MAX;
                 blk |= in ? 1u << s2 : 0u;
                 best = min_u32(best, sad[s2]);
             }
             o->me_distortion[pu] = best;
-            // pruning of the unipred candidates (each against the best alone)
+            // pruning of the unipred candidates (each against the best alone; a slot
+            // outside blk has no bit to clear)
             const uint32_t prune_th = (uint32_t)job.ctrl.prune_me_candidates_th;
             if (prune_th > 0) {
+                const uint32_t bt = best * prune_th;
 #pragma unroll
                 for (int s2 = 0; s2 < 8; s2++)
-                    if (((blk >> s2) & 1u) && (sad[s2] - best) * 100 > best * prune_th)
-                        blk &= ~(1u << s2);
+                    if ((slots >> s2) & 1u) // wave-uniform
+                        blk &= (sad[s2] - best) * 100u > bt ? ~(1u << s2) : ~0u;
             }
-            // the first candidate (GM detection reads it; 0 for a PU without
-            // candidates), then, for a PU with candidates, the whole list: unipred in (list, ref) order with their MVs,
-            // bipred (L0 x L1), L0-L0 (0, a), L1-L1 (0, 2)
-            const int first = blk ? __builtin_ctz(blk) : -1;
-            st.cand0[pu]    = !use || first < 0 ? 0 : mk_cand(first >> 2, first & 3, first & 3, first < 4 ? 0 : 24,
-                                                              first < 4 ? 24 : 1);
-            if (use) {
-                uint8_t *ca = o->me_candidate_array[pu];
-                int off     = 0;
+            // the list as a mask over the potential candidates in the reference's order:
+            // bit s2 unipred (list, ref) (:2597-2628), 8 + 4 a + b bipred L0 a x L1 b
+            // (:2705-2732), 24 + a - 1 L0-L0 (0, a) (:2737-2760), 27 L1-L1 (0, 2) (:2763-2790)
+            const bool lbwd = SF(job, only_l_bwd) != 0;
+            const uint32_t m1 = (blk >> 4) & 0xFu;
+            uint32_t bip = 0;
 #pragma unroll
-                for (int s2 = 0; s2 < 8; s2++)
-                    if ((blk >> s2) & 1u) {
-                        const int li = s2 >> 2, r = s2 & 3;
-                        ca[off++]    = mk_cand(li, r, r, li == 0 ? 0 : 24, li == 1 ? 1 : 24);
-                        o->me_mv_array[pu][(li ? job.max_l0 : 0) + r] = st.rec[s2][SVTME_PU_COUNT + n];
-                    }
-                if (nl == 2) {
-                    for (int a2 = 0; a2 < nr0; a2++)
-                        for (int b2 = 0; b2 < nr1; b2++)
-                            if ((!job.only_l_bwd || (a2 == 0 && b2 == 0)) && ((blk >> a2) & 1u) &&
-                                ((blk >> (4 + b2)) & 1u))
-                                ca[off++] = mk_cand(2, a2, b2, 0, 1);
-                    if (!job.only_l_bwd) {
-                        for (int a2 = 1; a2 < nr0; a2++)
-                            if ((blk & 1u) && ((blk >> a2) & 1u))
-                                ca[off++] = mk_cand(2, 0, a2, 0, 0);
-                        if (nr1 == 3 && ((blk >> 4) & 1u) && ((blk >> 6) & 1u))
-                            ca[off++] = mk_cand(2, 0, 2, 1, 1);
-                    }
-                }
-                o->total_me_candidate_index[pu] = (uint8_t)off;
+            for (int a2 = 0; a2 < 4; a2++)
+                bip |= (((blk >> a2) & 1u) * m1) << (4 * a2);
+            uint32_t cm = blk; // (no list-1 bits with one list)
+            if (nl == 2) {
+                cm |= (lbwd ? bip & 1u : bip) << 8;
+                if (!lbwd)
+                    cm |= ((blk & 1u) ? ((blk >> 1) & 7u) << 24 : 0u) |
+                          ((nr1 == 3 && ((blk >> 4) & 1u) && ((blk >> 6) & 1u)) ? 1u << 27 : 0u);
+            }
+            cm = use ? cm : 0u;
+            // the first candidate (GM detection reads it; 0 for a PU without candidates)
+            const uint32_t f = (uint32_t)__builtin_ctz(blk | 0x100u), fl = f >> 2;
+            st.cand0[pu]     = (uint8_t)((use && blk) ? fl | ((f & 3u) * 0x14u) | (fl << 7) : 0u);
+            // candidate p goes to position popcount(cm below p): every potential candidate is
+            // stored in order, one absent from the list at the position of the next present
+            // one (which overwrites it) or at the list's end (cleared after the loop)
+            uint32_t can = slots;
+            if (nl == 2) {
+                uint32_t bp = 0;
+                for (int a2 = 0; a2 < nr0; a2++)
+                    bp |= (0xFu >> (4 - nr1)) << (4 * a2);
+                can |= (lbwd ? bp & 1u : bp) << 8;
+                if (!lbwd)
+                    can |= (((0xFu >> (4 - nr0)) >> 1) << 24) | (nr1 == 3 ? 1u << 27 : 0u);
+            }
+            can = UNI(can);
+            uint8_t *ca = o->me_candidate_array[pu];
+#pragma unroll
+            for (int q = 0; q < 28; q++) {
+                if (!((can >> q) & 1u))
+                    continue; // wave-uniform
+                const uint32_t v = q < 4 ? (uint32_t)q * 0x14u : q < 8 ? 0x81u | (uint32_t)(q & 3) * 0x14u
+                                   : q < 24 ? 0x82u | (uint32_t)(((q - 8) >> 2) << 2) | (uint32_t)(((q - 8) & 3) << 4)
+                                   : q < 27 ? 0x02u | (uint32_t)((q - 23) << 4) : 0xE2u;
+                ca[__builtin_popcount(cm & ((1u << q) - 1u))] = (uint8_t)v;
+            }
+            const uint32_t cnt = (uint32_t)__builtin_popcount(cm);
+            if (cnt < SVTME_MAX_PA_ME_CAND)
+                ca[cnt] = 0;
+            o->total_me_candidate_index[pu] = (uint8_t)cnt;
+            // the unipred candidates' MVs (a PU without them writes to st.sink)
+#pragma unroll
+            for (int s2 = 0; s2 < 8; s2++) {
+                if (!((slots >> s2) & 1u))
+                    continue; // wave-uniform
+                const uint32_t mv = st.rec[s2][SVTME_PU_COUNT + n];
+                uint32_t *dst     = ((cm >> s2) & 1u) ? &o->me_mv_array[pu][(s2 >> 2 ? max_l0 : 0) + (s2 & 3)]
+                                                      : &st.sink;
+                *dst = mv;
             }
         }
     }
@@ -1784,7 +1819,7 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             const uint32_t x  = dd * 4096u;
             const uint32_t nd = pix == 4096u ? x >> 12 : x / pix;
             w6 = lane == 0 ? (uint32_t)(sq / 64)                        // me_8x8_cost_variance
-                 : lane == 1 ? ((job.input_resolution <= 2) ? d8 : d16) // rc_me_distortion
+                 : lane == 1 ? ((SF(job, input_resolution) <= 2) ? d8 : d16) // rc_me_distortion
                              : nd;                                      // me_{64x64,32x32,16x16,8x8}_distortion
         }
         if (lane < 6)
@@ -1794,23 +1829,24 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
         // direction counters are LDS adds, the stationary count a ballot; the flag
         // bytes (stationary_block_present, rc_me_allow_gm) and the padding to HBM
         uint32_t flags = 0;
-        if (!mctf && job.gm_enabled) {
+        if (!mctf && SF(job, gm_enabled)) {
             uint32_t *cntf = &st.gm_cnt[0][0][0][0];
             if (lane < 32)
                 cntf[lane] = 0;
             wave_lds_fence();
-            const bool low  = job.input_resolution <= 2;
+            const bool low  = SF(job, input_resolution) <= 2;
+            const bool gmd  = SF(job, gm_use_distance_based_active_th) != 0;
             const int n_blk = low ? 64 : 16;
             bool stat       = false;
             if (lane < n_blk) {
                 uint8_t n = (uint8_t)(low ? 21 + lane : 5 + lane);
-                if (low && !job.enable_me_8x8) {
+                if (low && !en8) {
                     if (n >= 21)
                         n = c_8x8_to_16x16[n - 21];
-                    if (!job.enable_me_16x16 && n >= 5)
+                    if (!en16 && n >= 5)
                         n = c_16x16_to_32x32[n - 5];
                 }
-                if (!low && !job.enable_me_16x16 && n >= 5)
+                if (!low && !en16 && n >= 5)
                     n = c_16x16_to_32x32[n - 5];
                 const uint8_t cb = st.cand0[n];
                 const int dir = cb & 3, r0 = (cb >> 2) & 3, r1 = (cb >> 4) & 3, l0 = (cb >> 6) & 1, l1 = (cb >> 7) & 1;
@@ -1824,10 +1860,10 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
                 if (low) {
                     const uint64_t a2 = job.picture_number, b2 = rp;
                     const uint16_t dist = (uint16_t)absi((int16_t)((a2 > b2 ? a2 : b2) - (a2 < b2 ? a2 : b2)));
-                    active_th = job.gm_use_distance_based_active_th ? max(dist >> 1, 4) : 4;
+                    active_th = gmd ? max(dist >> 1, 4) : 4;
                 } else {
                     const uint16_t dist = (uint16_t)absi((int16_t)(job.picture_number - rp));
-                    active_th = job.gm_use_distance_based_active_th ? max(dist * 16, 32) : 32;
+                    active_th = gmd ? max(dist * 16, 32) : 32;
                 }
                 const uint32_t mv = st.rec[li * 4 + ri][SVTME_PU_COUNT + n];
                 const int mx = (int)(int16_t)(mv & 0xFFFF) * 4, my = (int)(int16_t)(mv >> 16) * 4;
@@ -1865,7 +1901,7 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
     const int tid = threadIdx.x, lane = tid & 63;
     const bool w0 = (tid >> 6) == 0;
     // ---- me_prune_ref (motion_estimation.c:1522-1565)
-    if (job.me_type != SVTME_ME_MCTF && c.enable_hme_flag && c.enable_me_hme_ref_pruning && w0) {
+    if (SF(job, me_type) != SVTME_ME_MCTF && SF(c, enable_hme_flag) && SF(c, enable_me_hme_ref_pruning) && w0) {
         const int s = lane;
         // the 64 8x8 best SADs of every searched slot, summed across the wave
         // (searched == do_ref outside MCTF: each SAD < 2^15, the sum fits 32 bits)
@@ -1890,7 +1926,7 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
                 st.hme_sad[s] = v;
             }
         }
-        const uint16_t th = c.prune_ref_if_me_sad_dev_bigger_than_th;
+        const uint16_t th = (uint16_t)SF(c, prune_ref_if_me_sad_dev_bigger_than_th);
         if (th != (uint16_t)~0) {
             const uint64_t best = wave_min_u64(v);
             if (s < 8 && (s & 3) >= 1 && (v - best) * 100 > (th * best))
@@ -1906,10 +1942,10 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
     {
         static_assert(sizeof(svtme_ref_record) == 176 * 4, "svtme_ref_record: 176 dwords");
         svtme_ref_record *out = dj.out_records + (size_t)sb_local * dj.R;
-        const int R = (int)dj.R;
+        const int R = (int)dj.R, nr0 = (int)SF(job, num_refs[0]);
         for (int i = tid; i < R * 44; i += 256) {
             const int k = i / 44, q = i - 44 * k;
-            const int s = k < job.num_refs[0] ? k : 4 + (k - job.num_refs[0]);
+            const int s = k < nr0 ? k : 4 + (k - nr0);
             uint4 v     = ((const uint4 *)st.rec[s])[q];
             if (q < 22 && !st.searched[s]) { // words 0 .. 87: the SADs (< 85) of an unsearched slot
                 if (4 * q + 0 < 85) v.x = U32MAX;
@@ -2578,20 +2614,21 @@ __device__ __forceinline__ FpArea fp_area(const DevJob &dj, const SbGeo &G, int 
     const svtme_controls &c = job.ctrl;
     const int l = s >> 2, r = s & 3;
     const uint32_t ox = G.ox, oy = G.oy;
-    const bool mctf   = job.me_type == SVTME_ME_MCTF;
+    const bool mctf   = SF(job, me_type) == SVTME_ME_MCTF;
     const DevPlane &C = dj.cur.lv[0];
     const DevPlane &P = dj.ref[l][r].lv[0];
     int16_t xc = sc_x, yc = sc_y;
     uint16_t dist = ref_dist_const(job, l, r);
     if (!mctf) // :1300-1302
         dist = scaled_dist(dist);
-    int16_t w = i16(min((int)(c.me_sa.sa_min.width * dist), (int)c.me_sa.sa_max.width));
-    int16_t h = i16(min((int)(c.me_sa.sa_min.height * dist), (int)c.me_sa.sa_max.height));
-    if (c.mv_sa_adj_enabled && (!c.mv_sa_adj_nearest_ref_only || r == 0)) {
-        if (absi(xc) > c.mv_sa_adj_mv_size_th)
-            w = i16(w * c.mv_sa_adj_sa_multiplier);
-        if (absi(yc) > c.mv_sa_adj_mv_size_th)
-            h = i16(h * c.mv_sa_adj_sa_multiplier);
+    int16_t w = i16(min((int)(SF(c, me_sa.sa_min.width) * dist), (int)SF(c, me_sa.sa_max.width)));
+    int16_t h = i16(min((int)(SF(c, me_sa.sa_min.height) * dist), (int)SF(c, me_sa.sa_max.height)));
+    if (SF(c, mv_sa_adj_enabled) && (!SF(c, mv_sa_adj_nearest_ref_only) || r == 0)) {
+        const int mth = (int)SF(c, mv_sa_adj_mv_size_th), mul = (int)SF(c, mv_sa_adj_sa_multiplier);
+        if (absi(xc) > mth)
+            w = i16(w * mul);
+        if (absi(yc) > mth)
+            h = i16(h * mul);
     }
     w = i16((max(1u, ((uint32_t)(int32_t)w / rdiv)) + 7) & ~0x07u);
     h = i16(max(3u, ((uint32_t)(int32_t)h / rdiv)));
@@ -2601,7 +2638,7 @@ __device__ __forceinline__ FpArea fp_area(const DevJob &dj, const SbGeo &G, int 
             w = 1;
             h = 1;
         }
-    } else if ((xc != 0 || yc != 0) && job.is_ref) { // check_00_center (:1139-1206)
+    } else if ((xc != 0 || yc != 0) && SF(job, is_ref)) { // check_00_center (:1139-1206)
         const int16_t pw = i16(P.width), ph = i16(P.height);
         xc = ((org_x + xc) < -pad) ? i16(-pad - org_x) : xc;
         xc = ((org_x + xc) > pw - 1) ? i16(xc - ((org_x + xc) - (pw - 1))) : xc;
@@ -2623,7 +2660,7 @@ __device__ __forceinline__ FpArea fp_area(const DevJob &dj, const SbGeo &G, int 
     }
     // 8x8-variance centre probe and search-area resize (:1391-1439); the probe's
     // keys (order 0) stay with the caller, so the centre wins ties against the search
-    const bool probe = c.me_8x8_var_enabled && (w * h > 24);
+    const bool probe = SF(c, me_8x8_var_enabled) && (w * h > 24);
     if (probe) {
         const uint32_t var = probe_var(P.base + (ptrdiff_t)((int)oy + yc) * P.stride + ((int)ox + xc));
         if (var > c.me_sr_mult2_th) {
@@ -2667,7 +2704,7 @@ __device__ __forceinline__ FpArea fp_area(const DevJob &dj, const SbGeo &G, int 
 // no per-SB output the record is the decode of this wavefront's 85 keys
 // (stage_e_body / stage_c_tail's record words) and k_stage_e is not launched
 __device__ __forceinline__ bool direct_records(const DevJob &dj) {
-    return dj.job.me_type == SVTME_ME_MCTF && dj.parts == 1 && dj.out_sb == nullptr;
+    return SF(dj.job, me_type) == SVTME_ME_MCTF && dj.parts == 1 && dj.out_sb == nullptr;
 }
 __device__ __forceinline__ void direct_record(svtme_ref_record *rec, const CSlot &v, unsigned long long k8,
                                               unsigned long long k16, unsigned long long k32, unsigned long long k64) {
@@ -3651,7 +3688,7 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
                                              unsigned long long *kb, bool reset) {
     const svtme_job &job = dj.job;
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    const int R = (int)dj.R, nr0 = job.num_refs[0];
+    const int R = (int)dj.R, nr0 = (int)SF(job, num_refs[0]);
     // the slot state in one pass: slot tid's record (k), or the defaults of a slot without one
     if (tid < 8) {
         const int s    = tid;
@@ -4385,7 +4422,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             src[rr][0] = v[0];
             src[rr][1] = v[1];
         }
-        const int s         = k < gj.job.num_refs[0] ? k : 4 + (k - gj.job.num_refs[0]);
+        const int nr0       = (int)SF(gj.job, num_refs[0]);
+        const int s         = k < nr0 ? k : 4 + (k - nr0);
         const SlotCentre &v = sh.cen[s];
         fp_slot<SUB_ME, K32, 2, false, HME_WHOLE>(gj, G, s, src, by, bx, rl64(v.hme_sad, 0), (uint32_t)UNI(v.zz), (uint32_t)UNI(v.reduce_div),
                                 (int16_t)UNI(v.sc_x), (int16_t)UNI(v.sc_y), (uint8_t)UNI(v.do_ref),
