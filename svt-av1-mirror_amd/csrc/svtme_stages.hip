@@ -1697,15 +1697,19 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             static_assert(offsetof(StC, do_ref) % 4 == 0, "StC::do_ref: two dword reads");
             const uint32_t dr0 = ((const uint32_t *)st.do_ref)[0], dr1 = ((const uint32_t *)st.do_ref)[1];
             const uint32_t slots = UNI((0xFu >> (4 - nr0)) | ((0xFu >> (4 - nr1)) << 4)); // r < nr[li]
-            uint32_t sad[8], blk = 0, best = U32MAX;
+            // every slot's SAD and MV read at once (one LDS round trip; a read under a
+            // per-slot branch waits for each): the slots outside `slots` are masked
+            uint32_t sad[8], mvs[8], blk = 0, best = U32MAX;
 #pragma unroll
             for (int s2 = 0; s2 < 8; s2++) {
-                sad[s2] = U32MAX;
-                if (!((slots >> s2) & 1u))
-                    continue; // wave-uniform
+                sad[s2] = st.rec[s2][n];
+                mvs[s2] = st.rec[s2][SVTME_PU_COUNT + n];
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 8; s2++) {
                 const int r   = s2 & 3;
-                const bool in = (((s2 < 4 ? dr0 : dr1) >> (8 * r)) & 0xFFu) != 0;
-                sad[s2]       = in ? st.rec[s2][n] : U32MAX;
+                const bool in = ((slots >> s2) & 1u) && (((s2 < 4 ? dr0 : dr1) >> (8 * r)) & 0xFFu) != 0;
+                sad[s2]       = in ? sad[s2] : U32MAX;
                 blk |= in ? 1u << s2 : 0u;
                 best = min_u32(best, sad[s2]);
             }
@@ -1772,10 +1776,8 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             for (int s2 = 0; s2 < 8; s2++) {
                 if (!((slots >> s2) & 1u))
                     continue; // wave-uniform
-                const uint32_t mv = st.rec[s2][SVTME_PU_COUNT + n];
-                uint32_t *dst     = ((cm >> s2) & 1u) ? &o->me_mv_array[pu][(s2 >> 2 ? max_l0 : 0) + (s2 & 3)]
-                                                      : &st.sink;
-                *dst = mv;
+                uint32_t *dst = ((cm >> s2) & 1u) ? &o->me_mv_array[pu][(s2 >> 2 ? max_l0 : 0) + (s2 & 3)] : &st.sink;
+                *dst          = mvs[s2];
             }
         }
     }
@@ -4193,18 +4195,140 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     const bool hsub = c.hme_search_method != SVTME_FULL_SAD_SEARCH; // true on this path
     if (wid == 0) {
         HME_PRIO_HI();
-        if (lane < SVTME_A_N && lane >= SVTME_A_PH) {
-            uint32_t best;
-            int x, y;
-            key_result(sh.u.a.key[lane], &best, &x, &y);
-            d.a[lane] = ARes{hsub ? best * 2 : best, i16((x + sh.u.a.kxo[lane]) * 4), i16((y + sh.u.a.kyo[lane]) * 4)};
+        // lane = slot * 4 + q (lane < 32): the slot's HME-L0 quadrant q (X, Y, SD), its zz SAD and do_ref
+        // (the lane id from mbcnt: the compiler would keep lane >> 2 live into the full-pel phase and spill it)
+        const int mlane = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        const int s = mlane >> 2, q = mlane & 3, l = s >> 2;
+        int16_t X0 = 0, Y0 = 0;
+        uint32_t S0 = 0, zzs, drs;
+        if constexpr (RT) {
+            if (lane < SVTME_A_N && lane >= SVTME_A_PH) {
+                uint32_t best;
+                int x, y;
+                key_result(sh.u.a.key[lane], &best, &x, &y);
+                d.a[lane] = ARes{hsub ? best * 2 : best, i16((x + sh.u.a.kxo[lane]) * 4), i16((y + sh.u.a.kyo[lane]) * 4)};
+            }
+            wave_lds_fence(); // (RT: dec_prehme ran before the second A1 round; its pruning is not idempotent)
+            dec_l0(d, job, vmask);
+            if (lane < 32) {
+                X0 = d.lx[s][q], Y0 = d.ly[s][q], S0 = (uint32_t)d.lsad[s][q];
+            }
+            zzs = d.zz[s & 7], drs = d.do_ref[s & 7];
+        } else {
+            // dec_prehme and dec_l0 (motion_estimation.c:1693-1796, 1906-2036) with the state in
+            // registers: every input read in one batch, the slot's two pre-HME regions in lanes
+            // q = 0, 1 of its quad, cross-lane values by DPP / permlane16_swap (no LDS round trips)
+            const svtme_controls &gc = gj.job.ctrl; // (uniform control values: scalar loads)
+            const uint32_t eet = gc.me_early_exit_th, pmse = gc.prev_me_stage_based_exit_th;
+            const uint32_t phth = gc.phme_sad_th, phpct = SF(gc, phme_sad_pct);
+            const bool ph_on = SF(gc, prehme_enable) != 0, l1ee = SF(gc, prehme_l1_early_exit) != 0;
+            const bool l0_on = SF(gc, enable_hme_flag) && SF(gc, enable_hme_level0_flag);
+            const int tli    = (int)SF(gj.job, temporal_layer_index);
+            const int i32    = lane & 31;
+            const unsigned long long kph = sh.u.a.key[SVTME_A_PH + ((2 * (i32 >> 2) + (q & 1)) & 15)];
+            const int pxo = sh.u.a.kxo[SVTME_A_PH + ((2 * (i32 >> 2) + (q & 1)) & 15)];
+            const int pyo = sh.u.a.kyo[SVTME_A_PH + ((2 * (i32 >> 2) + (q & 1)) & 15)];
+            const unsigned long long kl0 = sh.u.a.key[SVTME_A_L0 + i32];
+            const int lxo = sh.u.a.kxo[SVTME_A_L0 + i32], lyo = sh.u.a.kyo[SVTME_A_L0 + i32];
+            zzs = d.zz[s & 7];
+            drs = d.do_ref[s & 7];
+            const bool sv   = lane < 32 && slot_valid(vmask, s);
+            const bool tl   = tli > 0 || l == 0;
+            // pre-HME region q of slot s (q < 2): psad, pcr (col | row << 16), valid, performed
+            uint32_t psad = 0, pcr = 0;
+            bool pval = false, pperf = false;
+            if (ph_on) {
+                const bool have = sv && q < 2 && tl;
+                uint32_t kb;
+                int kx, ky;
+                key_result(kph, &kb, &kx, &ky);
+                if (have) {
+                    if (eet && zzs < eet) { // check_prehme_early_exit
+                        pval = true;
+                    } else if (!drs) {
+                        psad = U32MAX;
+                    } else { // searched in A1
+                        psad  = hsub ? kb * 2 : kb;
+                        pcr   = (uint32_t)(uint16_t)i16((kx + pxo) * 4) | ((uint32_t)(uint16_t)i16((ky + pyo) * 4) << 16);
+                        pval  = true;
+                        pperf = true;
+                    }
+                }
+                // list 1 mirrors list 0's region (lane - 16) when it is certain (:1693-1719)
+                const auto zs = __builtin_amdgcn_permlane16_swap(psad, psad, false, false);
+                const auto zc = __builtin_amdgcn_permlane16_swap(pcr, pcr, false, false);
+                const auto zv = __builtin_amdgcn_permlane16_swap(pval ? 1u : 0u, pval ? 1u : 0u, false, false);
+                const uint32_t zsad = zs[0], zcr = zc[0];
+                const int zcol = (int)(int16_t)(zcr & 0xFFFFu), zrow = (int)(int16_t)(zcr >> 16);
+                if (have && l == 1 && l1ee && !(eet && zzs < eet) && zv[0] &&
+                    (zsad < 32 * 32 || (absi(zcol) < 16 && absi(zrow) < 16))) {
+                    psad  = zsad;
+                    pcr   = (uint32_t)(uint16_t)(int16_t)-zcol | ((uint32_t)(uint16_t)(int16_t)-zrow << 16);
+                    pval  = true;
+                    pperf = false;
+                }
+                // the slot's best pre-HME SAD against the best slot's (:1773-1796)
+                const uint32_t p0 = dpp_or<0x00>(psad, 0u), p1 = dpp_or<0x55>(psad, 0u); // quad lanes 0, 1
+                const uint32_t m  = sv && tl ? min_u32(p0, p1) : U32MAX;
+                const uint32_t bm = wave_min_u32(m);
+                if (tli > 0 && bm < phth && sv && (s & 3) > 0 && drs && (uint32_t)((m - bm) * 100u) > (uint32_t)(phpct * bm))
+                    drs = 0;
+            }
+            // level 0 of quadrant q (dec_l0)
+            bool srch = false;
+            if (l0_on) {
+                // the slot's pre-HME region with the lower SAD (quad lanes 0, 1)
+                const uint32_t s0 = dpp_or<0x00>(psad, 0u), s1 = dpp_or<0x55>(psad, 0u);
+                const uint32_t c0 = dpp_or<0x00>(pcr, 0u), c1 = dpp_or<0x55>(pcr, 0u);
+                const uint32_t f0 = dpp_or<0x00>(pperf ? 1u : 0u, 0u), f1 = dpp_or<0x55>(pperf ? 1u : 0u, 0u);
+                const bool k1     = !(s0 <= s1);
+                const uint32_t bs = k1 ? s1 : s0, bcr = k1 ? c1 : c0;
+                const bool bperf  = (k1 ? f1 : f0) != 0;
+                uint32_t kb;
+                int kx, ky;
+                key_result(kl0, &kb, &kx, &ky);
+                if (sv) {
+                    if (eet && zzs < (eet >> 2)) {
+                    } else if (pmse && bperf && bs < (pmse >> 4)) {
+                        X0 = (int16_t)(bcr & 0xFFFFu), Y0 = (int16_t)(bcr >> 16), S0 = bs;
+                    } else if (!drs) {
+                        S0 = U32MAX;
+                    } else if (tl) {
+                        X0   = i16((kx + lxo) * 4);
+                        Y0   = i16((ky + lyo) * 4);
+                        S0   = hsub ? kb * 2 : kb;
+                        srch = true;
+                    }
+                }
+                // pre-HME replaces the worst quadrant of each searched slot (:2005-2032)
+                const unsigned long long sm = __ballot(srch);
+                if (ph_on && lane < 32 && ((sm >> (4 * s)) & 0xFu)) {
+                    const uint32_t q0 = dpp_or<0x00>(S0, 0u), q1 = dpp_or<0x55>(S0, 0u);
+                    const uint32_t q2 = dpp_or<0xAA>(S0, 0u), q3 = dpp_or<0xFF>(S0, 0u);
+                    int wq = 0; // get_worst_quadrant: strict > in (0,0),(1,0),(0,1),(1,1) order
+                    uint32_t mx = 0;
+                    if (q0 > mx) { mx = q0; wq = 0; }
+                    if (q2 > mx) { mx = q2; wq = 2; }
+                    if (q1 > mx) { mx = q1; wq = 1; }
+                    if (q3 > mx) { wq = 3; }
+                    const uint32_t sw = wq == 0 ? q0 : wq == 1 ? q1 : wq == 2 ? q2 : q3;
+                    if (q == wq && bs < sw) {
+                        S0 = bs;
+                        X0 = (int16_t)(bcr & 0xFFFFu);
+                        Y0 = (int16_t)(bcr >> 16);
+                    }
+                }
+            }
+            // the decisions' state for phase B's copy to BState
+            if (lane < 32) {
+                d.lx[s][q]   = X0;
+                d.ly[s][q]   = Y0;
+                d.lsad[s][q] = S0;
+            }
+            if (lane < 32 && q == 0)
+                d.do_ref[s] = (uint8_t)drs;
         }
-        wave_lds_fence();
-        if (!RT) // (RT: made before the second A1 round; its pruning is not idempotent)
-            dec_prehme(d, job, vmask);
-        dec_l0(d, job, vmask);
         // HME-L1 per (slot, quadrant), lane = slot * 4 + q (hme_level1_b64, :2041-2122)
-        const int s = lane >> 2, q = lane & 3, l = s >> 2;
         bool mk   = false;
         int items = 0;
         HSrch1 e;
@@ -4215,15 +4339,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             const bool listed = c.enable_hme_flag && c.enable_hme_level1_flag && slot_valid(vmask, s) &&
                                 tl_or_l0(job, l);
             if (listed) { // hme_level1_b64 (motion_estimation.c:2041-2122)
-                const int16_t X0 = d.lx[s][q], Y0 = d.ly[s][q];
-                const uint64_t S0 = d.lsad[s][q];
                 bool done = false;
-                if (c.me_early_exit_th && d.zz[s] < (c.me_early_exit_th >> 2)) {
+                if (c.me_early_exit_th && zzs < (c.me_early_exit_th >> 2)) {
                     X = Y = 0;
                     SD   = 0;
                     done = true;
                 }
-                if (!done && !d.do_ref[s]) {
+                if (!done && !drs) {
                     X = Y = 0;
                     SD   = U32MAX;
                     done = true;
