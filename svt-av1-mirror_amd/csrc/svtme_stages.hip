@@ -968,30 +968,49 @@ struct SlotCentre {
     uint8_t do_ref;
 };
 
+// set_final_seach_centre_sb and hme_prune_ref_and_adjust_sr (motion_estimation.c:
+// 2182-2380, 2477-2518), lane = slot. Every input is read first, unconditionally,
+// in one batch (control values by scalar loads when job is in global memory, the
+// slot's BState words): a read under a branch would wait for each in turn
 __device__ __forceinline__ SlotCentre final_centre(const svtme_job &job, const BState *b, uint32_t vmask) {
     const svtme_controls &c = job.ctrl;
     const int s             = threadIdx.x & 63;
-    const bool valid        = slot_valid(vmask, s);
-    int lvl                 = -1;
-    if (c.enable_hme_level0_flag && !c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
+    const bool hme_on = SF(c, enable_hme_flag) != 0, l0f = SF(c, enable_hme_level0_flag) != 0;
+    const bool l1f = SF(c, enable_hme_level1_flag) != 0, l2f = SF(c, enable_hme_level2_flag) != 0;
+    const bool mctf  = SF(job, me_type) == SVTME_ME_MCTF;
+    const int tli    = (int)SF(job, temporal_layer_index);
+    const uint32_t pth = SF(c, prune_ref_if_hme_sad_dev_bigger_than_th);
+    const bool prune = SF(c, enable_me_hme_ref_pruning) != 0, sradj = SF(c, enable_me_sr_adjustment) != 0;
+    const int mvlen  = (int)SF(c, reduce_me_sr_based_on_mv_length_th);
+    const uint32_t stat_th = SF(c, stationary_hme_sad_abs_th), stat_div = SF(c, stationary_me_sr_divisor);
+    const uint32_t low_th = SF(c, reduce_me_sr_based_on_hme_sad_abs_th), low_div = SF(c, me_sr_divisor_for_low_hme_sad);
+    int lvl = -1;
+    if (l0f && !l1f && !l2f)
         lvl = 0;
-    if (c.enable_hme_level1_flag && !c.enable_hme_level2_flag)
+    if (l1f && !l2f)
         lvl = 1;
-    if (c.enable_hme_level2_flag)
+    if (l2f)
         lvl = 2;
-    const bool hme_slot = valid && tl_or_l0(job, s >> 2) && c.enable_hme_flag;
+    const int sl = s & 7;
+    const int16_t *X  = lvl > 0 ? b->hx[sl] : b->lx[sl];
+    const int16_t *Y  = lvl > 0 ? b->hy[sl] : b->ly[sl];
+    const uint64_t *S = lvl > 0 ? b->hsad[sl] : b->lsad[sl];
+    // (named values, not arrays: small private arrays are promoted to LDS)
+    const int16_t x0 = X[0], x1 = X[1], x2 = X[2], x3 = X[3], y0 = Y[0], y1 = Y[1], y2 = Y[2], y3 = Y[3];
+    const uint64_t s0 = S[0], s1 = S[1], s2 = S[2], s3 = S[3];
+    const uint8_t dref0 = b->do_ref[sl];
+    const uint32_t zz0  = b->zz[sl];
+    const bool valid    = slot_valid(vmask, s);
+    const bool hme_slot = valid && (tli > 0 || (s >> 2) == 0) && hme_on;
     int16_t hx = 0, hy = 0;
     uint64_t hs    = 0;
     const bool own = hme_slot && lvl >= 0;
     if (own) {
-        const int16_t *X  = lvl ? b->hx[s] : b->lx[s];
-        const int16_t *Y  = lvl ? b->hy[s] : b->ly[s];
-        const uint64_t *S = lvl ? b->hsad[s] : b->lsad[s];
-        hx = X[0], hy = Y[0], hs = S[0];
+        hx = x0, hy = y0, hs = s0;
         // scan order (w, h): (1,0), (0,1), (1,1) = q 2, 1, 3
-        if (S[2] < hs) { hx = X[2]; hy = Y[2]; hs = S[2]; }
-        if (S[1] < hs) { hx = X[1]; hy = Y[1]; hs = S[1]; }
-        if (S[3] < hs) { hx = X[3]; hy = Y[3]; hs = S[3]; }
+        if (s2 < hs) { hx = x2; hy = y2; hs = s2; }
+        if (s1 < hs) { hx = x1; hy = y1; hs = s1; }
+        if (s3 < hs) { hx = x3; hy = y3; hs = s3; }
     }
     // the reference carries function-scope values across slots
     int16_t cx = 0, cy = 0, scx = 0, scy = 0;
@@ -1003,7 +1022,7 @@ __device__ __forceinline__ SlotCentre final_centre(const svtme_job &job, const B
             continue;
         const bool ok = rl32((uint32_t)own, k) != 0;
         const bool hk = rl32((uint32_t)hme_slot, k) != 0;
-        const bool tk = tl_or_l0(job, k >> 2);
+        const bool tk = tli > 0 || (k >> 2) == 0;
         const int16_t kx = (int16_t)rl32((uint32_t)(int32_t)hx, k), ky = (int16_t)rl32((uint32_t)(int32_t)hy, k);
         const uint64_t ks = rl64(hs, k);
         if (ok) {
@@ -1026,25 +1045,23 @@ __device__ __forceinline__ SlotCentre final_centre(const svtme_job &job, const B
     if (valid)
         hsad = my_hs;
     uint32_t rdiv = 1;
-    uint8_t dref  = s < 8 ? b->do_ref[s] : 0;
-    if (c.enable_hme_flag && job.me_type != SVTME_ME_MCTF) { // prune_ref (motion_estimation.c:3103)
-        const uint16_t th = c.prune_ref_if_hme_sad_dev_bigger_than_th;
-        if (c.enable_me_hme_ref_pruning && th != (uint16_t)~0) {
+    uint8_t dref  = s < 8 ? dref0 : 0;
+    if (hme_on && !mctf) { // prune_ref (motion_estimation.c:3103)
+        if (prune && pth != 0xFFFFu) {
             const uint64_t best = wave_min_u64(s < 8 ? hsad : ~0ull);
-            if (s < 8 && (s & 3) >= 1 && (hsad - best) * 100 > (th * best))
+            if (s < 8 && (s & 3) >= 1 && (hsad - best) * 100 > (pth * best))
                 dref = 0;
         }
-        if (c.enable_me_sr_adjustment && s < 8) {
-            if (absi(my_scx) <= c.reduce_me_sr_based_on_mv_length_th &&
-                absi(my_scy) <= c.reduce_me_sr_based_on_mv_length_th && hsad < c.stationary_hme_sad_abs_th)
-                rdiv = c.stationary_me_sr_divisor;
-            else if (hsad < c.reduce_me_sr_based_on_hme_sad_abs_th)
-                rdiv = c.me_sr_divisor_for_low_hme_sad;
+        if (sradj && s < 8) {
+            if (absi(my_scx) <= mvlen && absi(my_scy) <= mvlen && hsad < stat_th)
+                rdiv = stat_div;
+            else if (hsad < low_th)
+                rdiv = low_div;
         }
     }
     SlotCentre o;
     o.hme_sad    = hsad;
-    o.zz         = s < 8 ? b->zz[s] : U32MAX;
+    o.zz         = s < 8 ? zz0 : U32MAX;
     o.reduce_div = rdiv;
     o.sc_x       = valid ? my_scx : 0;
     o.sc_y       = valid ? my_scy : 0;
@@ -4517,7 +4534,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     // integer_search_b64 of every record, one wavefront each (k_stage_c1, one band)
     if (wid == 0) {
         HME_PRIO_HI();
-        const SlotCentre scv = final_centre(job, &sh.bs, vmask); // lane = slot
+        const SlotCentre scv = final_centre(gj.job, &sh.bs, vmask); // lane = slot (controls by scalar loads)
         if (lane < 8)
             sh.cen[lane] = scv;
         if (lane == 0)
