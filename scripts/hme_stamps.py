@@ -50,7 +50,7 @@ def main():
     gpu.sync()
     lib = S.load_product()
     nb = n_sb * P
-    st = np.zeros((nb, 24), np.uint64)
+    st = np.zeros((nb, 32), np.uint64)
     fn = lib.svtme_debug_hme_stamps
     fn.argtypes = [C.c_void_p, C.c_uint32]
     fn.restype = C.c_int
@@ -59,6 +59,15 @@ def main():
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{name}_x{P}.npy"), st)
     rt, ids, st_w = st[:, 8:10], st[:, 10:12], st[:, 12:16]
+    wv = st[:, 24:32]  # per wavefront: phase-0 work done, full-pel records done
+    if wv.any():
+        for w in range(4):
+            print(f"  wave {w}: phase-0 work done at mean {np.mean(wv[:, w] - st[:, 0]):7.0f} cycles after start; "
+                  f"full-pel records done {np.mean(wv[:, 4 + w] - st[:, 16]):7.0f} after the final centre")
+    fp = st[:, 22:24]  # wave 0's record: search area (check_00_center, probe) done, search done
+    if fp.all():
+        print(f"  wave 0 full-pel: area + probe {np.mean(fp[:, 0] - st[:, 16]):7.0f} cycles after the final centre, "
+              f"search {np.mean(fp[:, 1] - fp[:, 0]):7.0f}, keys {np.mean(wv[:, 4] - fp[:, 1]):7.0f}")
     esub = st[:, [6, 17, 18, 19, 20, 21, 7]]  # stage E: decode + prune, records, image zero, SB results
     st = np.concatenate([st[:, :6], st[:, 16:17], st[:, 6:8]], axis=1)  # ... L1, centre, full-pel, E
     if not st[:, 8].any():  # HME-only build: the last stamp is 6

@@ -15,7 +15,7 @@
 #include <stdint.h>
 
 #ifdef SVTME_STAMPS
-__device__ unsigned long long g_hme_stamps[1 << 17][24];
+__device__ unsigned long long g_hme_stamps[1 << 17][32];
 // slots 0-7 shader clock per phase; 8 / 9 the 100 MHz real-time clock at the
 // first / latest stamp; 10 XCC_ID, 11 HW_ID (CU, SE) register values; 12-15
 // HW_ID of waves 0-3; 16 shader clock after the final search centre (HME_STOP(55))
@@ -39,6 +39,14 @@ __device__ unsigned long long g_hme_stamps[1 << 17][24];
     } while (0)
 // stage E's sub-phases (stage_c_tail): 17 after me_prune_ref, 18 after the records, 19 after the image zeroing,
 // 20 after the candidate arrays (finish_sb's barrier), 21 at the end of wave 0's SB results
+// 22 / 23 in fp_slot: after the search area (and its probe), after the search
+// HME_WAVE(k): lane 0 of every wavefront w stamps slot 24 + 4 k + w (k 0: its phase-0 work done,
+// k 1: its full-pel records done), before the barrier that ends the phase
+#define HME_WAVE(k)                                                                                                    \
+    do {                                                                                                               \
+        if ((threadIdx.x & 63) == 0 && blockIdx.x < (1u << 17))                                                        \
+            g_hme_stamps[blockIdx.x][24 + 4 * (k) + (threadIdx.x >> 6)] = __builtin_readcyclecounter();                 \
+    } while (0)
 #define HME_SUB(k)                                                                                                     \
     do {                                                                                                               \
         if (threadIdx.x == 0 && blockIdx.x < (1u << 17))                                                               \
@@ -47,7 +55,7 @@ __device__ unsigned long long g_hme_stamps[1 << 17][24];
 extern "C" int svtme_debug_hme_stamps(unsigned long long *out, uint32_t nblocks) {
     if (nblocks > (1u << 17))
         nblocks = 1u << 17;
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 24 * sizeof(unsigned long long));
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_hme_stamps), (size_t)nblocks * 32 * sizeof(unsigned long long));
 }
 #elif defined(SVTME_STOP_AFTER)
 #define HME_STAMP(k)                                                                                                   \

@@ -1102,6 +1102,9 @@ __device__ __forceinline__ SlotCentre final_centre(const svtme_job &job, const B
 #ifndef HME_SUB
 #define HME_SUB(k)
 #endif
+#ifndef HME_WAVE
+#define HME_WAVE(k)
+#endif
 
 #define HQ 2  // position quads per HME-L2 tile (rows realigned to position 0: 8-wide areas = 2 quads)
 #define HQ1 2 // position quads per HME-L1 tile (rows realigned to position 0: 8-wide areas = 2 quads)
@@ -2802,6 +2805,7 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     });
     const int16_t xo = A.xo, yo = A.yo, w = A.w, h = A.h, xc = A.xc, yc = A.yc;
     const bool probe = A.probe;
+    HME_SUB(22);
 
     // full-pel search of this part's rows (open_loop_me_fullpel_search_sblock, :781-817)
     const uint8_t *g = P.base + (ptrdiff_t)((int)oy + yo) * P.stride + ((int)ox + xo);
@@ -2819,6 +2823,7 @@ __device__ __forceinline__ void fp_slot(const DevJob &dj, const SbGeo &G, int s,
     }
     else
         fp_rows<SUB, K32, TQ>(M, (const uint32_t *)(g - sh), P.stride >> 2, sh, w, nq, y0, y1, obase, src, by, bx);
+    HME_SUB(23);
     M.finalize();
     const unsigned long long k8  = PuMin<K32>::template out<SUB>(M.b8, true);
     const unsigned long long k16 = PuMin<K32>::template out<SUB>(M.b16, false);
@@ -4061,6 +4066,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
             ((uint4 *)sh.u.a.src4[row])[half] = make_uint4(v.x, v.y, v.z, v.w);
         }
     }
+    HME_WAVE(0);
     __syncthreads();
     HME_STAMP(1);
     // ---- zz decisions; which searches the reference performs (wave 0)
@@ -4568,6 +4574,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                                 (int16_t)UNI(v.sc_x), (int16_t)UNI(v.sc_y), (uint8_t)UNI(v.do_ref),
                                 (uint8_t)UNI(sh.tf_exit), 0, 1u, &sh.u.st.keys[k][0], &sh.cin[k]);
     }
+    HME_WAVE(1);
     __syncthreads();
     HME_STAMP(6);
     // ---- E: decode, me_prune_ref, records, candidates / distortions / GM detection
