@@ -1628,27 +1628,20 @@ __device__ void fullpel(StC &st, const DevPlane &C, uint32_t ox, uint32_t oy) {
 // wave 0 (compute_distortion) and wave 1 (GM detection) finish the last words
 // and store them themselves: no zero fill of the HBM copy, no scattered byte
 // stores to HBM, one barrier.
-__device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
+// finish_sb in two parts, a barrier between: the candidate arrays, me_distortion and the
+// first candidates into the zeroed image (threads < 85), then the stores, distortions and
+// GM detection (waves 2-3, 0, 1)
+__device__ __forceinline__ void finish_sb_cands(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
     static_assert(sizeof(svtme_sb_result) % 4 == 0 && sizeof(svtme_sb_result) <= sizeof(st.keys) &&
                       sizeof(st.keys) % 16 == 0, "svtme_sb_result image over st.keys");
-    static_assert(offsetof(svtme_sb_result, me_8x8_cost_variance) ==
-                          offsetof(svtme_sb_result, me_distortion) + 4 * SVTME_PU_COUNT &&
-                      offsetof(svtme_sb_result, stationary_block_present) ==
-                          offsetof(svtme_sb_result, me_8x8_cost_variance) + 24 &&
-                      sizeof(svtme_sb_result) == offsetof(svtme_sb_result, stationary_block_present) + 8,
-                  "svtme_sb_result tail: 6 distortion words, then the GM flag bytes and padding");
-    constexpr int NIMG = (int)(offsetof(svtme_sb_result, me_8x8_cost_variance) / 4); // words stored from the image
-    constexpr int WDIST = NIMG, WGM = NIMG + 6;                                         // tail words
     const svtme_job &job = dj.job;
-    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const int tid        = threadIdx.x;
     // (the byte fields by scalar dword loads: SF)
     const int nl = (int)SF(job, num_lists), nr0 = (int)SF(job, num_refs[0]), nr1 = nl == 2 ? (int)SF(job, num_refs[1]) : 0;
     const bool mctf = SF(job, me_type) == SVTME_ME_MCTF; // (no candidates / distortions, motion_estimation.c:3126)
     const bool en8 = SF(job, enable_me_8x8) != 0, en16 = SF(job, enable_me_16x16) != 0;
-    const int max_l0 = (int)SF(job, max_l0);
-    uint32_t *img      = (uint32_t *)&st.keys[0][0];
-    svtme_sb_result *o = (svtme_sb_result *)img;
-    uint32_t *ow       = (uint32_t *)(dj.out_sb + sb_local);
+    const int max_l0   = (int)SF(job, max_l0);
+    svtme_sb_result *o = (svtme_sb_result *)&st.keys[0][0];
     if (!mctf && tid < SVTME_PU_COUNT) {
         const int npus = en16 ? (en8 ? 85 : 21) : 5;
         const int mode = (nr0 == 1 && nr1 == 0) ? 0 : (nr0 == 1 && nr1 == 1) ? 1 : 2;
@@ -1801,8 +1794,24 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
             }
         }
     }
-    __syncthreads();
-    HME_SUB(20);
+}
+
+__device__ __forceinline__ void finish_sb_out(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
+    static_assert(offsetof(svtme_sb_result, me_8x8_cost_variance) ==
+                          offsetof(svtme_sb_result, me_distortion) + 4 * SVTME_PU_COUNT &&
+                      offsetof(svtme_sb_result, stationary_block_present) ==
+                          offsetof(svtme_sb_result, me_8x8_cost_variance) + 24 &&
+                      sizeof(svtme_sb_result) == offsetof(svtme_sb_result, stationary_block_present) + 8,
+                  "svtme_sb_result tail: 6 distortion words, then the GM flag bytes and padding");
+    constexpr int NIMG = (int)(offsetof(svtme_sb_result, me_8x8_cost_variance) / 4); // words stored from the image
+    constexpr int WDIST = NIMG, WGM = NIMG + 6;                                         // tail words
+    const svtme_job &job = dj.job;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const bool mctf = SF(job, me_type) == SVTME_ME_MCTF; // (no candidates / distortions, motion_estimation.c:3126)
+    const bool en8 = SF(job, enable_me_8x8) != 0, en16 = SF(job, enable_me_16x16) != 0;
+    uint32_t *img      = (uint32_t *)&st.keys[0][0];
+    svtme_sb_result *o = (svtme_sb_result *)img;
+    uint32_t *ow       = (uint32_t *)(dj.out_sb + sb_local);
     if (wid >= 2) {
         // the image up to me_distortion: the result is 4-byte aligned (sizeof 4796),
         // so up to 3 head words, 16-byte stores, up to 3 tail words
@@ -1909,19 +1918,60 @@ __device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb
         }
         if (lane < 2)
             ow[WGM + lane] = lane == 0 ? flags : 0u;
+    }}
+
+__device__ __forceinline__ void finish_sb(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
+    finish_sb_cands(st, dj, sb_local, bw, bh);
+    __syncthreads();
+    HME_SUB(20);
+    finish_sb_out(st, dj, sb_local, bw, bh);
+}
+
+// the records (sb_count x R, slots in list-0-then-list-1 order) by threads [t0, t0 + nt): the
+// LDS record images, 44 16-byte pieces each (704 bytes), the tail words and the SADs of an
+// unsearched slot patched on the way
+__device__ __forceinline__ void write_records(const StC &st, const DevJob &dj, uint32_t sb_local, int t, int nt) {
+    static_assert(sizeof(svtme_ref_record) == 176 * 4, "svtme_ref_record: 176 dwords");
+    svtme_ref_record *out = dj.out_records + (size_t)sb_local * dj.R;
+    const int R = (int)dj.R, nr0 = (int)SF(dj.job, num_refs[0]);
+    for (int i = t; i < R * 44; i += nt) {
+        const int k = i / 44, q = i - 44 * k;
+        const int s = k < nr0 ? k : 4 + (k - nr0);
+        uint4 v     = ((const uint4 *)st.rec[s])[q];
+        if (q < 22 && !st.searched[s]) { // words 0 .. 87: the SADs (< 85) of an unsearched slot
+            if (4 * q + 0 < 85) v.x = U32MAX;
+            if (4 * q + 1 < 85) v.y = U32MAX;
+            if (4 * q + 2 < 85) v.z = U32MAX;
+            if (4 * q + 3 < 85) v.w = U32MAX;
+        }
+        if (q == 42) { // words 168, 169 (MVs), 170, 171: hme_sad
+            v.z = (uint32_t)st.hme_sad[s];
+            v.w = (uint32_t)(st.hme_sad[s] >> 32);
+        } else if (q == 43) { // 172: search centre, 173: zz SAD, 174: flags, 175: 0
+            v.x = (uint32_t)(uint16_t)st.sc_x[s] | ((uint32_t)(uint16_t)st.sc_y[s] << 16);
+            v.y = st.zz[s];
+            v.z = (uint32_t)st.searched[s] | ((uint32_t)st.do_ref[s] << 8) | ((uint32_t)st.tf_exit << 16);
+            v.w = 0;
+        }
+        ((uint4 *)(out + k))[q] = v;
     }
 }
 
 // me_prune_ref, the per-reference records and the candidate arrays /
 // distortions / GM detection of one SB from its searched best SADs and MVs
 // (motion_estimation.c:1522-1565, 2520-3007); all threads of the workgroup
-// SUMS: st.sum8 holds the 8x8 sums of the searched slots (stage_e_body made them)
+// SUMS: st.sum8 holds the 8x8 sums of the searched slots (stage_e_body made them),
+// and the keys (under the svtme_sb_result image) are dead: waves 1-3 zero the image
+// while wave 0 prunes, then waves 0-1 build the candidate arrays while waves 2-3
+// write the records (one barrier less, the records off the critical path)
 template <bool SUMS>
 __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh, uint32_t vmask) {
     const svtme_job &job    = dj.job;
     const svtme_controls &c = job.ctrl;
     const int tid = threadIdx.x, lane = tid & 63;
     const bool w0 = (tid >> 6) == 0;
+    const bool sbr = dj.out_sb != nullptr;
+    uint32_t *img  = (uint32_t *)&st.keys[0][0];
     // ---- me_prune_ref (motion_estimation.c:1522-1565)
     if (SF(job, me_type) != SVTME_ME_MCTF && SF(c, enable_hme_flag) && SF(c, enable_me_hme_ref_pruning) && w0) {
         const int s = lane;
@@ -1955,41 +2005,26 @@ __device__ __forceinline__ void stage_c_tail(StC &st, const DevJob &dj, uint32_t
                 st.do_ref[s] = 0;
         }
     }
+    if (SUMS && sbr && !w0) // the svtme_sb_result image (finish_sb) starts zeroed
+        for (int i = tid - 64; i < (int)(sizeof(svtme_sb_result) + 15) / 16; i += 192)
+            ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     HME_SUB(17);
-
-    // ---- records (sb_count x R, slots in list-0-then-list-1 order): the LDS record
-    // images, 44 16-byte pieces each (704 bytes), the tail words and the SADs of an
-    // unsearched slot patched on the way
-    {
-        static_assert(sizeof(svtme_ref_record) == 176 * 4, "svtme_ref_record: 176 dwords");
-        svtme_ref_record *out = dj.out_records + (size_t)sb_local * dj.R;
-        const int R = (int)dj.R, nr0 = (int)SF(job, num_refs[0]);
-        for (int i = tid; i < R * 44; i += 256) {
-            const int k = i / 44, q = i - 44 * k;
-            const int s = k < nr0 ? k : 4 + (k - nr0);
-            uint4 v     = ((const uint4 *)st.rec[s])[q];
-            if (q < 22 && !st.searched[s]) { // words 0 .. 87: the SADs (< 85) of an unsearched slot
-                if (4 * q + 0 < 85) v.x = U32MAX;
-                if (4 * q + 1 < 85) v.y = U32MAX;
-                if (4 * q + 2 < 85) v.z = U32MAX;
-                if (4 * q + 3 < 85) v.w = U32MAX;
-            }
-            if (q == 42) { // words 168, 169 (MVs), 170, 171: hme_sad
-                v.z = (uint32_t)st.hme_sad[s];
-                v.w = (uint32_t)(st.hme_sad[s] >> 32);
-            } else if (q == 43) { // 172: search centre, 173: zz SAD, 174: flags, 175: 0
-                v.x = (uint32_t)(uint16_t)st.sc_x[s] | ((uint32_t)(uint16_t)st.sc_y[s] << 16);
-                v.y = st.zz[s];
-                v.z = (uint32_t)st.searched[s] | ((uint32_t)st.do_ref[s] << 8) | ((uint32_t)st.tf_exit << 16);
-                v.w = 0;
-            }
-            ((uint4 *)(out + k))[q] = v;
-        }
+    if (SUMS && sbr) {
+        if (tid < 128)
+            finish_sb_cands(st, dj, sb_local, bw, bh);
+        else
+            write_records(st, dj, sb_local, tid - 128, 128);
+        HME_SUB(18);
+        __syncthreads();
+        HME_SUB(20);
+        finish_sb_out(st, dj, sb_local, bw, bh);
+        HME_SUB(21);
+        return;
     }
+    write_records(st, dj, sb_local, tid, 256);
     HME_SUB(18);
-    if (dj.out_sb) { // the svtme_sb_result image (finish_sb) starts zeroed
-        uint32_t *img = (uint32_t *)&st.keys[0][0];
+    if (sbr) {
         for (int i = tid; i < (int)(sizeof(svtme_sb_result) + 15) / 16; i += 256)
             ((uint4 *)img)[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
@@ -4551,7 +4586,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     HME_STOP(55);
     for (int k = wid; k < (int)dj.R; k += 4) {
         constexpr int ROWS = SUB_ME ? 4 : 8, RSTEP = SUB_ME ? 2 : 1;
-        const int z16 = lane >> 2, k4 = lane & 3;
+        // an opaque lane index: the block's address terms are made per record, not hoisted
+        // out of this loop (live across it, they spill at 64 VGPRs)
+        int fl = lane;
+        asm volatile("" : "+v"(fl));
+        const int z16 = fl >> 2, k4 = fl & 3;
         const int by  = ((z16 >> 3) << 2) | (((z16 >> 1) & 1) << 1) | (k4 >> 1);
         const int bx  = (((z16 >> 2) & 1) << 2) | ((z16 & 1) << 1) | (k4 & 1);
         // this lane's 8x8 source block: buffer loads from the SB origin (a 32-bit
