@@ -584,6 +584,8 @@ def main():
                      "); pyramids resident in HBM"),
             "config": {"workload": wl["desc"], "name": name, "sbs_per_picture": n_sb, "refs": R,
                        "pictures_per_step": P,
+                       "job_sets": NS, "resident_pyramids": hi_t - lo_t + 1,
+                       "outputs": "records + svtme_sb_result" if with_sb else "records",
                        "lanes": NL,
                        "parallelism": f"{world} GPU(s): each picture split in {world} equal SB chunks, "
                                       f"rank r searches chunk r of all {P} pictures in {-(-P // LP)} launch(es) per step" +
