@@ -1437,7 +1437,6 @@ struct StC {
     __attribute__((aligned(16))) uint32_t rec[8][176];
     uint8_t cand0[SVTME_PU_COUNT + 3];
     uint32_t gm_cnt[2][4][2][2];
-    uint32_t wm[8]; // magic_u32 of each slot's full-pel width (key decode)
     uint32_t sink;  // finish_sb's stores that have no target
 };
 
@@ -3742,7 +3741,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 // jobs merge into it with atomic min). Wavefront w decodes the records w, w + 4
 // whole (its lanes the 64 8x8 PUs, then 21 the larger ones) and sums the 8x8
 // best SADs of each for me_prune_ref on the way (st.sum8): no serial sums later.
-__device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const DevJob &dj, uint32_t sb_local,
+__device__ __forceinline__ void stage_e_body(StC &st, const DevJob &dj, uint32_t sb_local,
                                              const SbGeo &G, uint32_t vmask, const CSlot *cin,
                                              unsigned long long *kb, bool reset) {
     const svtme_job &job = dj.job;
@@ -3756,23 +3755,24 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
         CSlot v{};
         if (has)
             v = cin[k];
-        csl[s]         = v;
-        st.wm[s]       = has && v.searched ? magic_u32((uint32_t)max(1, (int)v.w)) : 0u;
         st.hme_sad[s]  = has ? v.hme_sad : U32MAX;
         st.zz[s]       = has ? v.zz : U32MAX;
         st.sc_x[s]     = has ? v.sc_x : 0;
         st.sc_y[s]     = has ? v.sc_y : 0;
         st.searched[s] = has ? v.searched : 0;
         st.do_ref[s]   = has ? v.do_ref : 0;
-        st.sum8[s]     = 0;
+        if (!(has && v.searched)) // (a searched slot's sum: its record's decode below)
+            st.sum8[s] = 0;
         if (s == (nr0 > 0 ? 0 : 4)) // record 0's
             st.tf_exit = has ? v.tf_exit : 0;
     }
-    __syncthreads();
+    // the records' decode reads its record's state straight from cin (not the slot
+    // state above): no barrier between the two
     for (int kk = wid; kk < R; kk += 4) {
         const int s      = kk < nr0 ? kk : 4 + (kk - nr0);
-        const bool srch  = st.searched[s] != 0;
-        const CSlot &v   = csl[s];
+        const CSlot &v   = cin[kk];
+        const bool srch  = v.searched != 0;
+        const uint32_t wm = srch ? magic_u32((uint32_t)max(1, (int)v.w)) : 0u;
         auto decode = [&](int pu, uint32_t &sad, uint32_t &mv) {
             sad = U32MAX, mv = 0;
             if (srch) {
@@ -3788,7 +3788,7 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
                     my = v.yc;
                 } else { // p / w by multiply-high (p * w < 2^32)
                     const int p = (int)o - (int)v.probe;
-                    const int q = mdiv(p, st.wm[s]);
+                    const int q = mdiv(p, wm);
                     my          = i16(v.yo + q);
                     mx          = i16(v.xo + (p - q * v.w));
                 }
@@ -3813,12 +3813,11 @@ __device__ __forceinline__ void stage_e_body(StC &st, CSlot (&csl)[8], const Dev
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_stage_e(const DevBatch B) {
     __shared__ StC st;
-    __shared__ CSlot csl[8];
     uint32_t sb_local;
     const DevJob &dj     = batch_job(B, xcd_remap(blockIdx.x, gridDim.x), &sb_local);
     const SbGeo G        = sb_geo(dj, sb_local);
     const uint32_t vmask = valid_mask(dj.job);
-    stage_e_body(st, csl, dj, sb_local, G, vmask, dj.cslot + (size_t)sb_local * dj.R,
+    stage_e_body(st, dj, sb_local, G, vmask, dj.cslot + (size_t)sb_local * dj.R,
                  dj.keys + (size_t)sb_local * dj.R * SVTME_PU_COUNT, dj.parts > 1);
 }
 
@@ -3982,7 +3981,6 @@ struct HmeSh {
     DevJob dj; // the job, copied once: every later job / control read is an LDS read
     BState bs;
     CSlot cin[8]; // by record
-    CSlot csl[8]; // by slot (stage_e_body)
     SlotCentre cen[8]; // final search centre / pruning by slot
     uint8_t tf_exit;
     union U {
@@ -4570,11 +4568,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         HME_STAMP(6);
         return;
     }
-    __syncthreads(); // phase A..B state is dead from here (StC overlays it)
+    // (no barrier: wave 0 alone reads the phase A..B state above and then the BState in
+    // LDS; the other waves write nothing before the barrier after the final centre, from
+    // which StC overlays the A..B state)
     // ---- C: set_final_seach_centre_sb / hme_prune_ref_and_adjust_sr once (wave 0), then
     // integer_search_b64 of every record, one wavefront each (k_stage_c1, one band)
     if (wid == 0) {
         HME_PRIO_HI();
+        wave_lds_fence(); // (the BState other lanes of this wave just wrote)
         const SlotCentre scv = final_centre(gj.job, &sh.bs, vmask); // lane = slot (controls by scalar loads)
         if (lane < 8)
             sh.cen[lane] = scv;
@@ -4617,7 +4618,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     __syncthreads();
     HME_STAMP(6);
     // ---- E: decode, me_prune_ref, records, candidates / distortions / GM detection
-    stage_e_body(sh.u.st, sh.csl, gj, sb_local, G, vmask, sh.cin, &sh.u.st.keys[0][0], false);
+    stage_e_body(sh.u.st, gj, sb_local, G, vmask, sh.cin, &sh.u.st.keys[0][0], false);
     HME_STAMP(7);
 }
 
