@@ -602,8 +602,11 @@ def main():
             "records_only": None if ro_ms is None else {
                 "ms_per_step": round(ro_ms, 4), "value": round(n_sb * P / (ro_ms * 1e-3), 1),
                 "sb_results_cost": round(ms_per_step / ro_ms - 1.0, 4),
-                "note": "the same steps writing the records alone (no svtme_sb_result); `value` writes both, the "
-                        "whole output of svt_aom_motion_estimation_b64 that cpu_baseline times"},
+                "note": "the same steps writing the records alone (no svtme_sb_result), timed after the main "
+                        "window and the overlapped leg, i.e. further into the clock ramp: its ratio to `value` "
+                        "overstates the per-SB results' cost (steady_state.records_only alternates blocks and is "
+                        "the fair comparison; --records-only times them in the main window); `value` writes both, "
+                        "the whole output of svt_aom_motion_estimation_b64 that cpu_baseline times"},
             "steady_state": steady,
             "upload": upload,
             "sb_ref_per_s": round(value * R, 1),
