@@ -17,13 +17,17 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def run_case(S, gpu, kind, w, h, mode, tl, l0, l1, cur=8, gm=False, is_ref=True, e8=None, sb_begin=0, sb_count=0):
+def run_case(S, gpu, kind, w, h, mode, tl, l0, l1, cur=8, gm=False, is_ref=True, e8=None, sb_begin=0, sb_count=0,
+             only_l_bwd=True, ctrl_set=None):
     frames = S.test_frames(kind, w, h, sorted(set([cur] + list(l0) + list(l1))))
     res = S.input_resolution_of(w, h)
     ctrl = S.derive_controls(mode, 35, res, tl)
+    for k, v in (ctrl_set or {}).items():
+        setattr(ctrl, k, v)
     job = S.make_job(w, h, ctrl, cur, l0, l1, temporal_layer_index=tl, is_ref=is_ref,
                      enable_me_8x8=(res <= S.RES_720P) if e8 is None else e8,
-                     ref_count_used=(max(len(l0), 1), len(l1)), gm_enabled=gm, sb_begin=sb_begin, sb_count=sb_count)
+                     ref_count_used=(max(len(l0), 1), len(l1)), gm_enabled=gm, sb_begin=sb_begin, sb_count=sb_count,
+                     only_l_bwd=only_l_bwd)
     for t, f in frames.items():
         gpu.upload(1000 + t, f)
     job.picture_number = 1000 + cur
@@ -41,7 +45,7 @@ def run_case(S, gpu, kind, w, h, mode, tl, l0, l1, cur=8, gm=False, is_ref=True,
     ojob = S.make_job(w, h, ctrl, cur, l0, l1, temporal_layer_index=tl, is_ref=is_ref,
                       enable_me_8x8=(res <= S.RES_720P) if e8 is None else e8,
                       ref_count_used=(max(len(l0), 1), len(l1)), gm_enabled=gm, sb_begin=sb_begin,
-                      sb_count=sb_count)
+                      sb_count=sb_count, only_l_bwd=only_l_bwd)
     orecs, osbr = S.run_checker(ojob, pyr[cur], refs, "oracle", nthreads=8)
     for t in frames:
         gpu.release(1000 + t)
@@ -71,6 +75,28 @@ CASES = [
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-{c[1]}x{c[2]}-p{c[3]}-tl{c[4]}-{len(c[5])}+{len(c[6])}")
 def test_picture_parity(svtme, gpu, case):
     errs = run_case(svtme, gpu, *case)
+    assert not errs, errs[:5]
+
+
+# The per-SB candidate arrays (finish_sb: construct_me_candidate_array*, motion_estimation.c:
+# 2532-2835) off the default path: every bipred pair, L0-L0 and L1-L1 candidates (only_l_bwd 0,
+# 4 + 3 references), the unipred pruning threshold on and off, the best-unipred-only rule of the
+# one-reference-per-list case, and the single-reference case
+SB_CASES = [
+    ("pan", 640, 360, 8, 3, (7, 6, 4, 3), (9, 10, 12), False, None),
+    ("noise", 320, 192, 8, 1, (7, 6), (9, 10), False, None),
+    ("stripes", 320, 192, 8, 1, (7, 6, 5), (9,), False, {"prune_me_candidates_th": 0}),
+    ("pan", 320, 192, 8, 1, (7, 6), (9, 10, 11), False, {"prune_me_candidates_th": 5}),
+    ("noise", 320, 192, 8, 1, (7,), (9,), False, {"use_best_unipred_cand_only": 1}),
+    ("pan", 320, 192, 8, 1, (7,), (9,), True, {"use_best_unipred_cand_only": 0}),
+    ("flat", 320, 192, 8, 1, (7,), (), False, None),
+]
+
+
+@pytest.mark.parametrize("case", SB_CASES, ids=lambda c: f"{c[0]}-{len(c[5])}+{len(c[6])}-lbwd{int(c[7])}-{c[8]}")
+def test_candidate_arrays_parity(svtme, gpu, case):
+    kind, w, h, mode, tl, l0, l1, lbwd, cs = case
+    errs = run_case(svtme, gpu, kind, w, h, mode, tl, l0, l1, gm=True, only_l_bwd=lbwd, ctrl_set=cs)
     assert not errs, errs[:5]
 
 
