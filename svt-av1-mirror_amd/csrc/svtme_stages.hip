@@ -1619,17 +1619,14 @@ __device__ void fullpel(StC &st, const DevPlane &C, uint32_t ox, uint32_t oy) {
         fullpel_run<SUB, false>(st, C, ox, oy);
 }
 
-// Candidate arrays + distortions + GM detection for one SB, all threads
-// (motion_estimation.c:2532-3007). Thread n builds Z-order PU n. The result is
-// assembled in an LDS image laid over st.keys (dead once the keys are decoded
-// into st.rec; stage_c_tail zeroes it beside the record stores). After one
-// barrier, waves 2-3 store the image up to me_distortion in 16-byte pieces while
-// wave 0 (compute_distortion) and wave 1 (GM detection) finish the last words
-// and store them themselves: no zero fill of the HBM copy, no scattered byte
-// stores to HBM, one barrier.
-// finish_sb in two parts, a barrier between: the candidate arrays, me_distortion and the
-// first candidates into the zeroed image (threads < 85), then the stores, distortions and
-// GM detection (waves 2-3, 0, 1)
+// Candidate arrays + distortions + GM detection for one SB (motion_estimation.c:
+// 2532-3007), in two parts with a barrier between. finish_sb_cands: thread n < 85
+// builds Z-order PU n's candidates, MVs and me_distortion in an LDS image laid over
+// st.keys (dead once the keys are decoded into st.rec; stage_c_tail zeroes it).
+// finish_sb_out: waves 2-3 store the image up to me_distortion in 16-byte pieces
+// while wave 0 (compute_distortion) and wave 1 (GM detection) finish the last words
+// and store them themselves: no zero fill of the HBM copy, no scattered byte stores
+// to HBM.
 __device__ __forceinline__ void finish_sb_cands(StC &st, const DevJob &dj, uint32_t sb_local, uint32_t bw, uint32_t bh) {
     static_assert(sizeof(svtme_sb_result) % 4 == 0 && sizeof(svtme_sb_result) <= sizeof(st.keys) &&
                       sizeof(st.keys) % 16 == 0, "svtme_sb_result image over st.keys");
