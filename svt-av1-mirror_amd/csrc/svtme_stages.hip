@@ -3822,7 +3822,6 @@ struct HmeA { // state of phases A0 .. B
     Dec d;
     unsigned long long key[SVTME_A_N]; // search minima by ARes index
     int16_t kxo[SVTME_A_N], kyo[SVTME_A_N];
-    uint32_t zzacc[8];
     uint32_t need;                     // bit slot * 2: pre-HME searched, slot * 2 + 1: HME-L0 searched
     HSrch srch[48];
     int32_t nsrch, nitems;
@@ -4006,8 +4005,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         static_assert(sizeof(DevJob) % 16 == 0 && sizeof(DevJob) / 16 <= 256, "DevJob: one uint4 per thread");
         if (tid < (int)(sizeof(DevJob) / 16))
             ((uint4 *)&sh.dj)[tid] = ((const uint4 *)&gj)[tid];
-        if (tid < 8)
-            sh.u.a.zzacc[tid] = 0;
     }
     __syncthreads();
     const DevJob &dj        = sh.dj;
@@ -4023,84 +4020,67 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
     HME_STAMP(0);
 
     // ---- phase 0 (independent work of all waves):
-    //   wave 0: A1 search table of every search the slots may need (geometry only)
-    //   waves 1-3: zz SADs (init_zz_sad, motion_estimation.c:2382-2437), one slot per
-    //              wave at a time (lane = sub row x half row); the quarter-resolution source
+    //   wave 0: zz SADs of every slot (init_zz_sad, motion_estimation.c:2382-2437), lane = sub
+    //           row x half row, in two batches of four slots, then the zz decisions in the same
+    //           wave (which searches the reference performs): no barrier between the two
+    //   wave 1: A1 search table of every search the slots may need (geometry only)
+    //   waves 2-3: the full- and quarter-resolution source blocks of HME-L2 / HME-L1
     if (wid == 0) {
         dec_init(d);
-        if (lane < SVTME_A_N)
-            sh.u.a.key[lane] = ~0ull;
-        // list-1 pre-HME regions in a second, gated A1 round (a1_mirrored)
-        const bool gate = !RT && c.prehme_enable && c.prehme_l1_early_exit && job.num_lists == 2 &&
-                          c.hme_search_method != SVTME_FULL_SAD_SEARCH && !(dj.paths & SVTME_PATH_NO_A1_GATE);
-        a1_table<RT ? 1 : 0>(sh.u.a, dj, vmask, sox, soy, kh, 0, 0, 0, gate);
-    } else {
+        uint32_t accv = 0; // lane s: slot s's zz sum
         if (zz_on) {
-            // the wave's slots are wid - 1, wid + 2, wid + 5: the current rows are
-            // loaded once and every slot's reference rows are issued before the first
-            // SAD, so the wave waits for one load round trip instead of one per slot
+            // the current rows loaded once; each batch issues its four slots' reference rows
+            // before the first SAD (one load round trip per batch)
             const int r = lane >> 1, h = lane & 1; // sub row r, half row h
             const bool row_in = r < (int)(G.bh >> 1);
             const DevPlane &C = dj.cur.lv[0];
-            u32x4a4 b0{}, b1{}, a[3][2];
-            bool sv[3];
+            u32x4a4 b0{}, b1{};
             if (row_in) {
                 const uint32_t *cr = (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox) + 8 * h;
                 b0 = ldg4(cr), b1 = ldg4(cr + 4);
             }
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const int s = wid - 1 + 3 * j; // wave-uniform slot
-                sv[j]       = s < 8 && slot_valid(vmask, s) && tl_or_l0(job, s >> 2);
-                a[j][0] = a[j][1] = u32x4a4{};
-                if (sv[j] && row_in) {
-                    const DevPlane &F = dj.ref[s >> 2][s & 3].lv[0];
-                    const uint32_t *rr =
-                        (const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * r) * F.stride + G.ox) + 8 * h;
-                    a[j][0] = ldg4(rr), a[j][1] = ldg4(rr + 4);
-                }
-            }
+            for (int bt = 0; bt < 2; bt++) {
+                const uint8_t *fb[4];
+                int fs[4];
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                if (!sv[j])
-                    continue;
-                uint32_t acc = 0;
-                if (row_in) {
-                    acc = __builtin_amdgcn_sad_u8(a[j][0].x, b0.x, acc);
-                    acc = __builtin_amdgcn_sad_u8(a[j][0].y, b0.y, acc);
-                    acc = __builtin_amdgcn_sad_u8(a[j][0].z, b0.z, acc);
-                    acc = __builtin_amdgcn_sad_u8(a[j][0].w, b0.w, acc);
-                    acc = __builtin_amdgcn_sad_u8(a[j][1].x, b1.x, acc);
-                    acc = __builtin_amdgcn_sad_u8(a[j][1].y, b1.y, acc);
-                    acc = __builtin_amdgcn_sad_u8(a[j][1].z, b1.z, acc);
-                    acc = __builtin_amdgcn_sad_u8(a[j][1].w, b1.w, acc);
+                for (int j = 0; j < 4; j++) { // the batch's plane addresses first (one LDS round trip)
+                    fb[j] = dj.ref[bt][j].lv[0].base;
+                    fs[j] = dj.ref[bt][j].lv[0].stride;
                 }
-                acc = wave_sum_u32(acc);
-                if (lane == 0)
-                    sh.u.a.zzacc[wid - 1 + 3 * j] = acc;
+                u32x4a4 a[4][2];
+                bool sv[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int sl = 4 * bt + j; // wave-uniform slot
+                    sv[j]        = slot_valid(vmask, sl) && tl_or_l0(job, bt);
+                    a[j][0] = a[j][1] = u32x4a4{};
+                    if (sv[j] && row_in) {
+                        const uint32_t *rr =
+                            (const uint32_t *)(fb[j] + (ptrdiff_t)(G.oy + 2 * r) * fs[j] + G.ox) + 8 * h;
+                        a[j][0] = ldg4(rr), a[j][1] = ldg4(rr + 4);
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    if (!sv[j])
+                        continue;
+                    uint32_t acc = 0;
+                    if (row_in) {
+                        acc = __builtin_amdgcn_sad_u8(a[j][0].x, b0.x, acc);
+                        acc = __builtin_amdgcn_sad_u8(a[j][0].y, b0.y, acc);
+                        acc = __builtin_amdgcn_sad_u8(a[j][0].z, b0.z, acc);
+                        acc = __builtin_amdgcn_sad_u8(a[j][0].w, b0.w, acc);
+                        acc = __builtin_amdgcn_sad_u8(a[j][1].x, b1.x, acc);
+                        acc = __builtin_amdgcn_sad_u8(a[j][1].y, b1.y, acc);
+                        acc = __builtin_amdgcn_sad_u8(a[j][1].z, b1.z, acc);
+                        acc = __builtin_amdgcn_sad_u8(a[j][1].w, b1.w, acc);
+                    }
+                    const uint32_t t = wave_sum_u32(acc);
+                    accv             = lane == 4 * bt + j ? t : accv;
+                }
             }
         }
-        // full-resolution source block (64 x 64, even rows) for HME-L2
-        if (c.enable_hme_level2_flag && tid >= 96 && tid < 224) {
-            const DevPlane &F = dj.cur.lv[0];
-            const int row = (tid - 96) >> 2, part = tid & 3;
-            const u32x4a4 v = ldg4((const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * row) * F.stride + G.ox + 16 * part));
-            ((uint4 *)sh.u.a.src1[row])[part] = make_uint4(v.x, v.y, v.z, v.w);
-        }
-        // quarter-resolution source block (32 x 32, even rows) for HME-L1
-        if (c.enable_hme_level1_flag && tid >= 224) {
-            const DevPlane &Q = dj.cur.lv[1];
-            const int row = (tid - 224) >> 1, half = tid & 1;
-            const u32x4a4 v = ldg4((const uint32_t *)(Q.base + (ptrdiff_t)((G.oy >> 1) + 2 * row) * Q.stride +
-                                                      (G.ox >> 1) + 16 * half));
-            ((uint4 *)sh.u.a.src4[row])[half] = make_uint4(v.x, v.y, v.z, v.w);
-        }
-    }
-    HME_WAVE(0);
-    __syncthreads();
-    HME_STAMP(1);
-    // ---- zz decisions; which searches the reference performs (wave 0)
-    if (wid == 0) {
         HME_PRIO_HI();
         // dec_zz's decisions (init_zz_sad, motion_estimation.c:2382-2437) with the state in
         // registers, lane = slot: every input read in one batch, cross-lane values by
@@ -4110,7 +4090,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         const uint32_t zpct = c.zz_sad_pct;
         const int tli = job.temporal_layer_index, hl = job.hierarchical_levels, nl = job.num_lists;
         const bool sbr = job.similar_brightness_refs != 0;
-        const uint32_t acc = sh.u.a.zzacc[lane & 7];
+        const uint32_t acc = accv;
         const bool have    = slot_valid(vmask, lane) && tl_or_l0(job, lane >> 2);
         uint32_t zz = U32MAX; // (dec_init's state)
         bool dref   = true;
@@ -4143,10 +4123,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         const unsigned long long m = __ballot(nd);
         if (lane == 0)
             sh.u.a.need = (uint32_t)m;
+        HME_PRIO_LO();
+    } else if (wid == 1) {
+        if (lane < SVTME_A_N)
+            sh.u.a.key[lane] = ~0ull;
+        // list-1 pre-HME regions in a second, gated A1 round (a1_mirrored)
+        const bool gate = !RT && c.prehme_enable && c.prehme_l1_early_exit && job.num_lists == 2 &&
+                          c.hme_search_method != SVTME_FULL_SAD_SEARCH && !(dj.paths & SVTME_PATH_NO_A1_GATE);
+        a1_table<RT ? 1 : 0>(sh.u.a, dj, vmask, sox, soy, kh, 0, 0, 0, gate);
+    } else {
+        // full-resolution source block (64 x 64, even rows) for HME-L2: waves 2-3
+        if (c.enable_hme_level2_flag) {
+            const DevPlane &F = dj.cur.lv[0];
+            const int row = (tid - 128) >> 2, part = tid & 3;
+            const u32x4a4 v = ldg4((const uint32_t *)(F.base + (ptrdiff_t)(G.oy + 2 * row) * F.stride + G.ox + 16 * part));
+            ((uint4 *)sh.u.a.src1[row])[part] = make_uint4(v.x, v.y, v.z, v.w);
+        }
+        // quarter-resolution source block (32 x 32, even rows) for HME-L1: threads 128-159
+        if (c.enable_hme_level1_flag && tid < 160) {
+            const DevPlane &Q = dj.cur.lv[1];
+            const int row = (tid - 128) >> 1, half = tid & 1;
+            const u32x4a4 v = ldg4((const uint32_t *)(Q.base + (ptrdiff_t)((G.oy >> 1) + 2 * row) * Q.stride +
+                                                      (G.ox >> 1) + 16 * half));
+            ((uint4 *)sh.u.a.src4[row])[half] = make_uint4(v.x, v.y, v.z, v.w);
+        }
     }
+    HME_WAVE(0);
     __syncthreads();
-    HME_PRIO_LO();
-    HME_STAMP(2);
+    HME_STAMP(1);
+    HME_STAMP(2); // (the zz decisions are part of phase 0)
     // ---- A1: pre-HME regions and HME-L0 quadrants, one HT16 x HQ tile per thread
     auto a1_tiles = [&]() {
         // source block of the 1/16 searches (16 x 8 sub rows) into SGPRs (live in A1 only)
