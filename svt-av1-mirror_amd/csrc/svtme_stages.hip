@@ -4021,7 +4021,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
 
     // ---- phase 0 (independent work of all waves):
     //   wave 0: zz SADs of every slot (init_zz_sad, motion_estimation.c:2382-2437), lane = sub
-    //           row x half row, in two batches of four slots, then the zz decisions in the same
+    //           row x half row, two batches of loads in flight, then the zz decisions in the same
     //           wave (which searches the reference performs): no barrier between the two
     //   wave 1: A1 search table of every search the slots may need (geometry only)
     //   waves 2-3: the full- and quarter-resolution source blocks of HME-L2 / HME-L1
@@ -4029,8 +4029,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
         dec_init(d);
         uint32_t accv = 0; // lane s: slot s's zz sum
         if (zz_on) {
-            // the current rows loaded once; each batch issues its four slots' reference rows
-            // before the first SAD (one load round trip per batch)
+            // the current rows loaded once
             const int r = lane >> 1, h = lane & 1; // sub row r, half row h
             const bool row_in = r < (int)(G.bh >> 1);
             const DevPlane &C = dj.cur.lv[0];
@@ -4039,47 +4038,51 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HME_WA
                 const uint32_t *cr = (const uint32_t *)(C.base + (ptrdiff_t)(G.oy + 2 * r) * C.stride + G.ox) + 8 * h;
                 b0 = ldg4(cr), b1 = ldg4(cr + 4);
             }
+            // every slot's plane address first, then the slots' reference
+            // rows in three batches (3, 3, 2 slots), each batch's loads issued before the
+            // previous batch's SADs: two batches in flight, not one round trip per batch
+            // (from the job in global memory: scalar loads into SGPRs)
+            const uint8_t *fb[8];
+            int fs[8];
 #pragma unroll
-            for (int bt = 0; bt < 2; bt++) {
-                const uint8_t *fb[4];
-                int fs[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) { // the batch's plane addresses first (one LDS round trip)
-                    fb[j] = dj.ref[bt][j].lv[0].base;
-                    fs[j] = dj.ref[bt][j].lv[0].stride;
-                }
-                u32x4a4 a[4][2];
-                bool sv[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int sl = 4 * bt + j; // wave-uniform slot
-                    sv[j]        = slot_valid(vmask, sl) && tl_or_l0(job, bt);
-                    a[j][0] = a[j][1] = u32x4a4{};
-                    if (sv[j] && row_in) {
-                        const uint32_t *rr =
-                            (const uint32_t *)(fb[j] + (ptrdiff_t)(G.oy + 2 * r) * fs[j] + G.ox) + 8 * h;
-                        a[j][0] = ldg4(rr), a[j][1] = ldg4(rr + 4);
-                    }
-                }
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    if (!sv[j])
-                        continue;
-                    uint32_t acc = 0;
-                    if (row_in) {
-                        acc = __builtin_amdgcn_sad_u8(a[j][0].x, b0.x, acc);
-                        acc = __builtin_amdgcn_sad_u8(a[j][0].y, b0.y, acc);
-                        acc = __builtin_amdgcn_sad_u8(a[j][0].z, b0.z, acc);
-                        acc = __builtin_amdgcn_sad_u8(a[j][0].w, b0.w, acc);
-                        acc = __builtin_amdgcn_sad_u8(a[j][1].x, b1.x, acc);
-                        acc = __builtin_amdgcn_sad_u8(a[j][1].y, b1.y, acc);
-                        acc = __builtin_amdgcn_sad_u8(a[j][1].z, b1.z, acc);
-                        acc = __builtin_amdgcn_sad_u8(a[j][1].w, b1.w, acc);
-                    }
-                    const uint32_t t = wave_sum_u32(acc);
-                    accv             = lane == 4 * bt + j ? t : accv;
-                }
+            for (int sl = 0; sl < 8; sl++) {
+                fb[sl] = gj.ref[sl >> 2][sl & 3].lv[0].base;
+                fs[sl] = gj.ref[sl >> 2][sl & 3].lv[0].stride;
             }
+            u32x4a4 a[8][2];
+            bool sv[8];
+            auto issue = [&](int sl) {
+                sv[sl]    = slot_valid(vmask, sl) && tl_or_l0(job, sl >> 2);
+                a[sl][0] = a[sl][1] = u32x4a4{};
+                if (sv[sl] && row_in) {
+                    const uint32_t *rr =
+                        (const uint32_t *)(fb[sl] + (ptrdiff_t)(G.oy + 2 * r) * fs[sl] + G.ox) + 8 * h;
+                    a[sl][0] = ldg4(rr), a[sl][1] = ldg4(rr + 4);
+                }
+            };
+            auto sum = [&](int sl) {
+                if (!sv[sl])
+                    return;
+                uint32_t acc = 0;
+                if (row_in) {
+                    acc = __builtin_amdgcn_sad_u8(a[sl][0].x, b0.x, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[sl][0].y, b0.y, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[sl][0].z, b0.z, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[sl][0].w, b0.w, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[sl][1].x, b1.x, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[sl][1].y, b1.y, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[sl][1].z, b1.z, acc);
+                    acc = __builtin_amdgcn_sad_u8(a[sl][1].w, b1.w, acc);
+                }
+                const uint32_t t = wave_sum_u32(acc);
+                accv             = lane == sl ? t : accv;
+            };
+            issue(0), issue(1), issue(2);
+            issue(3), issue(4), issue(5);
+            sum(0), sum(1), sum(2);
+            issue(6), issue(7);
+            sum(3), sum(4), sum(5);
+            sum(6), sum(7);
         }
         HME_PRIO_HI();
         // dec_zz's decisions (init_zz_sad, motion_estimation.c:2382-2437) with the state in
