@@ -2975,7 +2975,7 @@ __device__ __forceinline__ uint32_t fpw_min_hr(uint32_t v) {
 // each block, then the 16x16 / 32x32 / 64x64 sums and keys into the set minima.
 // T / T2 (top), Bq / B2 (bottom): the qsad accumulators of quads a and b.
 // MASK: positions >= ev are outside the area (the last, partial pair).
-template <bool MASK>
+template <bool MASK, bool K8 = true>
 __device__ __forceinline__ void fpw_pair(FpW &m, unsigned long long T, unsigned long long T2, unsigned long long Bq,
                                          unsigned long long B2, int e0, int ev, uint32_t sel16, uint32_t sel32,
                                          int p16, int p32) {
@@ -2985,14 +2985,16 @@ __device__ __forceinline__ void fpw_pair(FpW &m, unsigned long long T, unsigned 
         const uint32_t k = (e & 1) ? ((v & 0xFFFF0000u) | (uint32_t)e) : ((v << 16) | (uint32_t)e);
         return (MASK && e >= ev) ? 0xFFFFFFFFu : k;
     };
-    m.b8t = min_u32(min_u32(m.b8t, k8(tl, e0)), k8(tl, e0 + 1));
-    m.b8t = min_u32(min_u32(m.b8t, k8(th, e0 + 2)), k8(th, e0 + 3));
-    m.b8t = min_u32(min_u32(m.b8t, k8(tl2, e0 + 4)), k8(tl2, e0 + 5));
-    m.b8t = min_u32(min_u32(m.b8t, k8(th2, e0 + 6)), k8(th2, e0 + 7));
-    m.b8b = min_u32(min_u32(m.b8b, k8(bl, e0)), k8(bl, e0 + 1));
-    m.b8b = min_u32(min_u32(m.b8b, k8(bh, e0 + 2)), k8(bh, e0 + 3));
-    m.b8b = min_u32(min_u32(m.b8b, k8(bl2, e0 + 4)), k8(bl2, e0 + 5));
-    m.b8b = min_u32(min_u32(m.b8b, k8(bh2, e0 + 6)), k8(bh2, e0 + 7));
+    if constexpr (K8) {
+        m.b8t = min_u32(min_u32(m.b8t, k8(tl, e0)), k8(tl, e0 + 1));
+        m.b8t = min_u32(min_u32(m.b8t, k8(th, e0 + 2)), k8(th, e0 + 3));
+        m.b8t = min_u32(min_u32(m.b8t, k8(tl2, e0 + 4)), k8(tl2, e0 + 5));
+        m.b8t = min_u32(min_u32(m.b8t, k8(th2, e0 + 6)), k8(th2, e0 + 7));
+        m.b8b = min_u32(min_u32(m.b8b, k8(bl, e0)), k8(bl, e0 + 1));
+        m.b8b = min_u32(min_u32(m.b8b, k8(bh, e0 + 2)), k8(bh, e0 + 3));
+        m.b8b = min_u32(min_u32(m.b8b, k8(bl2, e0 + 4)), k8(bl2, e0 + 5));
+        m.b8b = min_u32(min_u32(m.b8b, k8(bh2, e0 + 6)), k8(bh2, e0 + 7));
+    }
     // 8x16 columns, then 16x16 over bx ^ 1 (packed: both halves stay below 2^15)
     const uint32_t sl = dpp_add<0xB1>(tl + bl), sh = dpp_add<0xB1>(th + bh);
     const uint32_t sl2 = dpp_add<0xB1>(tl2 + bl2), sh2 = dpp_add<0xB1>(th2 + bh2);
@@ -3019,6 +3021,12 @@ __device__ __forceinline__ void fpw_pair(FpW &m, unsigned long long T, unsigned 
     const uint32_t s64  = sw2[0] + sw2[1];
     const uint32_t k64  = (s64 << 12) | (uint32_t)e0;
     m.b64               = min_u32(m.b64, (MASK && e0 + p32 >= ev) ? 0xFFFFFFFFu : k64);
+}
+
+// packed minimum of two u16 pairs (v_pk_min_u16)
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a), __builtin_bit_cast(u16x2, b)));
 }
 
 // set-local minima (orders within the set) into the running minima (raster order)
@@ -3241,6 +3249,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
     const int p16 = bx & 1, p32 = c32 + 4 * (by2 & 1);
     const int L   = 2 * bx;
     const int nwhole = w / (4 * FPW_TQ); // sets with all 16 positions inside the area
+    // 8x8 classes in two passes: per set only each block's packed SAD minimum (v_pk_min_u16
+    // over the set's 16 positions) and the first set, in scan order, that lowered it; after
+    // the loop the position inside that set (one more set of SADs per block). Scan order is
+    // raster order and the pass keeps the earliest set, so the reference's tie-break holds
+    uint32_t r8t = 0xFFFFu, r8b = 0xFFFFu, rc8t = 0, rc8b = 0;
     for (int ty = y0; ty < y1; ty += 2) {
         const int tyh = min(ty + hr, y1 - 1); // an odd band: half 1 repeats the last row (same keys)
         // one set of 16 positions into the set minima m (orders EOFF + position in the
@@ -3280,11 +3293,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
 #pragma unroll
                 for (int iq = 0; iq < FPW_TQ; iq++) asm volatile("" : "+v"(acc[blk][iq]));
             const int left = w - 4 * tq; // positions of the area in this set (wave-uniform)
+            {
+                auto pmin = [&](int blk) -> uint32_t {
+                    uint32_t p = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int iq = 0; iq < FPW_TQ; iq++) {
+                        uint32_t lo = (uint32_t)acc[blk][iq], hi = (uint32_t)(acc[blk][iq] >> 32);
+                        if constexpr (!decltype(WHOLE)::value) { // positions outside the area
+                            lo |= (4 * iq >= left ? 0xFFFFu : 0u) | (4 * iq + 1 >= left ? 0xFFFF0000u : 0u);
+                            hi |= (4 * iq + 2 >= left ? 0xFFFFu : 0u) | (4 * iq + 3 >= left ? 0xFFFF0000u : 0u);
+                        }
+                        p = pk_min_u16(p, pk_min_u16(lo, hi));
+                    }
+                    return min_u32(p & 0xFFFFu, p >> 16);
+                };
+                const uint32_t code = ((uint32_t)tyh << 8) | (uint32_t)set;
+                const uint32_t st = pmin(0), sb = pmin(1);
+                rc8t = st < r8t ? code : rc8t;
+                r8t  = min_u32(r8t, st);
+                rc8b = sb < r8b ? code : rc8b;
+                r8b  = min_u32(r8b, sb);
+            }
             if constexpr (decltype(WHOLE)::value) {
 #pragma unroll
                 for (int pp = 0; pp < FPW_TQ / 2; pp++)
-                    fpw_pair<false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
-                                    decltype(EOFF)::value + 8 * pp, 8, sel16, sel32, p16, p32);
+                    fpw_pair<false, false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
+                                           decltype(EOFF)::value + 8 * pp, 8, sel16, sel32, p16, p32);
             } else {
 #pragma unroll
                 for (int pp = 0; pp < FPW_TQ / 2; pp++) {
@@ -3292,11 +3326,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
                     if (ev <= 0)
                         break;
                     if (ev >= 8)
-                        fpw_pair<false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
-                                        8 * pp, 8, sel16, sel32, p16, p32);
+                        fpw_pair<false, false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
+                                               8 * pp, 8, sel16, sel32, p16, p32);
                     else
-                        fpw_pair<true>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
-                                       8 * pp, ev + 8 * pp, sel16, sel32, p16, p32);
+                        fpw_pair<true, false>(m, acc[0][2 * pp], acc[0][2 * pp + 1], acc[1][2 * pp], acc[1][2 * pp + 1],
+                                              8 * pp, ev + 8 * pp, sel16, sel32, p16, p32);
                 }
             }
         };
@@ -3304,14 +3338,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
         auto fold = [&](const FpW &m, const int tq, const bool keyed) {
             const uint32_t ob = obase + (uint32_t)(tyh * w + 4 * tq);
             if (keyed) { // a whole first pair: every class of every lane has a key
-                b.b8t = min_u32(b.b8t, m.b8t + ob);
-                b.b8b = min_u32(b.b8b, m.b8b + ob);
                 b.b16 = min_u32(b.b16, m.b16 + ob + (uint32_t)p16);
                 b.b32 = min_u32(b.b32, m.b32 + ob + (uint32_t)p32);
                 b.b64 = min_u32(b.b64, m.b64 + ob + (uint32_t)p32);
             } else {
-                b.b8t = fpw_rebase(b.b8t, m.b8t, ob);
-                b.b8b = fpw_rebase(b.b8b, m.b8b, ob);
                 b.b16 = fpw_rebase(b.b16, m.b16, ob + (uint32_t)p16);
                 b.b32 = fpw_rebase(b.b32, m.b32, ob + (uint32_t)p32);
                 b.b64 = fpw_rebase(b.b64, m.b64, ob + (uint32_t)p32);
@@ -3337,6 +3367,47 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(FPW_WA
             fold(m, nwhole * FPW_TQ, w - 4 * nwhole * FPW_TQ >= 8);
         }
     }
+    // 8x8 pass 2: the block's SADs in its recorded set again, the lowest position at the minimum
+    auto find8 = [&](auto BLK, const uint32_t rmin, const uint32_t rc, uint32_t &best) {
+        constexpr int blk = decltype(BLK)::value;
+        if (rmin == 0xFFFFu)
+            return; // no position searched
+        const int tyr = (int)(rc >> 8), tq = (int)(rc & 0xFFu) * FPW_TQ;
+        const uint32_t lb = fw_lds + 4u * (uint32_t)((tyr - Y0 + 2 * by2 * 8) * FPW_PITCH + L + tq);
+        unsigned long long acc[FPW_TQ];
+#pragma unroll
+        for (int iq = 0; iq < FPW_TQ; iq++) acc[iq] = 0;
+        FpwRow R[2];
+        fpw_row_issue<blk * ROWS>(R[0], lb);
+        fpw_sfor<0, ROWS>([&](auto RR) {
+            constexpr int rr = decltype(RR)::value, g = blk * ROWS + rr;
+            if constexpr (rr + 1 < ROWS) {
+                fpw_row_issue<g + 1>(R[(rr + 1) & 1], lb);
+                fpw_row_wait<5>(R[rr & 1]);
+            } else {
+                fpw_row_wait<0>(R[rr & 1]);
+            }
+            const FpwRow &q = R[rr & 1];
+#pragma unroll
+            for (int iq = 0; iq < FPW_TQ; iq++) {
+                acc[iq] = qsad(q.v[iq].x, q.v[iq].y, src[blk][rr][0], acc[iq]);
+                acc[iq] = qsad(q.v[iq + 1].x, q.v[iq + 1].y, src[blk][rr][1], acc[iq]);
+            }
+        });
+        const int left = w - tq * 4;
+        uint32_t k = 0xFFFFFFFFu;
+#pragma unroll
+        for (int iq = 0; iq < FPW_TQ; iq++)
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int e      = 4 * iq + j;
+                const uint32_t v = (uint32_t)(acc[iq] >> (16 * j)) & 0xFFFFu;
+                k                = min_u32(k, e >= left ? 0xFFFFFFFFu : (v << 16) | (uint32_t)e);
+            }
+        best = min_u32(best, k + obase + (uint32_t)(tyr * w + 4 * tq));
+    };
+    find8(std::integral_constant<int, 0>(), r8t, rc8t, b.b8t);
+    find8(std::integral_constant<int, 1>(), r8b, rc8b, b.b8b);
     // both halves, then the lanes of each class
     b.b8t = fpw_min_hr(b.b8t), b.b8b = fpw_min_hr(b.b8b), b.b16 = fpw_min_hr(b.b16);
     b.b32 = fpw_min_hr(b.b32), b.b64 = fpw_min_hr(b.b64);
