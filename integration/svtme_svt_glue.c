@@ -689,6 +689,10 @@ static struct {
     void *rtcd0[GLUE_RTCD_N]; /* the rtcd pointers at the first SB call (after svt_aom_setup_rtcd_internal) */
     uint32_t inflight;        /* jobs between their submission and their output in host memory */
     double busy_t0;
+    /* the last GLUE_CHG_LOG pictures svtme_picture_changed saw (G.mu): a prefetched job is
+     * unlisted while it is submitted, so its relink checks the changes made meanwhile */
+#define GLUE_CHG_LOG 64
+    uint64_t chg_pn[GLUE_CHG_LOG], chg_seq;
     struct {
         unsigned long long pa_jobs, tf_jobs, sbs, fallback_sbs, uploads, invalidations, evictions, verified, stale;
         unsigned long long job_sbs, max_inflight, unpinned, eager_uploads, verified_job, registrations;
@@ -1138,6 +1142,16 @@ static int job_names(const svtme_job *job, uint64_t pn) {
                 return 1;
     return 0;
 }
+/* a picture the job reads changed after change number gen (G.mu held; every change if
+ * the log wrapped) */
+static int changed_since(const svtme_job *job, uint64_t gen) {
+    if (G.chg_seq - gen > GLUE_CHG_LOG)
+        return 1;
+    for (uint64_t q = gen; q < G.chg_seq; q++)
+        if (job_names(job, G.chg_pn[q % GLUE_CHG_LOG]))
+            return 1;
+    return 0;
+}
 
 static void job_free(GlueJob *j) { /* G.mu held, j already unlinked */
     if (j->served == 0 && j->state == 1)
@@ -1246,6 +1260,7 @@ void svtme_picture_changed(PictureParentControlSet *pcs, const EbPictureBufferDe
     }
     pthread_mutex_unlock(&G.gpu);
     pthread_mutex_lock(&G.mu);
+    G.chg_pn[G.chg_seq++ % GLUE_CHG_LOG] = pn;
     for (GlueJob *j = G.jobs, *nx; j; j = nx) {
         nx = j->next;
         if (j->stale || !job_names(&j->job, pn))
@@ -1445,6 +1460,7 @@ void svtme_glue_prefetch_pa(PictureParentControlSet *pcs) {
     }
     GlueJob *j = job_new(pcs, &job, 0);
     job_unlink(j); /* listed once it is submitted */
+    const uint64_t gen = G.chg_seq;
     const int rc0 = buf_take(j, (size_t)j->n_sb * j->stride, buf_worst(j->n_sb));
     pthread_mutex_unlock(&G.mu);
     uint64_t ticket = 0;
@@ -1466,7 +1482,9 @@ void svtme_glue_prefetch_pa(PictureParentControlSet *pcs) {
         G.n.launches++;
         j->next = G.jobs;
         G.jobs  = j;
-        if (job_find(&job) != j) /* (an SB call started the same job meanwhile: this one goes) */
+        /* (an SB call started the same job meanwhile, or a picture it reads changed
+         * while it was unlisted: this one goes) */
+        if (job_find(&job) != j || changed_since(&job, gen))
             j->stale = 1, settle_prefetched(pick_stale, 0);
     }
     pthread_mutex_unlock(&G.mu);
@@ -1514,6 +1532,7 @@ void svtme_glue_prefetch_tf(PictureParentControlSet *centre) {
     const EbPaReferenceObject *objs[SVTME_MAX_BATCH_JOBS];
     int n = 0;
     pthread_mutex_lock(&G.mu);
+    const uint64_t gen = G.chg_seq;
     for (int k = 0; k < np; k++) {
         if (job_find(&pairs[k])) /* (already running) */
             continue;
@@ -1560,7 +1579,7 @@ void svtme_glue_prefetch_tf(PictureParentControlSet *centre) {
         G.n.tf_batched += k > 0;
         j->next = G.jobs;
         G.jobs  = j;
-        if (job_find(&j->job) != j)
+        if (job_find(&j->job) != j || changed_since(&j->job, gen))
             j->stale = 1;
     }
     settle_prefetched(pick_stale, 0);
