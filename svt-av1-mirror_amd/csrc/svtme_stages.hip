@@ -2955,8 +2955,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SUB ? 
 // the position within the set (inline constants), the set's raster order is
 // added once per set.
 // ============================================================================
-#define FPW_PITCH 80 // dwords per LDS row (fw_a then fw_b): 320 bytes = 64 (mod 128), so the two
-                     // search rows of a 16-lane read group (hr = 0, 1) fall on disjoint bank halves
+#define FPW_PITCH 80 // dwords per LDS row (fw_a then fw_b): the two search rows (hr = 0, 1) of one by2
+                     // fall on banks 0-15 / 16-31; the other by2 of a 32-lane ds_read_b64 group reads
+                     // rows 16 further (16 x 80 = 0 mod 64 banks): a 2-way conflict
 #define FPW_BOFF 40  // fw_b within the row: one base address serves both copies
 #define FPW_ROWS 96  // window rows per workgroup (4 bands + 62; the host bounds the band height)
 #define FPW_TQ 4 // position quads per set (2 quad pairs, 16 positions; 6 wastes a third of the
