@@ -1103,8 +1103,10 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
     uint64_t span;
     const uint8_t *y = span_of(full, w, h, &span);
     const double t0  = now_s();
+    double t_pin     = t0;
     if (G.pin) { /* SVTME_GLUE_PIN=1: page-lock the encoder's buffer, one DMA straight from it */
         pin_span(y, span, (int)(pn >> GLUE_NS_SHIFT)); /* (locked already when the caller pinned it first) */
+        t_pin = now_s();
         if (svtme_picture_upload_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
             return -1;
     } else if (svtme_picture_upload_copy_async(G.ctx, pn, y, full->stride_y, w, h) != SVTME_OK)
@@ -1112,7 +1114,7 @@ static int pic_ensure(uint64_t pn, const EbPictureBufferDesc *full, const EbPict
     const double t1 = now_s();
     G.n.upload_s += t1 - t0;
     if (G.trace_path) { /* uploads in the trace too (tf = 2), to place them beside the jobs */
-        const GlueTrace t = {pn & GLUE_PN_MASK, 2, 0, 0, 1, t0, t1, t1, t1 - t0, 0, 0};
+        const GlueTrace t = {pn & GLUE_PN_MASK, 2, 0, 0, 1, t0, t1, t1, t1 - t0, 0, 0, t_pin, t1}; /* prep: pinned */
         pthread_mutex_lock(&G.mu);
         trace_add(&t);
         pthread_mutex_unlock(&G.mu);

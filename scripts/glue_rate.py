@@ -41,7 +41,8 @@ def main():
         w, h, frames, preset = E.CASES[case][:4]
         r = {"case": case, "size": f"{w}x{h}", "frames": frames, "preset": preset,
              "identical": got["md5"] == ref["md5"], "md5": got["md5"], "ref_seconds": ref["seconds"],
-             "gpu_encoder_seconds": got["seconds"], **g, "jobs": jobs, "uploads_trace": ups,
+             "gpu_encoder_seconds": got["seconds"], **g, "svtme_log": got.get("svtme_log", []),
+             "jobs": jobs, "uploads_trace": ups,
              "registrations_trace": regs}
         lat = sorted(j["done_ms"] - j["create_ms"] for j in jobs)
         # jobs above 1 ms and the uploads that overlapped them (a stall's candidates)

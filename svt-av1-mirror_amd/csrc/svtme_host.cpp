@@ -645,7 +645,12 @@ extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, co
                                                    uint32_t w, uint32_t h) {
     if (!c || !y || w == 0 || h == 0 || stride < w)
         return fail(SVTME_ERR_BAD_PARAMETER, "svtme_picture_upload_async: bad arguments");
+    // SVTME_SLOW_UPLOAD_MS=t: a call over t ms prints where its time went (stderr)
+    static const double slow_ms = getenv("SVTME_SLOW_UPLOAD_MS") ? atof(getenv("SVTME_SLOW_UPLOAD_MS")) : 0.0;
+    using clk     = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     std::lock_guard<std::mutex> lk(c->mu);
+    const auto t1 = clk::now();
     HIP_TRY(hipSetDevice(c->device));
     {
         const svtme_status us = ensure_ustream(c);
@@ -655,10 +660,29 @@ extern "C" svtme_status svtme_picture_upload_async(svtme_ctx *c, uint64_t pn, co
     const bool resident = c->pics.count(pn) != 0;
     PicBuf *pb;
     svtme_status st;
+    const size_t nfree = c->freebufs.size();
     if ((st = alloc_pic(c, pn, svtme_align8_u(w), svtme_align8_u(h), &pb)))
         return st;
+    const auto t2 = clk::now();
     if (resident && (st = after_readers(c, *pb, c->ustream))) // queued jobs may still read the old planes
         return st;
+    struct SlowLog {
+        double lim;
+        std::chrono::steady_clock::time_point t0, t1, t2;
+        uint64_t pn;
+        size_t nfree;
+        bool resident;
+        ~SlowLog() {
+            if (lim <= 0.0)
+                return;
+            const auto t3 = std::chrono::steady_clock::now();
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            if (ms(t0, t3) > lim)
+                fprintf(stderr, "[svtme] slow upload pn %llu: %.3f ms (lock %.3f, alloc %.3f, rest %.3f; free bufs %zu, %s)\n",
+                        (unsigned long long)pn, ms(t0, t3), ms(t0, t1), ms(t1, t2), ms(t2, t3), nfree,
+                        resident ? "resident" : "new");
+        }
+    } slow_log{slow_ms, t0, t1, t2, pn, nfree, resident};
     if (!pb->ready)
         HIP_TRY(hipEventCreateWithFlags(&pb->ready, hipEventDisableTiming));
     // a page-locked plane the device can read: the pyramid build reads it over PCIe

@@ -138,6 +138,8 @@ def encode(kind: str, case: str, workdir: str, env_extra=None, timeout: int = 60
     if kind != "ref":
         with open(stats) as f:
             res["glue"] = json.loads(f.read().strip().splitlines()[-1])
+        # the library's diagnostics (e.g. SVTME_SLOW_UPLOAD_MS lines)
+        res["svtme_log"] = [ln for ln in r.stderr.splitlines() if ln.startswith("[svtme]")]
     return res
 
 
